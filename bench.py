@@ -1,0 +1,224 @@
+"""Benchmark: log_prob throughput of the gfx950 flow-transform hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One step = one log_prob pass over the per-GPU batch: every flow layer's fused kernel
+(conditioner MLP on fp32 MFMA + transform + log-det accumulate), the fused Gaussian base term
+with the float64 NLL partial sum, and (N > 1) ONE RCCL all-reduce of the 16-byte partial
+[sum log p, count] — the whole data-parallel exchange of the path.
+Weak scaling: each rank owns a fixed 1M-sample shard (configs[1] of BASELINE.json at N=1).
+
+Rank 0 prints ONE JSON line with the throughput, the roofline of the dominant kernel (HIP
+events on the launch stream, over the timed steps) and, at N=1, the oracle CPU baseline timed on
+this host on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "normalizing-flows-study_amd"))
+sys.path.insert(0, ROOT)
+
+import nfs_amd  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
+METRIC = "log_prob samples/sec/GPU + test-NLL match; RealNVP d=2 and MAF d=63"
+
+
+def perturb(model, sigma, seed):
+    """Same recipe as tests/golden/make_golden.py: no layer is the identity, BN stats non-trivial."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for _, p in model.named_parameters():
+            p.add_(sigma * torch.randn(p.shape, generator=g))
+        for _, mod in model.named_modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.copy_(0.1 * torch.randn(mod.running_mean.shape, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(mod.running_var.shape, generator=g))
+
+
+def build(config):
+    """(model, d, flops_per_sample_per_layer, oracle spec, description)."""
+    if config == "cfg2":
+        torch.manual_seed(0)
+        m = nfs_amd.RealNVP(2, 8, 64)
+        perturb(m, 0.1, 1)
+        H, d = 64, 2
+        # 2 nets x 2 flop x (n_c*H + H*H + H*n_t), n_c = n_t = 1
+        f = 2 * 2 * (1 * H + H * H + H * 1)
+        import oracle
+        return m, d, f, oracle.realnvp_spec(8), "cfg2 RealNVP(data_dim=2, n_layers=8, hidden_dim=64) log_prob, eval"
+    if config == "cfg3":
+        torch.manual_seed(10)
+        layers = []
+        for i in range(8):
+            mask = torch.zeros(2)
+            if i % 2 == 0:
+                mask[:1] = 1
+            else:
+                mask[1:] = 1
+            layers.append(nfs_amd.SplineCouplingLayer(2, 64, mask, num_bins=8))
+        m = nfs_amd.NormalizingFlowModel(layers)
+        perturb(m, 0.1, 11)
+        H, K = 64, 8
+        f = 2 * (1 * H + H * H + H * (3 * K - 1))
+        import oracle
+        return m, 2, f, [("spline", f"flows.{i}.", {"K": 8}) for i in range(8)], \
+            "cfg3 8x SplineCouplingLayer(2, 64, K=8) log_prob, eval"
+    if config == "cfg4":
+        torch.manual_seed(30)
+        m = nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(63, 64) for _ in range(5)])
+        perturb(m, 0.02, 31)
+        d, H = 63, 64
+        f = 2 * (d * H + 2 * H * H + 2 * d * H)
+        import oracle
+        return m, d, f, oracle.maf_spec(5), "cfg4 5x MaskedAutoregressiveFlow(63, 64) log_prob, eval"
+    raise ValueError(config)
+
+
+def cpu_baseline(model, spec, x_gpu, budget_s=12.0):
+    """The oracle (op-for-op CPU restatement of the reference) timed on this host."""
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    n = min(x_gpu.shape[0], 262144)
+    x = x_gpu[:n].float().cpu()
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    times = []
+    with torch.no_grad():
+        z, ld = oracle.flow_model(sd, spec, x, -1)  # warm-up
+        lp = oracle.gauss_log_prob(z, ld)
+        t_end = time.perf_counter() + budget_s
+        while len(times) < 5 and (time.perf_counter() < t_end or len(times) < 2):
+            t0 = time.perf_counter()
+            z, ld = oracle.flow_model(sd, spec, x, -1)
+            oracle.gauss_log_prob(z, ld)
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} rows of the same seeded batch, log_prob via oracle/flows_ref.py "
+                      f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}, \
+        oracle.nll_f64(lp), x
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4"])
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default 1M; 500k for cfg4)")
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    model, d, f_layer, spec, desc = build(a.config)
+    model = model.to(dev).eval()
+    B = a.batch or (500_000 if a.config == "cfg4" else 1_000_000)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.randn(B, d, device=dev, generator=g)
+    flow = model.flow if hasattr(model, "flow") else model
+
+    def step():
+        logp, sums = flow.log_prob(x, return_sums=True)
+        if world > 1:
+            dist.all_reduce(sums)  # RCCL over xGMI: 16 bytes
+        return sums
+
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        nfs_amd.reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            sums = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter() - t0
+        # Kernel durations: the same K steps again with HIP events around every layer launch
+        # on the launch stream. Kept out of the headline loop because each event record adds
+        # ~5 us of GPU idle between kernels (measured, profiles/).
+        flow.layer_events = []
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        events = flow.layer_events
+        flow.layer_events = None
+    if nfs_amd.STATS["torch"] != 0 or nfs_amd.STATS["hip"] == 0:
+        raise RuntimeError(f"hot path did not run on the HIP kernels: {nfs_amd.STATS}")
+    t_all = torch.tensor([t], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
+    t_max = float(t_all.item())
+
+    # dominant kernel: the per-layer fused kernel (every launch of the timed steps)
+    durs = [e0.elapsed_time(e1) for _, e0, e1 in events]
+    kname = events[0][0] if events else "?"
+    mean_ms = sum(durs) / max(1, len(durs))
+    achieved = f_layer * B / (mean_ms * 1e-3) / 1e12
+    nll = -float(sums[0] / sums[1])
+
+    result = None
+    if rank == 0:
+        traffic = None
+        tp = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
+        if os.path.exists(tp):
+            with open(tp) as fh:
+                traffic = json.load(fh).get("hbm_bytes_per_launch")
+        result = {
+            "metric": METRIC,
+            "value": world * B * a.steps / t_max,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * t_max / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: x ~ N(0,1) generated on device (seed 1234+rank); seeded random-init "
+                    "weights perturbed N(0, 0.1^2) with non-trivial BatchNorm running stats",
+            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": world * B,
+                       "parallelism": f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"},
+            "nll_f64": nll,
+            "roofline": {"bound": "mfma", "kernel": kname, "achieved": achieved,
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
+                         "traffic": traffic, "flop_per_sample_per_launch": f_layer,
+                         "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu:
+            cb, cpu_nll, xs = cpu_baseline(model, spec, x)
+            gpu_nll = flow.nll(xs.to(dev))
+            cb["nll_abs_diff_vs_gpu"] = abs(cpu_nll - gpu_nll)
+            result["cpu_baseline"] = cb
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * nfx.h — C-ABI of libnfx.so, the MI355X (gfx950) flow-transform hot path.
+ *
+ * The reference (itxtx/normalizing-flows-study) has no native boundary: its hot path is the
+ * Python `Flow` contract `forward(z) -> (x, log_det)` / `inverse(x) -> (z, log_det)`
+ * (src/flows/flow/flow.py:12-38). Each entry point below replaces the ATen op chain of one
+ * reference layer method; the Python mirror in normalizing-flows-study_amd/nfs_amd binds them
+ * with ctypes (INTEGRATION.md shows the same stub for the reference tree).
+ *
+ * Conventions (all entry points):
+ *   - Every tensor pointer is a DEVICE pointer owned by the caller (PyTorch allocator).
+ *     The library allocates nothing persistent and frees nothing.
+ *   - Tensors are fp32, row-major and contiguous: x/z `[B, d]`, log_det `[B]`.
+ *   - `stream` is a hipStream_t (0 = null stream). Every call is stream-ordered and
+ *     asynchronous; no call synchronises the device, so calls can be captured in a hipGraph.
+ *   - Return 0 on success; < 0 on error, with a message in nfx_last_error() (thread-local).
+ *     NFX_EINVAL invalid argument, NFX_EUNSUPPORTED shape outside the compiled kernel
+ *     family, NFX_ELAUNCH a HIP launch error.
+ *   - `accumulate` = 0 stores the layer's log|det J| into log_det; 1 adds it in place
+ *     (log_det[i] += ld_i), reproducing the sequential float32 accumulation of
+ *     NormalizingFlowModel.forward/inverse (src/models/normalizing_flow_model.py:30-65).
+ *   - `direction` = NFX_FORWARD (+1, Flow.forward, z -> x) or NFX_INVERSE (-1, Flow.inverse).
+ *   - Numerical guards of the reference (NaN/Inf replacement, clamps) are part of the contract
+ *     and reproduced exactly.
+ */
+#ifndef NFX_H
+#define NFX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NFX_ABI_VERSION 1
+
+#define NFX_OK 0
+#define NFX_EINVAL (-1)
+#define NFX_EUNSUPPORTED (-2)
+#define NFX_ELAUNCH (-3)
+
+#define NFX_FORWARD 1
+#define NFX_INVERSE (-1)
+
+/* MADE-affine variants (nfx_made_affine). */
+#define NFX_MAF_INVERSE 0 /* MaskedAutoregressiveFlow.inverse  (density, parallel)   */
+#define NFX_IAF_FORWARD 1 /* InverseAutoregressiveFlow.forward (sampling, parallel)  */
+#define NFX_MAF_FORWARD 2 /* MaskedAutoregressiveFlow.forward  (sampling, sequential) */
+#define NFX_IAF_INVERSE 3 /* InverseAutoregressiveFlow.inverse (density, sequential)  */
+
+/*
+ * Raw (unpacked) parameters of one conditioner MLP, exactly as the reference nn.Modules
+ * hold them (device pointers, nn.Linear layout [out, in]). A NULL bias means zero bias;
+ * a NULL mask means dense; a NULL bn_w[i] means no BatchNorm after hidden layer i.
+ * Used by the *_pack entry points, which fold BatchNorm (eval, running stats) and masks into
+ * the MFMA operand layout the kernels read (see DESIGN.md "HBM/LDS layout").
+ */
+typedef struct NfxMlpRaw {
+    const float* w[4];
+    const float* b[4];
+    const float* mask[4];
+    const float* bn_w[3];
+    const float* bn_b[3];
+    const float* bn_rm[3];
+    const float* bn_rv[3];
+    float bn_eps;
+    int n_layers;
+} NfxMlpRaw;
+
+int nfx_abi_version(void);
+const char* nfx_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Affine coupling — CouplingLayer (src/flows/coupling/coupling_layer.py:5-111).
+ *   forward  replaces coupling_layer.py:40-68, inverse replaces coupling_layer.py:70-96.
+ * s_net / b_net: Linear(d,H) -> BN(H) -> ReLU -> Linear(H,H) -> BN(H) -> ReLU -> Linear(H,d)
+ * (coupling_layer.py:18-35); BatchNorm is folded with its running statistics (eval mode).
+ * mask: [d] fp32 0/1 (the layer's `mask` buffer).
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_affine_packed_floats(int d, int H);
+int nfx_affine_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, const float* mask, int d,
+                    int H, float* packed, void* stream);
+int nfx_affine_coupling(const float* packed, const float* in, float* out, float* log_det,
+                        int64_t B, int d, int H, int direction, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Rational-quadratic spline coupling — SplineCouplingLayer
+ * (src/flows/spline/spline_coupling_layer.py:6-323): forward :96-137, inverse :139-180,
+ * spline core _rational_quadratic_spline :182-309, param net :56-62 (no BatchNorm).
+ * rescale: 0 = data_min/data_max None (identity, :78-94); 1 = scalar rescale with
+ * data_min/data_max given as fp32 scalars.
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_spline_packed_floats(int d, int H, int K);
+int nfx_spline_pack(const NfxMlpRaw* param_net, const float* mask, int d, int H, int K,
+                    float* packed, void* stream);
+int nfx_spline_coupling(const float* packed, const float* in, float* out, float* log_det,
+                        int64_t B, int d, int H, int K, float bound, float min_bin_width,
+                        float min_bin_height, float min_derivative, int rescale,
+                        float data_min, float data_max, int direction, int accumulate,
+                        void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Unit-interval RQ spline — rational_quadratic_spline
+ * (src/flows/spline/rational_quadratic_spline.py:4-104). Elementwise over N inputs with
+ * per-input unnormalised widths/heights [N,K] and derivatives [N,K-1]; epsilon is forced to
+ * 1e-6 exactly as the reference does (:19).
+ * ------------------------------------------------------------------------------------- */
+int nfx_rqs_unit(const float* in, const float* widths, const float* heights,
+                 const float* derivatives, float* out, float* log_det, int64_t N, int K,
+                 float min_bin_width, float min_bin_height, float min_derivative, int inverse,
+                 void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * MADE-masked autoregressive affine flows — MADE (src/flows/autoregressive/made.py:6-140),
+ * MaskedLinear (masked_linear.py:4-18), MaskedAutoregressiveFlow
+ * (masked_autoregressive_flow.py:18-78), InverseAutoregressiveFlow
+ * (inverse_autoregressive_flow.py:30-103). net: 4 masked layers, output order [mu | alpha].
+ * variant: NFX_MAF_INVERSE / NFX_IAF_FORWARD (parallel, MFMA) or
+ *          NFX_MAF_FORWARD / NFX_IAF_INVERSE (sequential over d).
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_made_packed_floats(int d, int H);
+int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
+int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
+                    int64_t B, int d, int H, int variant, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Gaussian base log-density + NLL partial sums — the log_prob glue of the callers
+ * (Flow.log_prob src/flows/flow/flow.py:56-73; README.md:113-114; src/utils.py:39-55):
+ *   logp[i] = -0.5 * (fp32(d*log(2*pi)) + sum_j z[i,j]^2) + log_det[i]
+ * (torch.distributions.MultivariateNormal(0, I).log_prob(z) + log_det).
+ * sums[0] = sum_i logp[i] in float64, sums[1] = B (as double). `workspace` must hold
+ * nfx_gauss_workspace_bytes(B) bytes. logp may be NULL (NLL-only).
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_gauss_workspace_bytes(int64_t B);
+int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
+                      void* workspace, int64_t B, int d, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NFX_H */

@@ -1,0 +1,163 @@
+// Fused affine-coupling layer (RealNVP CouplingLayer) for gfx950.
+//
+// Reference: src/flows/coupling/coupling_layer.py
+//   forward :40-68   x = z*m + (1-m)*(z*exp(s)+b),  ld = sum((1-m)*s)
+//   inverse :70-96   z = x*m + (1-m)*((x-b)*exp(-s)), ld = sum((1-m)*(-s))
+//   s = clamp(s_net(x*m), -10, 10), b = clamp(b_net(x*m), -10, 10)   (:50-51, :79-80)
+//   s_net/b_net: Linear(d,H) BN ReLU Linear(H,H) BN ReLU Linear(H,d)   (:18-35)
+//   guards: non-finite outputs -> 0, non-finite ld -> 0                 (:61-66, :89-94)
+//
+// One kernel = one layer, fully fused: conditioner MLPs on fp32 MFMA (32x32x2, activations
+// kept in accumulator registers between layers, weights staged once per workgroup in LDS),
+// the 64->d output layer on VALU with a v_permlane32_swap half-wave combine, the affine
+// transform, the NaN/Inf guards and the per-sample log-det accumulate. HBM traffic is the
+// x row in, the y row out and the log-det read-modify-write: 8d+8 bytes per sample.
+//
+// Work decomposition: a wave owns 64-sample chunks (two 32-sample MFMA column tiles);
+// after the output layer lane l holds sample (chunk*64 + l) for the epilogue, so x/y/log_det
+// accesses are fully coalesced. Waves grid-stride over chunks so the LDS weight image is
+// loaded once per workgroup.
+#include "nfx_affine_kernel.h"
+
+namespace nfx {
+
+// Folded weight W'[row][col] of layer `layer` (0-based) of an MLP:
+// MaskedLinear mask (w*m, masked_linear.py:18) then eval BatchNorm scale gamma/sqrt(rv+eps).
+__device__ float mlp_weight(const NfxMlpRaw& net, int layer, int in_dim, int row, int col) {
+    size_t idx = (size_t)row * in_dim + col;
+    float w = net.w[layer][idx];
+    if (net.mask[layer]) w = w * net.mask[layer][idx];
+    if (layer < 3 && net.bn_w[layer]) {
+        double a = (double)net.bn_w[layer][row] / sqrt((double)net.bn_rv[layer][row] + (double)net.bn_eps);
+        return (float)(a * (double)w);
+    }
+    return w;
+}
+
+__device__ float mlp_bias(const NfxMlpRaw& net, int layer, int row) {
+    float b = net.b[layer] ? net.b[layer][row] : 0.f;
+    if (layer < 3 && net.bn_w[layer]) {
+        double a = (double)net.bn_w[layer][row] / sqrt((double)net.bn_rv[layer][row] + (double)net.bn_eps);
+        return (float)(a * ((double)b - (double)net.bn_rm[layer][row]) + (double)net.bn_b[layer][row]);
+    }
+    return b;
+}
+
+__global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float* mask, int d,
+                                   int H, float* packed) {
+    const int HT = (H + 31) / 32;
+    const AffineLayout L = affine_layout(d, HT);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
+        float v = 0.f;
+        if (i >= L.mask) {
+            int j = i - L.mask;
+            v = j < d ? mask[j] : 0.f;
+        } else {
+            const int net = i / L.net;
+            const NfxMlpRaw& P = net ? b_net : s_net;
+            const int o = i - net * L.net;
+            if (o < L.b1) {
+                int t = o - L.w1, lane = t & 63, ks = (t >> 6) % L.KS1, ht = (t >> 6) / L.KS1;
+                int row = 32 * ht + (lane & 31), col = 2 * ks + (lane >> 5);
+                v = (row < H && col < d) ? mlp_weight(P, 0, d, row, col) : 0.f;
+            } else if (o < L.w2) {
+                int t = o - L.b1, h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+                int row = 32 * ht + crow(r, h);
+                v = row < H ? mlp_bias(P, 0, row) : 0.f;
+            } else if (o < L.b2) {
+                int t = o - L.w2, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+                int kt = (t >> 10) % HT, hto = (t >> 10) / HT;
+                int row = 32 * hto + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
+                v = (row < H && col < H) ? mlp_weight(P, 1, H, row, col) : 0.f;
+            } else if (o < L.w3) {
+                int t = o - L.b2, h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+                int row = 32 * ht + crow(r, h);
+                v = row < H ? mlp_bias(P, 1, row) : 0.f;
+            } else if (o < L.b3) {
+                int t = o - L.w3, h = t & 1, r = (t >> 1) & 15, ht = (t >> 5) % HT, j = (t >> 5) / HT;
+                int col = 32 * ht + crow(r, h);
+                v = col < H ? mlp_weight(P, 2, H, j, col) : 0.f;
+            } else {
+                int j = o - L.b3;
+                v = j < d ? mlp_bias(P, 2, j) : 0.f;
+            }
+        }
+        packed[i] = v;
+    }
+}
+
+static affine_kernel_t pick_affine(int HT, int d, int dir) {
+    switch (HT) {
+        case 1: return affine_pick_ht<1>(d, dir);
+        case 2: return affine_pick_ht<2>(d, dir);
+        case 3: return affine_pick_ht<3>(d, dir);
+        case 4: return affine_pick_ht<4>(d, dir);
+        default: return nullptr;
+    }
+}
+
+// Grid: enough resident workgroups to fill every CU (occupancy from the runtime), never more
+// than there are 4-chunk groups of work.
+int resident_grid(const void* kernel, int threads, size_t lds_bytes, int64_t work_groups) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds_bytes) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 1;
+    int64_t g = (int64_t)num_cus() * per_cu;
+    if (work_groups < g) g = work_groups;
+    return (int)(g < 1 ? 1 : g);
+}
+
+int prepare_lds(const void* kernel, size_t bytes) {
+    if (bytes > 65536) {
+        if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) !=
+            hipSuccess)
+            return set_error(NFX_ELAUNCH, "hipFuncSetAttribute(dynamic LDS %zu B) failed", bytes);
+    }
+    return NFX_OK;
+}
+
+}  // namespace nfx
+
+using namespace nfx;
+
+extern "C" size_t nfx_affine_packed_floats(int d, int H) {
+    if (d <= 0 || H <= 0) return 0;
+    return (size_t)affine_layout(d, (H + 31) / 32).total;
+}
+
+extern "C" int nfx_affine_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, const float* mask,
+                               int d, int H, float* packed, void* stream) {
+    if (!s_net || !b_net || !mask || !packed) return set_error(NFX_EINVAL, "affine_pack: null pointer");
+    if (d <= 0 || H <= 0) return set_error(NFX_EINVAL, "affine_pack: bad shape d=%d H=%d", d, H);
+    const NfxMlpRaw* nets[2] = {s_net, b_net};
+    for (int n = 0; n < 2; ++n)
+        for (int l = 0; l < 3; ++l)
+            if (!nets[n]->w[l]) return set_error(NFX_EINVAL, "affine_pack: net %d layer %d weight is null", n, l);
+    const int total = (int)nfx_affine_packed_floats(d, H);
+    int blocks = (total + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    affine_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*s_net, *b_net, mask, d, H, packed);
+    return check_launch("affine_pack_kernel");
+}
+
+extern "C" int nfx_affine_coupling(const float* packed, const float* in, float* out, float* log_det,
+                                   int64_t B, int d, int H, int direction, int accumulate,
+                                   void* stream) {
+    if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "affine_coupling: bad shape B=%lld d=%d H=%d", (long long)B, d, H);
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE)
+        return set_error(NFX_EINVAL, "affine_coupling: direction must be +1 or -1");
+    if (B == 0) return NFX_OK;
+    if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "affine_coupling: null pointer");
+    if (in == out) return set_error(NFX_EINVAL, "affine_coupling: in and out must not alias");
+    const int HT = (H + 31) / 32;
+    affine_kernel_t k = pick_affine(HT, d, direction);
+    if (!k) return set_error(NFX_EUNSUPPORTED, "affine_coupling: d=%d H=%d outside the compiled family (d<=8, H<=128)", d, H);
+    const size_t lds = (size_t)affine_layout(d, HT).total * sizeof(float);
+    int rc = prepare_lds((const void*)k, lds);
+    if (rc) return rc;
+    const int64_t nchunks = (B + 63) / 64;
+    const int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
+    k<<<grid, 256, lds, (hipStream_t)stream>>>(packed, in, out, log_det, B, accumulate, nchunks);
+    return check_launch("affine_coupling_kernel");
+}

@@ -1,0 +1,213 @@
+// Affine-coupling kernel template (see nfx_affine.hip for the design notes).
+#pragma once
+#include "nfx_common.h"
+
+namespace nfx {
+
+__host__ __device__ constexpr int up4(int v) { return (v + 3) & ~3; }
+
+// Packed weight image (floats). Per net (s_net = 0, b_net = 1):
+//   w1 [HT][KS1][64]        A operand of layer 1 (BN folded)
+//   b1 [HT][16][2]          bias of layer 1 at accumulator row crow(r,h) (BN folded)
+//   w2 [HT][HT][4][64][4]   A operand of layer 2: [out tile][k tile][r/4][lane][r%4]
+//   b2 [HT][16][2]
+//   w3 [d][HT][16][2]       output layer, by (j, k tile, r, half) for the VALU dot
+//   b3 [up4(d)]
+// then mask [up4(d)].
+struct AffineLayout {
+    int d, HT, KS1;
+    int w1, b1, w2, b2, w3, b3, net, mask, total;
+};
+
+__host__ __device__ constexpr AffineLayout affine_layout(int d, int HT) {
+    AffineLayout L{};
+    L.d = d;
+    L.HT = HT;
+    L.KS1 = (d + 1) / 2;
+    int o = 0;
+    L.w1 = o; o += HT * L.KS1 * 64;
+    L.b1 = o; o += HT * 32;
+    L.w2 = o; o += HT * HT * 16 * 64;
+    L.b2 = o; o += HT * 32;
+    L.w3 = o; o += d * HT * 32;
+    L.b3 = o; o += up4(d);
+    L.net = o;
+    L.mask = 2 * o;
+    L.total = 2 * o + up4(d);
+    return L;
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&v)[D]) {
+    if constexpr (D == 2) {
+        float2 t = *reinterpret_cast<const float2*>(p);
+        v[0] = t.x; v[1] = t.y;
+    } else if constexpr (D == 4) {
+        float4 t = *reinterpret_cast<const float4*>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[j] = p[j];
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v)[D]) {
+    if constexpr (D == 2) {
+        *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+    } else if constexpr (D == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) p[j] = v[j];
+    }
+}
+
+// Conditioner MLP of one net for a 64-sample chunk; returns clamp(net(x*m), -10, 10)[j] for the
+// lane's own sample (lane l <-> sample chunk*64 + l).
+template <int HT, int D>
+__device__ __forceinline__ void affine_net(const float* __restrict__ P, const AffineLayout& L,
+                                           const float (&xb)[2][(D + 1) / 2], float (&res)[D]) {
+    constexpr int KS1 = (D + 1) / 2;
+    const int lane = lane_id(), h = lane >> 5;
+
+    // Layer 1: [H x d] * [d x 32] per sample tile, bias-initialised accumulators, ReLU.
+    f32x16 h1[HT][2];
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) {
+        f32x16 a0, a1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b1 + (ht * 16 + r) * 2 + h];
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) {
+            const float w = P[L.w1 + (ht * KS1 + ks) * 64 + lane];
+            a0 = mfma32(w, xb[0][ks], a0);
+            a1 = mfma32(w, xb[1][ks], a1);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            a1[r] = trelu(a1[r]);
+        }
+        h1[ht][0] = a0;
+        h1[ht][1] = a1;
+    }
+
+    // Layer 2 (H x H) tile by tile; each finished tile is ReLU'd and folded into the
+    // output-layer partial dot products right away (keeps one tile of h2 live).
+    float part[D][2];
+#pragma unroll
+    for (int j = 0; j < D; ++j) part[j][0] = part[j][1] = 0.f;
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a0, a1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b2 + (hto * 16 + r) * 2 + h];
+#pragma unroll
+        for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(
+                    P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
+                    a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float w3 = P[L.w3 + ((j * HT + hto) * 16 + r) * 2 + h];
+                part[j][0] = fmaf(w3, trelu(a0[r]), part[j][0]);
+                part[j][1] = fmaf(w3, trelu(a1[r]), part[j][1]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        res[j] = tclamp(halves_sum(part[j][0], part[j][1]) + P[L.b3 + j], -10.f, 10.f);
+}
+
+template <int HT, int D, int DIR>
+__global__ __launch_bounds__(256) void affine_coupling_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int accumulate, int64_t nchunks) {
+    constexpr AffineLayout L = affine_layout(D, HT);
+    constexpr int KS1 = L.KS1;
+    extern __shared__ f32x4 lds4[];
+    {
+        const f32x4* src = reinterpret_cast<const f32x4*>(packed);
+        for (int i = threadIdx.x; i < L.total / 4; i += 256) lds4[i] = src[i];
+    }
+    __syncthreads();
+    const float* sm = reinterpret_cast<const float*>(lds4);
+
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    float mk[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) mk[j] = sm[L.mask + j];
+
+    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nchunks; c += nwaves) {
+        const int64_t base = c * 64;
+        const float* smi = sm + opaque_zero();
+        // Layer-1 B operands: lane supplies x_a[sample base + 32*st + col][2*ks + h].
+        float xb[2][KS1];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const int64_t s = base + 32 * st + col;
+#pragma unroll
+            for (int ks = 0; ks < KS1; ++ks) {
+                const int k = 2 * ks + h;
+                float v = 0.f;
+                if (k < D && s < B) v = in[s * D + k] * sm[L.mask + k];
+                xb[st][ks] = v;
+            }
+        }
+        const int64_t so = base + lane;
+        float xr[D];
+        if (so < B) {
+            load_row<D>(in + so * D, xr);
+        } else {
+#pragma unroll
+            for (int j = 0; j < D; ++j) xr[j] = 0.f;
+        }
+
+        float sv[D], bv[D];
+        affine_net<HT, D>(smi, L, xb, sv);
+        affine_net<HT, D>(smi + L.net, L, xb, bv);
+
+        if (so < B) {
+            float y[D];
+            float ld = 0.f;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const float m = mk[j], om = 1.f - m;
+                const float xa = xr[j] * m;
+                float t;
+                if constexpr (DIR < 0) {
+                    t = (xr[j] - bv[j]) * expf(-sv[j]);
+                    ld = ld + om * (-sv[j]);
+                } else {
+                    t = xr[j] * expf(sv[j]) + bv[j];
+                    ld = ld + om * sv[j];
+                }
+                const float v = xa + om * t;
+                y[j] = nonfinite(v) ? 0.f : v;
+            }
+            if (nonfinite(ld)) ld = 0.f;
+            store_row<D>(out + so * D, y);
+            logdet[so] = accumulate ? logdet[so] + ld : ld;
+        }
+    }
+}
+
+typedef void (*affine_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int64_t);
+
+template <int HT>
+affine_kernel_t affine_pick_ht(int d, int dir);
+
+}  // namespace nfx

@@ -1,0 +1,82 @@
+// Shared device helpers for the gfx950 flow kernels.
+//
+// MFMA tile convention used by every conditioner MLP in this library
+// (v_mfma_f32_32x32x2_f32, exact fp32, 64 FLOP/clk/SIMD):
+//   D[32 x 32] += A[32 x 2] * B[2 x 32]
+//   A: lane l holds A[i = l & 31][k = l >> 5]       (weights, packed on device by *_pack)
+//   B: lane l holds B[k = l >> 5][j = l & 31]       (activations, column j = one sample)
+//   C/D: lane l, register r holds D[crow(r, l >> 5)][l & 31]
+// Activations therefore live "hidden-unit rows x sample columns": a layer's accumulator tile
+// is directly the B operand of the next layer (k-step (kt, r) reads register r of tile kt),
+// with the weight operand permuted on the host side of the pack to match. No LDS round trip
+// and no lane shuffles between layers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nfx.h"
+
+namespace nfx {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Row of register r in lane-half h of a 32x32 fp32 MFMA accumulator.
+__host__ __device__ constexpr int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// torch.clamp semantics: NaN propagates (fminf/fmaxf = IEEE minNum/maxNum would drop it).
+// gfx950 has the IEEE-754-2019 NaN-propagating v_maximum3_f32 / v_minimum3_f32, reached
+// through the elementwise maximum/minimum builtins: one instruction per bound.
+__device__ __forceinline__ float tmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float tmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float tclamp(float v, float lo, float hi) { return tmin(tmax(v, lo), hi); }
+__device__ __forceinline__ float tclamp_min(float v, float lo) { return tmax(v, lo); }
+// torch.relu == clamp_min(0): NaN propagates.
+__device__ __forceinline__ float trelu(float v) { return tmax(v, 0.f); }
+// torch.isnan(v) | torch.isinf(v)
+__device__ __forceinline__ bool nonfinite(float v) { return !__builtin_isfinite(v); }
+
+// Sum of lane-halves with the lane<->sample convention of the small-d epilogues:
+// lanes 0..31 return p0[l] + p0[l+32], lanes 32..63 return p1[l-32] + p1[l].
+// v_permlane32_swap: vdst[32..63] <-> vsrc[0..31]; afterwards vdst + vsrc is exactly that.
+__device__ __forceinline__ float halves_sum(float p0, float p1) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false,
+                                              false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Same exchange without the add: lanes 0..31 get p0[l+32] (the other half of tile 0),
+// lanes 32..63 get p1[l-32] (the other half of tile 1).
+__device__ __forceinline__ float halves_other(float p0, float p1) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false,
+                                              false);
+    return (threadIdx.x & 32) ? __uint_as_float(r[0]) : __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// A zero the compiler cannot see through. Offsetting the LDS weight pointer by it inside a
+// grid-stride loop stops LICM from hoisting every (loop-invariant) weight read out of the
+// loop into registers, which would otherwise blow the VGPR budget and spill.
+__device__ __forceinline__ int opaque_zero() {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return z;
+}
+
+}  // namespace nfx
+
+// Error reporting shared by the C-ABI translation units (nfx_abi.hip).
+namespace nfx {
+int set_error(int code, const char* fmt, ...);
+int check_launch(const char* what);
+int num_cus();
+// Workgroups that fill every CU at the kernel's occupancy, capped by the available work.
+int resident_grid(const void* kernel, int threads, size_t lds_bytes, int64_t work_groups);
+// Raise the dynamic-LDS limit of `kernel` when it needs more than 64 KiB.
+int prepare_lds(const void* kernel, size_t bytes);
+}  // namespace nfx

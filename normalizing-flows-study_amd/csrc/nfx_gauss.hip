@@ -1,0 +1,88 @@
+// Gaussian base log-density and NLL partial sums (the log_prob glue of the reference callers).
+//
+// Reference: Flow.log_prob src/flows/flow/flow.py:56-73 and the inline callers README.md:113-114,
+// src/utils.py:39-55, plots/_common.py:201-202:
+//   log_p = MultivariateNormal(0, I).log_prob(z) + log_det,   loss = -log_p.mean()
+// torch's MVN log_prob with identity scale_tril reduces to -0.5*(fp32(d*log 2pi) + sum_j z_j^2)
+// (bit-exact). The mean is accumulated in float64 (NLL parity at 1M-4M
+// samples needs it) with a deterministic two-pass block reduction.
+#include <math.h>
+
+#include "nfx_common.h"
+
+namespace nfx {
+
+constexpr int kGaussThreads = 256;
+constexpr int kGaussMaxBlocks = 1024;
+
+__device__ __forceinline__ double block_sum_f64(double v) {
+    __shared__ double red[kGaussThreads / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < kGaussThreads / 64; ++w) t += red[w];
+    return t;
+}
+
+__global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
+    const float* __restrict__ z, const float* __restrict__ ld, float* __restrict__ logp,
+    double* __restrict__ partials, int64_t B, int d, float c) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kGaussThreads + threadIdx.x; i < B;
+         i += (int64_t)gridDim.x * kGaussThreads) {
+        const float* zr = z + i * d;
+        float m = zr[0] * zr[0];
+        for (int j = 1; j < d; ++j) m = m + zr[j] * zr[j];
+        const float lp = -0.5f * (m + c) + ld[i];
+        if (logp) logp[i] = lp;
+        acc += (double)lp;
+    }
+    const double t = block_sum_f64(acc);
+    if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kGaussThreads) void gauss_finish_kernel(const double* __restrict__ partials,
+                                                                     int n, double* __restrict__ sums,
+                                                                     int64_t B) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += kGaussThreads) acc += partials[i];
+    const double t = block_sum_f64(acc);
+    if (threadIdx.x == 0) {
+        sums[0] = t;
+        sums[1] = (double)B;
+    }
+}
+
+}  // namespace nfx
+
+using namespace nfx;
+
+extern "C" size_t nfx_gauss_workspace_bytes(int64_t B) {
+    (void)B;
+    return (size_t)kGaussMaxBlocks * sizeof(double);
+}
+
+extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
+                                 void* workspace, int64_t B, int d, void* stream) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "gauss_logprob: bad shape B=%lld d=%d", (long long)B, d);
+    if (!sums || !workspace) return set_error(NFX_EINVAL, "gauss_logprob: null sums/workspace");
+    if (B > 0 && (!z || !log_det)) return set_error(NFX_EINVAL, "gauss_logprob: null z/log_det");
+    hipStream_t s = (hipStream_t)stream;
+    int blocks = (int)((B + kGaussThreads - 1) / kGaussThreads);
+    if (blocks > kGaussMaxBlocks) blocks = kGaussMaxBlocks;
+    if (blocks < 1) blocks = 1;
+    const float c = (float)((double)d * log(2.0 * M_PI));
+    double* partials = reinterpret_cast<double*>(workspace);
+    if (B > 0) {
+        gauss_logprob_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, B, d, c);
+        int rc = check_launch("gauss_logprob_kernel");
+        if (rc) return rc;
+    } else {
+        blocks = 0;
+    }
+    gauss_finish_kernel<<<1, kGaussThreads, 0, s>>>(partials, blocks, sums, B);
+    return check_launch("gauss_finish_kernel");
+}

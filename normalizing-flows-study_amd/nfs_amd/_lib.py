@@ -1,0 +1,163 @@
+"""ctypes binding of libnfx.so (the C-ABI declared in include/nfx.h).
+
+The product path fails loudly when the library is missing: every HIP entry point goes through
+`lib()`, which raises NfxLibraryError instead of silently falling back to eager PyTorch.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NFX_LIB", os.path.join(_HERE, "libnfx.so"))
+
+NFX_OK = 0
+NFX_FORWARD = 1
+NFX_INVERSE = -1
+NFX_MAF_INVERSE = 0
+NFX_IAF_FORWARD = 1
+NFX_MAF_FORWARD = 2
+NFX_IAF_INVERSE = 3
+
+# Every symbol include/nfx.h declares (tests check the built library exports all of them).
+EXPORTED_SYMBOLS = (
+    "nfx_abi_version", "nfx_last_error",
+    "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling",
+    "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling",
+    "nfx_rqs_unit",
+    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine",
+    "nfx_gauss_workspace_bytes", "nfx_gauss_logprob",
+)
+
+
+class NfxLibraryError(RuntimeError):
+    pass
+
+
+class NfxError(RuntimeError):
+    pass
+
+
+class NfxMlpRaw(ctypes.Structure):
+    """Mirror of `NfxMlpRaw` in include/nfx.h (device pointers of one conditioner MLP)."""
+    _fields_ = [
+        ("w", ctypes.c_void_p * 4),
+        ("b", ctypes.c_void_p * 4),
+        ("mask", ctypes.c_void_p * 4),
+        ("bn_w", ctypes.c_void_p * 3),
+        ("bn_b", ctypes.c_void_p * 3),
+        ("bn_rm", ctypes.c_void_p * 3),
+        ("bn_rv", ctypes.c_void_p * 3),
+        ("bn_eps", ctypes.c_float),
+        ("n_layers", ctypes.c_int),
+    ]
+
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+_SIGNATURES = {
+    "nfx_abi_version": (_int, []),
+    "nfx_last_error": (ctypes.c_char_p, []),
+    "nfx_affine_packed_floats": (_sz, [_int, _int]),
+    "nfx_affine_pack": (_int, [ctypes.POINTER(NfxMlpRaw), ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _vp, _vp]),
+    "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
+    "nfx_spline_packed_floats": (_sz, [_int, _int, _int]),
+    "nfx_spline_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _int, _vp, _vp]),
+    "nfx_spline_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _f,
+                                   _int, _f, _f, _int, _int, _vp]),
+    "nfx_rqs_unit": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int, _vp]),
+    "nfx_made_packed_floats": (_sz, [_int, _int]),
+    "nfx_made_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
+    "nfx_made_affine": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
+    "nfx_gauss_workspace_bytes": (_sz, [_i64]),
+    "nfx_gauss_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libnfx.so without touching the GPU (safe on CPU-only hosts)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NfxLibraryError(
+                f"libnfx.so not found at {path}: build it with "
+                f"`python normalizing-flows-study_amd/build.py` (or __graft_entry__.build()). "
+                f"The HIP path has no eager fallback.")
+        l = ctypes.CDLL(path)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(l, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+        return l
+
+
+def lib():
+    return load()
+
+
+def available():
+    try:
+        load()
+        return True
+    except NfxLibraryError:
+        return False
+
+
+def check(rc, what):
+    if rc != NFX_OK:
+        msg = lib().nfx_last_error().decode(errors="replace")
+        raise NfxError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    """hipStream_t of torch's current stream on t's device (the stream kernels are enqueued on)."""
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def mlp_raw(linears, batchnorms=(), masks=None):
+    """Build an NfxMlpRaw from nn.Linear modules (+ optional BatchNorm1d after hidden layers).
+
+    Returns (struct, keepalive) — keepalive holds the contiguous tensors the pointers refer to.
+    """
+    raw = NfxMlpRaw()
+    keep = []
+
+    def p(t):
+        t = t.detach().contiguous().float()
+        keep.append(t)
+        return t.data_ptr()
+
+    raw.n_layers = len(linears)
+    for i, lin in enumerate(linears):
+        raw.w[i] = p(lin.weight)
+        raw.b[i] = p(lin.bias) if lin.bias is not None else None
+        if masks is not None and masks[i] is not None:
+            raw.mask[i] = p(masks[i])
+    eps = 1e-5
+    for i, bn in enumerate(batchnorms):
+        if bn is None:
+            continue
+        raw.bn_w[i] = p(bn.weight) if bn.weight is not None else p(torch.ones_like(bn.running_var))
+        raw.bn_b[i] = p(bn.bias) if bn.bias is not None else p(torch.zeros_like(bn.running_var))
+        raw.bn_rm[i] = p(bn.running_mean)
+        raw.bn_rv[i] = p(bn.running_var)
+        eps = bn.eps
+    raw.bn_eps = eps
+    return raw, keep

@@ -1,0 +1,10 @@
+"""Flow layers on the hot path (mirrors src/flows/__init__.py for the in-scope symbols)."""
+from .flow import Flow, SequentialFlow, HipFlow, STATS, reset_stats
+from .coupling import CouplingLayer
+from .spline import SplineCouplingLayer, rational_quadratic_spline
+from .autoregressive import (MaskedLinear, MADE, MaskedAutoregressiveFlow,
+                             InverseAutoregressiveFlow, made_degrees)
+
+__all__ = ["Flow", "SequentialFlow", "HipFlow", "CouplingLayer", "SplineCouplingLayer",
+           "rational_quadratic_spline", "MaskedLinear", "MADE", "MaskedAutoregressiveFlow",
+           "InverseAutoregressiveFlow", "made_degrees", "STATS", "reset_stats"]

@@ -1,0 +1,193 @@
+"""Flow interface + HIP dispatch.
+
+Mirrors the reference boundary `Flow` / `SequentialFlow` (src/flows/flow/flow.py:4-73,
+src/flows/flow/sequential_flow.py:5-34): `forward(z) -> (x, log_det[B])`,
+`inverse(x) -> (z, log_det[B])`, `sample`, `log_prob`.
+
+Routing (HipFlow._route):
+  * fp32 tensors on a ROCm device  -> the layer's fused gfx950 kernel through libnfx.so.
+    If autograd needs gradients, the kernel still computes the outputs and the backward pass
+    recomputes through the layer's torch composite (HipFlowFunction).
+  * CPU tensors or fp64 (gradcheck)  -> the layer's torch composite (same math as the reference).
+  * train-mode BatchNorm in a conditioner (CouplingLayer) -> torch composite: the batch
+    statistics are batch-global (out of the eval hot path).
+A shape outside the compiled kernel family raises NotImplementedError on the GPU instead of
+silently running eager (set nfs_amd.flows.flow.ALLOW_TORCH_FALLBACK = True to permit it).
+"""
+import torch
+import torch.nn as nn
+
+from .. import _lib
+
+ALLOW_TORCH_FALLBACK = False
+
+# Counters so tests and the bench can prove which path ran.
+STATS = {"hip": 0, "torch": 0}
+
+
+def reset_stats():
+    STATS["hip"] = 0
+    STATS["torch"] = 0
+
+
+class Flow(nn.Module):
+    """Base class for normalizing flow layers (src/flows/flow/flow.py:4-73)."""
+
+    def __init__(self):
+        super().__init__()
+        self.data_dim = None
+
+    def forward(self, z):
+        raise NotImplementedError
+
+    def inverse(self, x):
+        raise NotImplementedError
+
+    def sample(self, num_samples, base_dist, device="cpu"):
+        """flow.py:40-54: z ~ base, return forward(z)[0]."""
+        z = base_dist.sample((num_samples,)).to(device)
+        x, _ = self.forward(z)
+        return x
+
+    def log_prob(self, x, base_dist):
+        """flow.py:56-73: log p(x) = base.log_prob(inverse(x)) + log|det J_inv|."""
+        z, log_det_inv = self.inverse(x)
+        log_p_z = base_dist.log_prob(z)
+        if len(log_p_z.shape) > 1:
+            log_p_z = log_p_z.sum(dim=1)
+        return log_p_z + log_det_inv
+
+
+class HipFlowFunction(torch.autograd.Function):
+    """HIP forward, torch-composite backward (recompute) for a HipFlow layer."""
+
+    @staticmethod
+    def forward(ctx, layer, direction, x, *params):
+        ctx.layer = layer
+        ctx.direction = direction
+        ctx.save_for_backward(x)
+        with torch.no_grad():
+            y, ld = layer._hip_call(x, direction)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, gy, gld):
+        (x,) = ctx.saved_tensors
+        layer = ctx.layer
+        params = [p for p in layer.parameters()]
+        with torch.enable_grad():
+            xr = x.detach().requires_grad_(True)
+            y, ld = layer._torch_call(xr, ctx.direction)
+            outs, grads_out = [], []
+            if gy is not None:
+                outs.append(y)
+                grads_out.append(gy)
+            if gld is not None:
+                outs.append(ld)
+                grads_out.append(gld)
+            wrt = [xr] + [p for p in params if p.requires_grad]
+            grads = torch.autograd.grad(outs, wrt, grads_out, allow_unused=True)
+        gx = grads[0]
+        it = iter(grads[1:])
+        gparams = [next(it) if p.requires_grad else None for p in params]
+        return (None, None, gx, *gparams)
+
+
+class HipFlow(Flow):
+    """A Flow whose eval/sampling math runs in one fused gfx950 kernel per call.
+
+    Subclasses implement:
+      _torch_call(x, direction) -> (y, ld)            composite torch math (reference ops)
+      _hip_supported(x) -> (bool, reason)             shape/dtype inside the kernel family
+      _hip_launch(x, out, log_det, direction, accumulate)   enqueue the kernel
+      _torch_only() -> bool                           state that forces the composite path
+    """
+
+    def forward(self, z):
+        return self._dispatch(z, 1)
+
+    def inverse(self, x):
+        return self._dispatch(x, -1)
+
+    # -- routing -----------------------------------------------------------------------
+    def _route(self, x):
+        if x.device.type != "cuda" or x.dtype != torch.float32:
+            return "torch"
+        if self._torch_only():
+            return "torch"
+        ok, why = self._hip_supported(x)
+        if not ok:
+            if ALLOW_TORCH_FALLBACK:
+                return "torch"
+            raise NotImplementedError(
+                f"{type(self).__name__}: no gfx950 kernel for this call ({why}); "
+                f"set nfs_amd.flows.flow.ALLOW_TORCH_FALLBACK=True to run eager PyTorch")
+        return "hip"
+
+    def _dispatch(self, x, direction):
+        if self._route(x) == "torch":
+            STATS["torch"] += 1
+            return self._torch_call(x, direction)
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return HipFlowFunction.apply(self, direction, x, *list(self.parameters()))
+        return self._hip_call(x, direction)
+
+    def _hip_call(self, x, direction):
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        ld = torch.empty(x.shape[0], device=x.device, dtype=torch.float32)
+        self._hip_launch_counted(x, out, ld, direction, accumulate=False)
+        return out, ld
+
+    def _hip_launch_counted(self, x, out, log_det, direction, accumulate):
+        STATS["hip"] += 1
+        self._hip_launch(x, out, log_det, direction, accumulate)
+
+    # -- packed-weight cache -------------------------------------------------------------
+    def _state_key(self, device):
+        key = [str(device)]
+        for t in list(self.parameters()) + list(self.buffers()):
+            key.append((t.data_ptr(), t._version))
+        return tuple(key)
+
+    def _packed(self, device, build):
+        """Return the cached device weight image, rebuilding it when any parameter/buffer
+        changed (in-place optimizer steps and load_state_dict bump tensor versions)."""
+        key = self._state_key(device)
+        cache = getattr(self, "_nfx_pack_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        packed = build(device)
+        object.__setattr__(self, "_nfx_pack_cache", (key, packed))
+        return packed
+
+    def _torch_only(self):
+        return False
+
+
+class SequentialFlow(Flow):
+    """A sequence of flows applied in order (src/flows/flow/sequential_flow.py:5-34)."""
+
+    def __init__(self, flows):
+        super().__init__()
+        if not isinstance(flows, (list, nn.ModuleList)):
+            raise ValueError("flows must be a list or nn.ModuleList")
+        self.flows = nn.ModuleList(flows)
+
+    def forward(self, z):
+        total_log_det = torch.zeros(z.size(0), device=z.device)
+        for flow in self.flows:
+            z, log_det = flow.forward(z)
+            total_log_det += log_det
+        return z, total_log_det
+
+    def inverse(self, x):
+        total_log_det = torch.zeros(x.size(0), device=x.device)
+        for flow in reversed(self.flows):
+            x, log_det = flow.inverse(x)
+            total_log_det += log_det
+        return x, total_log_det
+
+
+def stream_ptr(t):
+    return _lib.stream_of(t)

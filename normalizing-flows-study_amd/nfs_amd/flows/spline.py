@@ -1,0 +1,289 @@
+"""Rational-quadratic spline coupling — drop-in for src/flows/spline/spline_coupling_layer.py.
+
+`SplineCouplingLayer` keeps the reference constructor (spline_coupling_layer.py:13-23),
+attributes, `param_net` (Linear -> ReLU -> Linear -> ReLU -> Linear, no BatchNorm, :56-62),
+initialisation (:311-323) and state_dict keys. On a ROCm device it runs as ONE fused gfx950
+kernel per call (csrc/nfx_spline*.hip): param MLP on fp32 MFMA, softmax/softplus/knots,
+bin search, the RQ spline (forward or citardauq inverse), guards and log-det.
+
+`rational_quadratic_spline` is the stand-alone unit-interval spline of
+src/flows/spline/rational_quadratic_spline.py:4-104 (elementwise kernel nfx_rqs_unit on GPU).
+"""
+import torch
+import torch.nn as nn
+from torch.nn import functional as F
+
+from .. import _lib
+from .flow import HipFlow, STATS
+
+MAX_K = 11        # 3K-1 <= 32: one MFMA row tile of spline parameters per transformed dim
+MAX_D = 8
+MAX_H = 128
+
+
+def _cum_knots(w, bound):
+    """Prepend 0 to cumsum(w) along bins, map to [-bound, bound], pin the ends
+    (spline_coupling_layer.py:208-213)."""
+    c = F.pad(torch.cumsum(w, dim=-1), pad=(1, 0), mode="constant", value=0.0)
+    c = (2 * bound) * c + (-bound)
+    c = torch.cat([torch.full_like(c[..., :1], -bound), c[..., 1:-1], torch.full_like(c[..., :1], bound)], dim=-1)
+    return c
+
+
+def rq_spline_bounded(inputs, uw, uh, ud, inverse, num_bins, bound, min_w, min_h, min_d):
+    """Composite form of SplineCouplingLayer._rational_quadratic_spline (:182-309).
+
+    inputs [B, n]; uw/uh [B, n, K]; ud [B, n, K-1] -> (outputs [B, n], logabsdet [B, n])."""
+    eps = 1e-8
+    inside = (inputs >= -bound) & (inputs <= bound)
+    outputs = torch.where(~inside, inputs, torch.zeros_like(inputs))
+    logabsdet = torch.zeros_like(inputs)
+    if not bool(inside.any()):
+        return outputs, logabsdet
+
+    w = torch.clamp(min_w + (1 - min_w * num_bins) * F.softmax(uw, dim=-1), min=eps)
+    cw = _cum_knots(w, bound)
+    w = torch.clamp(cw[..., 1:] - cw[..., :-1], min=eps)
+    h = torch.clamp(min_h + (1 - min_h * num_bins) * F.softmax(uh, dim=-1), min=eps)
+    ch = _cum_knots(h, bound)
+    h = torch.clamp(ch[..., 1:] - ch[..., :-1], min=eps)
+    dv = torch.clamp(min_d + F.softplus(ud), min=eps)
+    dv = F.pad(dv, pad=(1, 1), mode="constant", value=1.0)
+
+    flat = inputs.contiguous().view(-1)
+    knots = (ch if inverse else cw).contiguous().view(-1, num_bins + 1)
+    k = torch.searchsorted(knots, flat.unsqueeze(-1), right=True).squeeze(-1) - 1
+    k = torch.clamp(k, 0, num_bins - 1)
+
+    def pick(t, idx):
+        return torch.gather(t.contiguous().view(-1, t.shape[-1]), 1, idx.unsqueeze(-1)).squeeze(-1)
+
+    w_k, x_k, h_k, y_k = pick(w, k), pick(cw, k), pick(h, k), pick(ch, k)
+    d_k = pick(dv, k)
+    d_k1 = pick(dv, (k + 1).clamp(max=dv.shape[-1] - 1))
+    s_k = h_k / torch.clamp(w_k, min=eps)
+
+    if inverse:
+        dy = flat - y_k
+        a = dy * (d_k + d_k1 - 2 * s_k) + h_k * (s_k - d_k)
+        b = h_k * d_k - dy * (d_k + d_k1 - 2 * s_k)
+        c = -s_k * dy
+        disc = torch.clamp(b.pow(2) - 4 * a * c, min=0.0)
+        den = -b - torch.sqrt(disc)
+        den = torch.where(den.abs() < eps, torch.full_like(den, eps), den)
+        xi = torch.clamp((2 * c) / den, 0, 1)
+        out = xi * w_k + x_k
+        den_ld = s_k + (d_k1 + d_k - 2 * s_k) * xi * (1 - xi)
+        num_ld = s_k.pow(2) * (d_k1 * xi.pow(2) + 2 * s_k * xi * (1 - xi) + d_k * (1 - xi).pow(2))
+        lad = -torch.log(torch.clamp(num_ld, min=eps)) + 2 * torch.log(torch.clamp(den_ld, min=eps))
+    else:
+        xi = torch.clamp((flat - x_k) / torch.clamp(w_k, min=eps), 0, 1)
+        den = torch.clamp(s_k + (d_k1 + d_k - 2 * s_k) * xi * (1 - xi), min=eps)
+        out = y_k + h_k * (s_k * xi.pow(2) + d_k * xi * (1 - xi)) / den
+        num_d = s_k.pow(2) * (d_k1 * xi.pow(2) + 2 * s_k * xi * (1 - xi) + d_k * (1 - xi).pow(2))
+        lad = torch.log(torch.clamp(num_d / torch.clamp(den.pow(2), min=eps), min=eps))
+
+    sel = inside.view(-1)
+    outputs = outputs.clone().view(-1)
+    logabsdet = logabsdet.clone().view(-1)
+    outputs[sel] = out[sel]
+    logabsdet[sel] = lad[sel]
+    outputs = outputs.view_as(inputs)
+    logabsdet = logabsdet.view_as(inputs)
+    outputs = torch.where(torch.isnan(outputs) | torch.isinf(outputs), inputs, outputs)
+    logabsdet = torch.where(torch.isnan(logabsdet) | torch.isinf(logabsdet), torch.zeros_like(logabsdet), logabsdet)
+    return outputs, logabsdet
+
+
+class SplineCouplingLayer(HipFlow):
+    def __init__(self, data_dim, hidden_dim, mask, num_bins=10, bound=5.0, min_bin_width=1e-3,
+                 min_bin_height=1e-3, min_derivative=1e-3, data_min=None, data_max=None):
+        super().__init__()
+        self.data_dim = data_dim
+        self.num_bins = num_bins
+        self.bound = bound
+        self.min_bin_width = min_bin_width
+        self.min_bin_height = min_bin_height
+        self.min_derivative = min_derivative
+        self.data_min = data_min
+        self.data_max = data_max
+        self.register_buffer("mask", mask)
+        self.param_net = nn.Sequential(
+            nn.Linear(data_dim, hidden_dim), nn.ReLU(),
+            nn.Linear(hidden_dim, hidden_dim), nn.ReLU(),
+            nn.Linear(hidden_dim, data_dim * (3 * num_bins - 1)))
+        self._initialize_weights()
+
+    def _initialize_weights(self):
+        for layer in self.param_net[:-1]:
+            if isinstance(layer, nn.Linear):
+                nn.init.xavier_normal_(layer.weight, gain=1.0)
+                if layer.bias is not None:
+                    nn.init.zeros_(layer.bias)
+        final = self.param_net[-1]
+        nn.init.zeros_(final.weight)
+        if final.bias is not None:
+            nn.init.zeros_(final.bias)
+
+    def _get_spline_params(self, z_a):
+        params = self.param_net(z_a).view(-1, self.data_dim, 3 * self.num_bins - 1)
+        return torch.split(params, [self.num_bins, self.num_bins, self.num_bins - 1], dim=-1)
+
+    def _rescale_to_spline(self, x):
+        if self.data_min is None or self.data_max is None:
+            return x
+        scale = (2 * self.bound) / (self.data_max - self.data_min)
+        return scale * (x - self.data_min) - self.bound
+
+    def _rescale_from_spline(self, x):
+        if self.data_min is None or self.data_max is None:
+            return x
+        scale = (self.data_max - self.data_min) / (2 * self.bound)
+        return (x + self.bound) * scale + self.data_min
+
+    def _rational_quadratic_spline(self, inputs, unnormalized_widths, unnormalized_heights,
+                                   unnormalized_derivatives, inverse=False):
+        return rq_spline_bounded(inputs, unnormalized_widths, unnormalized_heights,
+                                 unnormalized_derivatives, inverse, self.num_bins, self.bound,
+                                 self.min_bin_width, self.min_bin_height, self.min_derivative)
+
+    # -- composite path (spline_coupling_layer.py:96-180) -------------------------------------
+    def _torch_call(self, x, direction):
+        xr = self._rescale_to_spline(x)
+        uw, uh, ud = self._get_spline_params(xr * self.mask)
+        sel = self.mask == 0
+        yb, ldb = self._rational_quadratic_spline(xr[:, sel], uw[:, sel], uh[:, sel], ud[:, sel],
+                                                  inverse=direction < 0)
+        yb = self._rescale_from_spline(yb)
+        y = x.clone()
+        y[:, sel] = yb
+        ld = ldb.sum(dim=1)
+        y = torch.where(torch.isnan(y) | torch.isinf(y), torch.zeros_like(y), y)
+        ld = torch.where(torch.isnan(ld) | torch.isinf(ld), torch.zeros_like(ld), ld)
+        return y, ld
+
+    # -- HIP path -------------------------------------------------------------------------------
+    def _hidden(self):
+        return self.param_net[0].out_features
+
+    def _rescale_scalars(self):
+        if self.data_min is None or self.data_max is None:
+            return 0, 0.0, 0.0
+        lo, hi = self.data_min, self.data_max
+        if torch.is_tensor(lo):
+            if lo.numel() != 1:
+                return None
+            lo = float(lo)
+        if torch.is_tensor(hi):
+            if hi.numel() != 1:
+                return None
+            hi = float(hi)
+        return 1, float(lo), float(hi)
+
+    def _hip_supported(self, x):
+        d, H, K = self.data_dim, self._hidden(), self.num_bins
+        if x.dim() != 2 or x.shape[1] != d:
+            return False, f"input shape {tuple(x.shape)} vs data_dim={d}"
+        if d > MAX_D or H > MAX_H or K > MAX_K or K < 1:
+            return False, f"d={d} (<= {MAX_D}) H={H} (<= {MAX_H}) K={K} (<= {MAX_K})"
+        if self._rescale_scalars() is None:
+            return False, "per-dimension data_min/data_max tensors"
+        return True, ""
+
+    def _build_pack(self, device):
+        d, H, K = self.data_dim, self._hidden(), self.num_bins
+        L = _lib.lib()
+        packed = torch.empty(L.nfx_spline_packed_floats(d, H, K), device=device, dtype=torch.float32)
+        raw, keep = _lib.mlp_raw([self.param_net[0], self.param_net[2], self.param_net[4]])
+        mask = self.mask.detach().to(device=device, dtype=torch.float32).contiguous()
+        _lib.check(L.nfx_spline_pack(raw, _lib.ptr(mask), d, H, K, _lib.ptr(packed),
+                                     _lib.stream_of(packed)), "nfx_spline_pack")
+        packed._nfx_keep = (keep, mask)
+        return packed
+
+    def _hip_launch(self, x, out, log_det, direction, accumulate):
+        packed = self._packed(x.device, self._build_pack)
+        rescale, lo, hi = self._rescale_scalars()
+        _lib.check(_lib.lib().nfx_spline_coupling(
+            _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), x.shape[0],
+            self.data_dim, self._hidden(), self.num_bins, float(self.bound),
+            float(self.min_bin_width), float(self.min_bin_height), float(self.min_derivative),
+            rescale, lo, hi, int(direction), int(bool(accumulate)), _lib.stream_of(x)),
+            "nfx_spline_coupling")
+
+
+def _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,
+                    min_bin_height, min_derivative):
+    """Composite of rational_quadratic_spline.py:4-104 (epsilon forced to 1e-6, :19)."""
+    eps = 1e-6
+    K = widths.shape[-1]
+    w = torch.clamp(min_bin_width + (1 - min_bin_width * K) * F.softmax(widths, dim=-1), min=eps)
+    h = torch.clamp(min_bin_height + (1 - min_bin_height * heights.shape[-1]) * F.softmax(heights, dim=-1), min=eps)
+    dv = torch.clamp(F.softplus(derivatives) + min_derivative, min=eps)
+    xk = F.pad(torch.cumsum(w, dim=-1), (1, 0), "constant", 0.0)
+    yk = F.pad(torch.cumsum(h, dim=-1), (1, 0), "constant", 0.0)
+    dv = F.pad(dv, (1, 1), "constant", 1.0)
+    knots = (yk if inverse else xk).contiguous()
+    if knots.dim() > 2:
+        knots = knots.view(-1, knots.shape[-1])
+    idx = torch.clamp(torch.searchsorted(knots, inputs.unsqueeze(-1), right=True) - 1, 0, K - 1)
+    x_k, y_k = torch.gather(xk, -1, idx), torch.gather(yk, -1, idx)
+    w_k, h_k = torch.gather(w, -1, idx), torch.gather(h, -1, idx)
+    d_k, d_k1 = torch.gather(dv, -1, idx), torch.gather(dv, -1, idx + 1)
+    s_k = h_k / torch.clamp(w_k, min=eps)
+    u = inputs.unsqueeze(-1)
+    if inverse:
+        t1 = (u - y_k) * (d_k + d_k1 - 2 * s_k)
+        a = h_k * (s_k - d_k) + t1
+        b = h_k * d_k - t1
+        c = -s_k * (u - y_k)
+        disc = torch.clamp(b.pow(2) - 4 * a * c, min=0)
+        th = torch.clamp((2 * c) / (-b - torch.sqrt(disc)), 0, 1)
+        out = th * w_k + x_k
+        tt = th * (1 - th)
+        num = s_k.pow(2) * (d_k1 * th.pow(2) + 2 * s_k * tt + d_k * (1 - th).pow(2))
+        den = (s_k + (d_k + d_k1 - 2 * s_k) * tt).pow(2)
+        ld = -torch.log(torch.clamp(num / torch.clamp(den, min=eps), min=eps))
+    else:
+        th = torch.clamp((u - x_k) / torch.clamp(w_k, min=eps), 0, 1)
+        tt = th * (1 - th)
+        den = s_k + (d_k + d_k1 - 2 * s_k) * tt
+        out = y_k + h_k * (s_k * th.pow(2) + d_k * tt) / torch.clamp(den, min=eps)
+        num = s_k.pow(2) * (d_k1 * th.pow(2) + 2 * s_k * tt + d_k * (1 - th).pow(2))
+        ld = torch.log(torch.clamp(num / torch.clamp(den.pow(2), min=eps), min=eps))
+    return out.squeeze(-1), ld.squeeze(-1)
+
+
+def rational_quadratic_spline(inputs, widths, heights, derivatives, inverse=False,
+                              min_bin_width=1e-3, min_bin_height=1e-3, min_derivative=1e-3,
+                              epsilon=1e-6):
+    """Unit-interval RQ spline (src/flows/spline/rational_quadratic_spline.py:4-104).
+
+    1-D inputs [N] with widths/heights [N,K], derivatives [N,K-1]. fp32 on a ROCm device runs
+    the elementwise gfx950 kernel; anything else (CPU, fp64, autograd) the composite."""
+    needs_grad = torch.is_grad_enabled() and any(
+        t.requires_grad for t in (inputs, widths, heights, derivatives))
+    if (inputs.device.type == "cuda" and inputs.dtype == torch.float32 and inputs.dim() == 1
+            and not needs_grad):
+        return _rqs_unit_hip(inputs, widths, heights, derivatives, inverse, min_bin_width,
+                             min_bin_height, min_derivative)
+    STATS["torch"] += 1
+    return _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,
+                           min_bin_height, min_derivative)
+
+
+def _rqs_unit_hip(inputs, widths, heights, derivatives, inverse, min_w, min_h, min_d):
+    N = inputs.shape[0]
+    K = widths.shape[-1]
+    if widths.shape != (N, K) or heights.shape != (N, K) or derivatives.shape != (N, K - 1):
+        raise ValueError("rational_quadratic_spline: expected widths/heights [N,K] and derivatives [N,K-1]")
+    x = inputs.contiguous()
+    uw, uh, ud = widths.contiguous().float(), heights.contiguous().float(), derivatives.contiguous().float()
+    out = torch.empty_like(x)
+    ld = torch.empty_like(x)
+    _lib.check(_lib.lib().nfx_rqs_unit(
+        _lib.ptr(x), _lib.ptr(uw), _lib.ptr(uh), _lib.ptr(ud), _lib.ptr(out), _lib.ptr(ld), N, K,
+        float(min_w), float(min_h), float(min_d), int(bool(inverse)), _lib.stream_of(x)),
+        "nfx_rqs_unit")
+    STATS["hip"] += 1
+    return out, ld

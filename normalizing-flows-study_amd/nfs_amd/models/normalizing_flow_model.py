@@ -1,0 +1,175 @@
+"""NormalizingFlowModel — drop-in for src/models/normalizing_flow_model.py:4-128.
+
+Same constructor, attributes (`flows`, `batch_norms`, `batch_norm_between_layers`) and
+state_dict keys. When every layer routes to its gfx950 kernel, forward/inverse run the layers
+back to back on the current stream with the per-sample log-det accumulated IN PLACE by the
+kernels (accumulate=1), which is exactly the reference's sequential float32
+`log_det_jacobian_sum += log_det` (normalizing_flow_model.py:30-65); there are no
+intermediate log-det tensors and no Python-side adds.
+
+`log_prob` / `nll` add the fused Gaussian base term and the float64 NLL partial sums
+(csrc/nfx_gauss.hip): the log_prob glue the reference's callers write inline
+(README.md:113-114, src/utils.py:39-55, plots/_common.py:201-202).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from ..flows.flow import HipFlow, STATS
+
+
+class NormalizingFlowModel(nn.Module):
+    def __init__(self, flows, batch_norm_between_layers=False):
+        super().__init__()
+        self.batch_norm_between_layers = batch_norm_between_layers
+        if self.batch_norm_between_layers:
+            data_dim = flows[0].data_dim if hasattr(flows[0], "data_dim") else None
+            if data_dim is None:
+                raise ValueError("Cannot use batch_norm_between_layers if flows do not have a 'data_dim' attribute.")
+            self.batch_norms = nn.ModuleList([nn.BatchNorm1d(data_dim) for _ in range(len(flows))])
+        self.flows = nn.ModuleList(flows)
+        # Profiling hook: when set to a list, _hip_chain appends (layer name, start, end) HIP
+        # events recorded on the launch stream around every layer kernel (bench.py uses it).
+        self.layer_events = None
+
+    # -- reference-order chaining ------------------------------------------------------------
+    def forward(self, z):
+        if self._hip_chain_ok(z):
+            return self._hip_chain(z, 1)
+        log_det_jacobian_sum = 0
+        for i, flow in enumerate(self.flows):
+            z, log_det_jacobian = flow(z)
+            log_det_jacobian_sum += log_det_jacobian
+            if self.batch_norm_between_layers and i < len(self.flows) - 1:
+                bn = self.batch_norms[i]
+                z = self._apply_batch_norm(bn, z)
+                log_det_jacobian_sum += self._batch_norm_log_det_jacobian(bn, z)
+        return z, log_det_jacobian_sum
+
+    def inverse(self, x):
+        if self._hip_chain_ok(x):
+            return self._hip_chain(x, -1)
+        log_det_jacobian_sum = 0
+        for i, flow in reversed(list(enumerate(self.flows))):
+            if self.batch_norm_between_layers and i < len(self.flows) - 1:
+                bn = self.batch_norms[i]
+                x = self._inverse_batch_norm(bn, x)
+                log_det_jacobian_sum -= self._batch_norm_log_det_jacobian(bn, x)
+            x, log_det_jacobian = flow.inverse(x)
+            log_det_jacobian_sum += log_det_jacobian
+        return x, log_det_jacobian_sum
+
+    # -- between-layer BatchNorm (normalizing_flow_model.py:67-128) ----------------------------
+    def _apply_batch_norm(self, bn_layer, x):
+        if self.training:
+            with torch.no_grad():
+                momentum = bn_layer.momentum if bn_layer.momentum is not None else 0.1
+                bn_layer.running_mean.mul_(1 - momentum).add_(momentum * x.mean(dim=0))
+                bn_layer.running_var.mul_(1 - momentum).add_(momentum * x.var(dim=0, unbiased=False))
+        gamma = bn_layer.weight.view(1, -1)
+        beta = bn_layer.bias.view(1, -1)
+        mean = bn_layer.running_mean.view(1, -1)
+        var = bn_layer.running_var.view(1, -1)
+        return (x - mean) / torch.sqrt(var + bn_layer.eps) * gamma + beta
+
+    def _batch_norm_log_det_jacobian(self, bn_layer, x):
+        log_det_per_dim = torch.log(torch.abs(bn_layer.weight)) - 0.5 * torch.log(bn_layer.running_var + bn_layer.eps)
+        return log_det_per_dim.sum()
+
+    def _inverse_batch_norm(self, bn_layer, y):
+        gamma = bn_layer.weight.view(1, -1)
+        beta = bn_layer.bias.view(1, -1)
+        mean = bn_layer.running_mean.view(1, -1)
+        var = bn_layer.running_var.view(1, -1)
+        return (y - beta) / gamma * torch.sqrt(var + bn_layer.eps) + mean
+
+    # -- gfx950 chain ----------------------------------------------------------------------
+    def _needs_grad(self, x):
+        if not torch.is_grad_enabled():
+            return False
+        return x.requires_grad or any(p.requires_grad for p in self.parameters())
+
+    def _hip_chain_ok(self, x):
+        if x.device.type != "cuda" or x.dtype != torch.float32 or x.dim() != 2:
+            return False
+        if self._needs_grad(x):
+            return False  # per-layer autograd Functions handle gradients
+        for f in self.flows:
+            if not isinstance(f, HipFlow) or f._route(x) != "hip":
+                return False
+        return True
+
+    def _hip_chain(self, x, direction):
+        x = x.contiguous()
+        B = x.shape[0]
+        ld = torch.empty(B, device=x.device, dtype=torch.float32)
+        bufs = [torch.empty_like(x), torch.empty_like(x)]
+        n = len(self.flows)
+        order = range(n) if direction > 0 else reversed(range(n))
+        cur, k, first = x, 0, True
+        for i in order:
+            if direction < 0 and self.batch_norm_between_layers and i < n - 1:
+                bn = self.batch_norms[i]
+                cur = self._inverse_batch_norm(bn, cur).contiguous()
+                if first:
+                    ld.zero_()
+                    first = False
+                ld.sub_(self._batch_norm_log_det_jacobian(bn, cur))
+            out = bufs[k]
+            if out is cur:
+                k ^= 1
+                out = bufs[k]
+            ev = self.layer_events
+            if ev is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            self.flows[i]._hip_launch_counted(cur, out, ld, direction, accumulate=not first)
+            if ev is not None:
+                e1.record()
+                ev.append((type(self.flows[i]).__name__, e0, e1))
+            first = False
+            cur, k = out, k ^ 1
+            if direction > 0 and self.batch_norm_between_layers and i < n - 1:
+                bn = self.batch_norms[i]
+                cur = self._apply_batch_norm(bn, cur).contiguous()
+                ld.add_(self._batch_norm_log_det_jacobian(bn, cur))
+        return cur, ld
+
+    # -- log-density -------------------------------------------------------------------------
+    def log_prob(self, x, return_sums=False):
+        """log p(x) = log N(z; 0, I) + log|det J_inv| per sample, z = inverse(x).
+
+        With return_sums=True also returns a float64 tensor [sum_i log p(x_i), B] on x's device
+        (the partial a data-parallel NLL all-reduces)."""
+        z, ld = self.inverse(x)
+        if z.device.type == "cuda" and z.dtype == torch.float32 and not self._needs_grad(x):
+            logp, sums = gauss_logprob(z, ld)
+        else:
+            d = z.shape[1]
+            logp = -0.5 * (d * math.log(2 * math.pi) + z.pow(2).sum(-1)) + ld
+            sums = torch.stack([logp.detach().double().sum(),
+                                torch.tensor(float(z.shape[0]), dtype=torch.float64, device=z.device)])
+        return (logp, sums) if return_sums else logp
+
+    def nll(self, x):
+        """Mean negative log-likelihood, accumulated in float64 (python float)."""
+        _, sums = self.log_prob(x, return_sums=True)
+        s = sums.cpu()
+        return -(s[0] / s[1]).item()
+
+
+def gauss_logprob(z, ld, logp=None):
+    """Fused `MultivariateNormal(0,I).log_prob(z) + ld` and float64 [sum, count] (nfx_gauss_logprob)."""
+    z = z.contiguous()
+    B, d = z.shape
+    if logp is None:
+        logp = torch.empty(B, device=z.device, dtype=torch.float32)
+    sums = torch.empty(2, device=z.device, dtype=torch.float64)
+    L = _lib.lib()
+    ws = torch.empty(L.nfx_gauss_workspace_bytes(B), device=z.device, dtype=torch.uint8)
+    _lib.check(L.nfx_gauss_logprob(_lib.ptr(z), _lib.ptr(ld), _lib.ptr(logp), _lib.ptr(sums),
+                                   _lib.ptr(ws), B, d, _lib.stream_of(z)), "nfx_gauss_logprob")
+    STATS["hip"] += 1
+    return logp, sums

@@ -1,0 +1,34 @@
+"""RealNVP — drop-in for src/models/real_nvp.py:6-49 (stack of affine CouplingLayers)."""
+import torch
+import torch.nn as nn
+
+from ..flows.coupling import CouplingLayer
+from .normalizing_flow_model import NormalizingFlowModel
+
+
+class RealNVP(nn.Module):
+    def __init__(self, data_dim, n_layers, hidden_dim, batch_norm_between_layers=False):
+        super().__init__()
+        assert n_layers % 2 == 0, "Number of layers must be even to ensure all dimensions are transformed."
+        layers = []
+        for i in range(n_layers):
+            # real_nvp.py:27-31: even layers condition on the first half, odd on the second
+            mask = torch.zeros(data_dim)
+            if i % 2 == 0:
+                mask[:data_dim // 2] = 1
+            else:
+                mask[data_dim // 2:] = 1
+            layers.append(CouplingLayer(data_dim, hidden_dim, mask))
+        self.flow = NormalizingFlowModel(layers, batch_norm_between_layers)
+
+    def forward(self, z):
+        return self.flow.forward(z)
+
+    def inverse(self, x):
+        return self.flow.inverse(x)
+
+    def log_prob(self, x, return_sums=False):
+        return self.flow.log_prob(x, return_sums=return_sums)
+
+    def nll(self, x):
+        return self.flow.nll(x)

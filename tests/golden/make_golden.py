@@ -1,0 +1,351 @@
+"""Generate the golden parity fixtures from the REFERENCE implementation itself.
+
+Runs only in the build container (needs /root/reference; never on the GPU box):
+
+    python tests/golden/make_golden.py [--skip-full]
+
+It imports itxtx/normalizing-flows-study from /root/reference (a stub `torchdiffeq` module is
+injected in-process because the continuous-flow package imports it at package import time; no
+hot-path code calls it), builds the reference modules with fixed seeds, perturbs their weights so
+no layer is the identity, runs them on seeded inputs, and writes plain arrays:
+
+  g1_made_masks.npz   MADE degrees/masks (uint8) for the (d, H) pairs of SURVEY §8(c) G1
+  g2_realnvp.npz      RealNVP(2,8,64) eval: inverse/forward/log_prob on 4,096 rows (+ edge rows)
+  g3_spline.npz       8x SplineCouplingLayer(2,64,K=8) and RealNVPSpline(2,8,64) (K=10)
+  g4_rqs_unit.npz     rational_quadratic_spline, N=4,096, K=8, both directions
+  g5_maf63.npz        5x MAF(63,64): inverse 1,024 rows, forward 128 rows
+  g6_iaf784.npz       IAF(784,64): forward 64 rows, inverse 16 rows
+  g7_moons.npz        config 1: two-moons 5k, RealNVP(2,8,64) trained 45 steps, eval log_prob/NLL
+  g9_small.npz        d=4/H=16 layers of the reference's own tests (+ MAF/IAF d=10)
+  g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes
+
+Each npz holds the module's state_dict arrays under their reference keys (prefixed per case),
+inputs and expected outputs. Nothing pickled; load with numpy.load(allow_pickle=False).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = os.environ.get("NFS_REFERENCE", "/root/reference")
+
+
+def import_reference():
+    stub = types.ModuleType("torchdiffeq")
+
+    def odeint(*a, **k):
+        raise RuntimeError("torchdiffeq is not installed (stub for the reference import)")
+
+    stub.odeint = odeint
+    sys.modules.setdefault("torchdiffeq", stub)
+    sys.dont_write_bytecode = True
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import src.flows as flows  # noqa: F401
+    import src.models as models  # noqa: F401
+    return sys.modules["src.flows"], sys.modules["src.models"]
+
+
+def perturb(module, sigma, seed):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            p.add_(sigma * torch.randn(p.shape, generator=g))
+        for name, mod in module.named_modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.copy_(0.1 * torch.randn(mod.running_mean.shape, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(mod.running_var.shape, generator=g))
+
+
+def sd_arrays(module, prefix):
+    out = {}
+    for k, v in module.state_dict().items():
+        if v.dtype == torch.int64:  # num_batches_tracked
+            continue
+        out[prefix + k] = v.detach().cpu().numpy()
+    return out
+
+
+def edge_rows(d):
+    vals = [0.0, 1e-6, -1e-6, 1e3, -1e3, 1e10, -1e10, 5.0, -5.0, 4.9999, -4.9999, 5.0001, -5.0001, 10.0, -10.0]
+    rows = []
+    for v in vals:
+        rows.append([v] * d)
+        r = [0.3] * d
+        r[0] = v
+        rows.append(r)
+        r = [-0.7] * d
+        r[-1] = v
+        rows.append(r)
+    return torch.tensor(rows, dtype=torch.float32)
+
+
+def mvn_logp(z, ld):
+    from torch.distributions import MultivariateNormal
+    d = z.shape[1]
+    base = MultivariateNormal(torch.zeros(d), torch.eye(d))
+    return base.log_prob(z) + ld
+
+
+def run_model(model, x_inv, z_fwd):
+    with torch.no_grad():
+        zi, ldi = model.inverse(x_inv)
+        xf, ldf = model.forward(z_fwd)
+        lp = mvn_logp(zi, ldi)
+    return {"inv_z": zi.numpy(), "inv_ld": ldi.numpy(), "fwd_x": xf.numpy(), "fwd_ld": ldf.numpy(),
+            "log_prob": lp.numpy(), "nll_f64": np.float64(-lp.double().mean().item())}
+
+
+def g1(flows):
+    MADE = flows.MADE
+    out = {}
+    for d, H in [(1, 8), (2, 64), (3, 16), (3, 32), (4, 16), (5, 16), (10, 16), (63, 64), (154, 64), (784, 64)]:
+        m = MADE(d, H)
+        out[f"d{d}_h{H}_deg"] = np.asarray(m.m[0], dtype=np.int32)
+        out[f"d{d}_h{H}_m1"] = m.masks[0].numpy().astype(np.uint8)
+        out[f"d{d}_h{H}_mhh"] = m.masks[1].numpy().astype(np.uint8)
+        out[f"d{d}_h{H}_m2"] = m.masks[2].numpy().astype(np.uint8)
+    np.savez_compressed(os.path.join(HERE, "g1_made_masks.npz"), **out)
+
+
+def moons(n, noise, rs):
+    from sklearn.datasets import make_moons
+    X, _ = make_moons(n_samples=n, noise=noise, random_state=rs)
+    return torch.FloatTensor(X)
+
+
+def g2(models):
+    torch.manual_seed(0)
+    m = models.RealNVP(2, 8, 64)
+    perturb(m, 0.1, 1)
+    m.eval()
+    g = torch.Generator().manual_seed(2)
+    x = torch.cat([moons(2048, 0.05, 42), torch.randn(2000, 2, generator=g), edge_rows(2)])
+    z = torch.randn(4096, 2, generator=g)
+    out = sd_arrays(m, "")
+    out.update({"x": x.numpy(), "z": z.numpy()})
+    out.update(run_model(m, x, z))
+    with torch.no_grad():
+        l0 = m.flow.flows[0]
+        zi, ldi = l0.inverse(x)
+        xf, ldf = l0.forward(z)
+    out.update({"l0_inv_z": zi.numpy(), "l0_inv_ld": ldi.numpy(), "l0_fwd_x": xf.numpy(), "l0_fwd_ld": ldf.numpy()})
+    np.savez_compressed(os.path.join(HERE, "g2_realnvp.npz"), **out)
+    return m
+
+
+def spline_stack(flows, models, d, H, K, n_layers, seed):
+    torch.manual_seed(seed)
+    layers = []
+    for i in range(n_layers):
+        mask = torch.zeros(d)
+        if i % 2 == 0:
+            mask[:d // 2] = 1
+        else:
+            mask[d // 2:] = 1
+        layers.append(flows.SplineCouplingLayer(d, H, mask, num_bins=K))
+    return models.NormalizingFlowModel(layers)
+
+
+def g3(flows, models):
+    m = spline_stack(flows, models, 2, 64, 8, 8, 10)
+    perturb(m, 0.1, 11)
+    m.eval()
+    g = torch.Generator().manual_seed(12)
+    x = torch.cat([moons(2048, 0.05, 42), torch.randn(2000, 2, generator=g) * 2.0, edge_rows(2)])
+    z = torch.randn(4096, 2, generator=g)
+    out = sd_arrays(m, "k8.")
+    out.update({"x": x.numpy(), "z": z.numpy()})
+    out.update({"k8." + k: v for k, v in run_model(m, x, z).items()})
+    torch.manual_seed(13)
+    m10 = models.RealNVPSpline(2, 8, 64)
+    perturb(m10, 0.1, 14)
+    m10.eval()
+    out.update(sd_arrays(m10, "k10."))
+    out.update({"k10." + k: v for k, v in run_model(m10, x, z).items()})
+    np.savez_compressed(os.path.join(HERE, "g3_spline.npz"), **out)
+    return m
+
+
+def g4(flows):
+    rqs = flows.rational_quadratic_spline
+    g = torch.Generator().manual_seed(20)
+    N, K = 4096, 8
+    uw = 1.5 * torch.randn(N, K, generator=g)
+    uh = 1.5 * torch.randn(N, K, generator=g)
+    ud = 1.5 * torch.randn(N, K - 1, generator=g)
+    x = torch.rand(N, generator=g) * 1.4 - 0.2
+    x[:8] = torch.tensor([0.0, 1.0, 0.5, -0.1, 1.1, 1e-7, 1 - 1e-7, 2.0])
+    yf, lf = rqs(x, uw, uh, ud, inverse=False)
+    yi, li = rqs(x, uw, uh, ud, inverse=True)
+    np.savez_compressed(os.path.join(HERE, "g4_rqs_unit.npz"), x=x.numpy(), uw=uw.numpy(), uh=uh.numpy(),
+                        ud=ud.numpy(), fwd_y=yf.numpy(), fwd_ld=lf.numpy(), inv_y=yi.numpy(), inv_ld=li.numpy())
+
+
+def maf_stack(flows, models, d, H, n, seed):
+    torch.manual_seed(seed)
+    return models.NormalizingFlowModel([flows.MaskedAutoregressiveFlow(d, H) for _ in range(n)])
+
+
+def g5(flows, models):
+    m = maf_stack(flows, models, 63, 64, 5, 30)
+    perturb(m, 0.02, 31)
+    m.eval()
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(1024, 63, generator=g)
+    z = torch.randn(128, 63, generator=g)
+    out = sd_arrays(m, "")
+    out.update({"x": x.numpy(), "z": z.numpy()})
+    with torch.no_grad():
+        zi, ldi = m.inverse(x)
+        xf, ldf = m.forward(z)
+        lp = mvn_logp(zi, ldi)
+    out.update({"inv_z": zi.numpy(), "inv_ld": ldi.numpy(), "fwd_x": xf.numpy(), "fwd_ld": ldf.numpy(),
+                "log_prob": lp.numpy(), "nll_f64": np.float64(-lp.double().mean().item())})
+    np.savez_compressed(os.path.join(HERE, "g5_maf63.npz"), **out)
+    return m
+
+
+def g6(flows):
+    torch.manual_seed(40)
+    f = flows.InverseAutoregressiveFlow(784, 64)
+    perturb(f, 0.01, 41)
+    f.eval()
+    g = torch.Generator().manual_seed(42)
+    z = torch.randn(64, 784, generator=g)
+    x = torch.randn(16, 784, generator=g)
+    with torch.no_grad():
+        xf, ldf = f.forward(z)
+        zi, ldi = f.inverse(x)
+    out = sd_arrays(f, "")
+    out.update({"z": z.numpy(), "x": x.numpy(), "fwd_x": xf.numpy(), "fwd_ld": ldf.numpy(),
+                "inv_z": zi.numpy(), "inv_ld": ldi.numpy()})
+    np.savez_compressed(os.path.join(HERE, "g6_iaf784.npz"), **out)
+    return f
+
+
+def g7(models, src_utils):
+    data = src_utils.get_two_moons_data(n_samples=5000, noise=0.05)
+    from torch.distributions import MultivariateNormal
+    base = MultivariateNormal(torch.zeros(2), torch.eye(2))
+    torch.manual_seed(0)
+    m = models.RealNVP(data_dim=2, n_layers=8, hidden_dim=64)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    curve = []
+    for epoch in range(45):  # README.md:111-117 quickstart loop; stopped at 45 steps, before the
+        # reference's train-mode-BN run diverges (NLL 1.16 at step 40, a 2e13 spike at step 50, 9.0 by step 300)
+        z, log_det = m.inverse(data)
+        loss = -(base.log_prob(z) + log_det).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        curve.append(loss.item())
+    m.eval()
+    with torch.no_grad():
+        z, ld = m.inverse(data)
+        lp = base.log_prob(z) + ld
+    out = sd_arrays(m, "")
+    out.update({"x": data.numpy(), "inv_z": z.numpy(), "inv_ld": ld.numpy(), "log_prob": lp.numpy(),
+                "nll_f64": np.float64(-lp.double().mean().item()), "train_curve": np.asarray(curve, np.float32)})
+    np.savez_compressed(os.path.join(HERE, "g7_moons.npz"), **out)
+
+
+def g9(flows, models):
+    """Small layers exactly as the reference's own correctness tests build them (d=4, H=16)."""
+    def create_mask(dim, kind):
+        mask = torch.zeros(dim)
+        if kind == "alternating":
+            mask[::2] = 1
+        else:
+            mask[:dim // 2] = 1
+        return mask
+
+    out = {}
+    g = torch.Generator().manual_seed(50)
+    cases = [
+        ("cpl_alt", lambda: flows.CouplingLayer(4, 16, create_mask(4, "alternating")), 0.1),
+        ("cpl_half", lambda: flows.CouplingLayer(4, 16, create_mask(4, "half")), 0.1),
+        ("cpl_d3", lambda: flows.CouplingLayer(3, 16, create_mask(3, "alternating")), 0.1),
+        ("cpl_d1", lambda: flows.CouplingLayer(1, 16, create_mask(1, "alternating")), 0.1),
+        ("spl_alt", lambda: flows.SplineCouplingLayer(4, 16, create_mask(4, "alternating")), 0.1),
+        ("spl_half", lambda: flows.SplineCouplingLayer(4, 16, create_mask(4, "half")), 0.1),
+        ("spl_d3", lambda: flows.SplineCouplingLayer(3, 16, create_mask(3, "alternating")), 0.1),
+        ("maf4", lambda: flows.MaskedAutoregressiveFlow(4, 16), 0.05),
+        ("iaf4", lambda: flows.InverseAutoregressiveFlow(4, 16), 0.05),
+        ("maf10", lambda: flows.MaskedAutoregressiveFlow(10, 16), 0.05),
+        ("iaf10", lambda: flows.InverseAutoregressiveFlow(10, 16), 0.05),
+        ("maf2", lambda: flows.MaskedAutoregressiveFlow(2, 64), 0.05),
+        ("iaf3", lambda: flows.InverseAutoregressiveFlow(3, 32), 0.05),
+    ]
+    for i, (name, ctor, sigma) in enumerate(cases):
+        torch.manual_seed(100 + i)
+        f = ctor()
+        perturb(f, sigma, 200 + i)
+        f.eval()
+        d = f.data_dim
+        x = torch.cat([torch.randn(61, d, generator=g), torch.zeros(1, d), torch.full((1, d), 3.0),
+                       torch.full((1, d), -6.0)])
+        with torch.no_grad():
+            yf, lf = f.forward(x)
+            yi, li = f.inverse(x)
+        out.update(sd_arrays(f, name + "."))
+        out.update({name + ".x": x.numpy(), name + ".fwd_y": yf.numpy(), name + ".fwd_ld": lf.numpy(),
+                    name + ".inv_y": yi.numpy(), name + ".inv_ld": li.numpy()})
+    np.savez_compressed(os.path.join(HERE, "g9_small.npz"), **out)
+
+
+def g8(m2, m3, m5):
+    """Full-scale NLL scalars (float64 mean of the reference's fp32 log_prob)."""
+    torch.set_num_threads(8)
+    res = {}
+
+    def run(name, model, B, d, seed, chunk):
+        x = torch.randn(B, d, generator=torch.Generator().manual_seed(seed))
+        t0 = time.time()
+        tot = 0.0
+        with torch.no_grad():
+            for s in range(0, B, chunk):
+                z, ld = model.inverse(x[s:s + chunk])
+                tot += mvn_logp(z, ld).double().sum().item()
+        res[name] = {"B": B, "d": d, "seed": seed, "input_sum_f64": float(x.double().sum()),
+                     "input_head": [float(v) for v in x.view(-1)[:8]], "nll_f64": -tot / B,
+                     "ref_seconds": time.time() - t0}
+        print(name, res[name], flush=True)
+
+    run("cfg2_realnvp_d2_B1M", m2, 1_000_000, 2, 1234, 1_000_000)
+    run("cfg3_spline_k8_d2_B1M", m3, 1_000_000, 2, 1235, 1_000_000)
+    run("cfg4_maf_d63_B4M", m5, 4_000_000, 63, 1236, 500_000)
+    res["_meta"] = {"torch": torch.__version__, "numpy": np.__version__,
+                    "input": "torch.randn(B, d, generator=torch.Generator().manual_seed(seed)) on CPU",
+                    "weights": "g2_realnvp.npz / g3_spline.npz (k8.) / g5_maf63.npz"}
+    with open(os.path.join(HERE, "g8_full_nll.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-full", action="store_true")
+    a = ap.parse_args()
+    flows, models = import_reference()
+    import src.utils as src_utils
+    g1(flows)
+    m2 = g2(models)
+    m3 = g3(flows, models)
+    g4(flows)
+    m5 = g5(flows, models)
+    g6(flows)
+    g7(models, src_utils)
+    g9(flows, models)
+    if not a.skip_full:
+        g8(m2, m3, m5)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

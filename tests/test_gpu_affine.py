@@ -1,0 +1,193 @@
+"""GPU parity of the fused affine-coupling kernel (csrc/nfx_affine*.hip) through the C-ABI.
+
+Checks against (a) the reference's own outputs (golden fixtures, tests/golden/) and (b) the CPU
+oracle on the same seeded inputs, including ragged batches, B=0 and non-finite inputs.
+Tolerances: per-sample z/x |d| <= 1e-5 * (1 + |ref|); log-det <= 1e-4 (d=2);
+NLL <= 1e-5 absolute.
+"""
+import numpy as np
+import pytest
+import torch
+
+import nfs_amd
+import oracle
+from conftest import golden_json, load_golden, oracle_sd, state_dict_from
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_y(y, ref, tol=1e-5):
+    y, ref = np.asarray(y, np.float64), np.asarray(ref, np.float64)
+    err = np.abs(y - ref) / (1 + np.abs(ref))
+    assert err.max() <= tol, f"max rel err {err.max():.3g} at {np.unravel_index(err.argmax(), err.shape)}"
+
+
+def assert_ld(ld, ref, tol=1e-4):
+    d = np.abs(np.asarray(ld, np.float64) - np.asarray(ref, np.float64))
+    assert d.max() <= tol, f"max |dld| {d.max():.3g} at {d.argmax()}"
+
+
+def assert_lp(lp, ref):
+    """log p = -0.5|z|^2 + ...: huge for the 1e3/1e10 edge rows, so the bound is relative there."""
+    lp, ref = np.asarray(lp, np.float64), np.asarray(ref, np.float64)
+    bad = np.abs(lp - ref) > 1e-4 + 2e-5 * np.abs(ref)
+    assert not bad.any(), f"log_prob mismatch at {np.flatnonzero(bad)[:5]}: {lp[bad][:5]} vs {ref[bad][:5]}"
+
+
+N_REGULAR = 4048  # g2/g3 rows before the 45 edge rows (|x| up to 1e10)
+
+
+def realnvp_from_golden(dev, name="g2_realnvp.npz"):
+    g = load_golden(name)
+    m = nfs_amd.RealNVP(2, 8, 64)
+    m.load_state_dict(state_dict_from(g, "", m))
+    return m.to(dev).eval(), g
+
+
+def test_layer0_inverse_forward(cuda_device):
+    m, g = realnvp_from_golden(cuda_device)
+    layer = m.flow.flows[0]
+    nfs_amd.reset_stats()
+    with torch.no_grad():
+        zi, ldi = layer.inverse(torch.from_numpy(g["x"]).to(cuda_device))
+        xf, ldf = layer.forward(torch.from_numpy(g["z"]).to(cuda_device))
+    assert nfs_amd.STATS["hip"] == 2 and nfs_amd.STATS["torch"] == 0
+    assert_y(zi.cpu(), g["l0_inv_z"])
+    assert_ld(ldi.cpu(), g["l0_inv_ld"])
+    assert_y(xf.cpu(), g["l0_fwd_x"])
+    assert_ld(ldf.cpu(), g["l0_fwd_ld"])
+
+
+def test_realnvp_model_vs_reference(cuda_device):
+    m, g = realnvp_from_golden(cuda_device)
+    x = torch.from_numpy(g["x"]).to(cuda_device)
+    z = torch.from_numpy(g["z"]).to(cuda_device)
+    nfs_amd.reset_stats()
+    with torch.no_grad():
+        zi, ldi = m.inverse(x)
+        xf, ldf = m.forward(z)
+        lp, sums = m.log_prob(x, return_sums=True)
+    assert nfs_amd.STATS["torch"] == 0
+    assert_y(zi.cpu(), g["inv_z"])
+    assert_ld(ldi.cpu(), g["inv_ld"])
+    assert_y(xf.cpu(), g["fwd_x"])
+    assert_ld(ldf.cpu(), g["fwd_ld"])
+    assert_lp(lp.cpu(), g["log_prob"])
+    assert float(sums[1]) == x.shape[0]
+    nll = -float(lp[:N_REGULAR].double().mean())
+    assert abs(nll - (-g["log_prob"][:N_REGULAR].astype(np.float64).mean())) <= 1e-5
+
+
+def test_moons_config1(cuda_device):
+    """Config 1 (two-moons 5k, trained RealNVP) log_prob / NLL vs the reference."""
+    m, g = realnvp_from_golden(cuda_device, "g7_moons.npz")
+    with torch.no_grad():
+        lp = m.log_prob(torch.from_numpy(g["x"]).to(cuda_device))
+    assert_lp(lp.cpu(), g["log_prob"])
+    assert abs(-float(lp.double().mean()) - float(g["nll_f64"])) <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["cpl_alt", "cpl_half", "cpl_d3", "cpl_d1"])
+def test_small_coupling_layers(cuda_device, name):
+    """d in {1,3,4}, H=16 (padded to one 32-row MFMA tile) as in the reference's own tests."""
+    g = load_golden("g9_small.npz")
+    sd = oracle_sd(g, name + ".")
+    d = sd["mask"].numel()
+    layer = nfs_amd.CouplingLayer(d, 16, sd["mask"].clone())
+    layer.load_state_dict(state_dict_from(g, name + ".", layer))
+    layer = layer.to(cuda_device).eval()
+    x = torch.from_numpy(g[name + ".x"]).to(cuda_device)
+    with torch.no_grad():
+        yf, lf = layer.forward(x)
+        yi, li = layer.inverse(x)
+    assert_y(yf.cpu(), g[name + ".fwd_y"])
+    assert_ld(lf.cpu(), g[name + ".fwd_ld"])
+    assert_y(yi.cpu(), g[name + ".inv_y"])
+    assert_ld(li.cpu(), g[name + ".inv_ld"])
+
+
+@pytest.mark.parametrize("B", [1, 31, 63, 64, 65, 1000, 4097])
+def test_ragged_batches_vs_oracle(cuda_device, B):
+    m, _ = realnvp_from_golden(cuda_device)
+    x = torch.randn(B, 2, generator=torch.Generator().manual_seed(B)) * 1.5
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        zi, ldi = m.inverse(x.to(cuda_device))
+        zr, ldr = oracle.flow_model(sd, oracle.realnvp_spec(8), x, -1)
+        xf, ldf = m.forward(x.to(cuda_device))
+        xr, lfr = oracle.flow_model(sd, oracle.realnvp_spec(8), x, 1)
+    assert_y(zi.cpu(), zr)
+    assert_ld(ldi.cpu(), ldr)
+    assert_y(xf.cpu(), xr)
+    assert_ld(ldf.cpu(), lfr)
+
+
+def test_empty_batch(cuda_device):
+    m, _ = realnvp_from_golden(cuda_device)
+    with torch.no_grad():
+        z, ld = m.inverse(torch.empty(0, 2, device=cuda_device))
+        lp, sums = m.log_prob(torch.empty(0, 2, device=cuda_device), return_sums=True)
+    assert z.shape == (0, 2) and ld.shape == (0,) and lp.shape == (0,)
+    assert float(sums[1]) == 0.0
+
+
+def test_nonfinite_inputs_follow_reference_guards(cuda_device):
+    """inf/NaN inputs: the reference's clamp (NaN-propagating), 0*inf=NaN masking and the
+    NaN/Inf -> 0 guards must come out identical (single layer, so no float drift)."""
+    m, _ = realnvp_from_golden(cuda_device)
+    layer = m.flow.flows[0]
+    inf, nan = float("inf"), float("nan")
+    x = torch.tensor([[inf, 0.5], [0.5, inf], [-inf, 1.0], [nan, 0.1], [0.2, nan], [1e38, 1e38],
+                      [3e38, -3e38], [0.0, 0.0]], dtype=torch.float32)
+    sd = {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+    for direction in (1, -1):
+        with torch.no_grad():
+            yg, lg = (layer.forward if direction > 0 else layer.inverse)(x.to(cuda_device))
+            yr, lr = oracle.coupling(sd, "", x, direction)
+        yg, lg = yg.cpu().numpy(), lg.cpu().numpy()
+        assert np.array_equal(np.isfinite(yg), np.isfinite(yr.numpy()))
+        assert_y(yg, yr.numpy())
+        assert_ld(lg, lr.numpy())
+
+
+def test_autograd_through_hip_forward(cuda_device):
+    """Eval-mode gradients: HIP forward + composite backward == CPU composite gradients."""
+    m, _ = realnvp_from_golden(cuda_device)
+    layer = m.flow.flows[1]
+    x = torch.randn(256, 2, generator=torch.Generator().manual_seed(3))
+    xg = x.to(cuda_device).requires_grad_(True)
+    y, ld = layer.inverse(xg)
+    (y.sum() + ld.sum()).backward()
+    cpu_layer = nfs_amd.CouplingLayer(2, 64, layer.mask.cpu().clone())
+    cpu_layer.load_state_dict({k: v.cpu() for k, v in layer.state_dict().items()})
+    cpu_layer.eval()
+    xc = x.clone().requires_grad_(True)
+    yc, lc = cpu_layer.inverse(xc)
+    (yc.sum() + lc.sum()).backward()
+    np.testing.assert_allclose(xg.grad.cpu().numpy(), xc.grad.numpy(), rtol=1e-4, atol=1e-4)
+    for (n, p), (_, q) in zip(layer.named_parameters(), cpu_layer.named_parameters()):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), q.grad.numpy(), rtol=1e-3, atol=1e-3, err_msg=n)
+
+
+def test_weight_update_invalidates_pack(cuda_device):
+    m, _ = realnvp_from_golden(cuda_device)
+    layer = m.flow.flows[0]
+    x = torch.randn(128, 2, device=cuda_device)
+    with torch.no_grad():
+        y0, _ = layer.inverse(x)
+        layer.s_net[6].weight.mul_(0.5)
+        y1, _ = layer.inverse(x)
+        sd = {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+        yr, _ = oracle.coupling(sd, "", x.cpu(), -1)
+    assert not torch.equal(y0, y1)
+    assert_y(y1.cpu(), yr)
+
+
+def test_full_scale_nll_cfg2(cuda_device):
+    """BASELINE cfg2 at its full size: RealNVP(2,8,64), B=1M, NLL vs the reference (G8)."""
+    meta = golden_json("g8_full_nll.json")["cfg2_realnvp_d2_B1M"]
+    x = torch.randn(meta["B"], meta["d"], generator=torch.Generator().manual_seed(meta["seed"]))
+    assert abs(float(x.double().sum()) - meta["input_sum_f64"]) < 1e-6
+    m, _ = realnvp_from_golden(cuda_device)
+    nll = m.nll(x.to(cuda_device))
+    assert abs(nll - meta["nll_f64"]) <= 1e-5, (nll, meta["nll_f64"])

@@ -1,0 +1,144 @@
+"""Pin the oracle (oracle/flows_ref.py) against golden vectors produced by the reference itself
+(tests/golden/make_golden.py). The oracle restates the reference op for op on the same ATen CPU
+kernels, so agreement is (near-)bitwise; tolerances below allow a few ulp."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden, oracle_sd
+
+T = dict(rtol=1e-6, atol=1e-6)
+
+
+def close(a, b, **kw):
+    kw = kw or T
+    np.testing.assert_allclose(np.asarray(a), np.asarray(b), **kw)
+
+
+@pytest.mark.parametrize("dH", [(1, 8), (2, 64), (3, 16), (3, 32), (4, 16), (5, 16), (10, 16),
+                                (63, 64), (154, 64), (784, 64)])
+def test_made_masks_bit_exact(dH):
+    d, H = dH
+    g = load_golden("g1_made_masks.npz")
+    assert oracle.made_degrees(d, H) == g[f"d{d}_h{H}_deg"].tolist()
+    m1, mhh, m2 = oracle.made_masks(d, H)
+    assert np.array_equal(m1.numpy(), g[f"d{d}_h{H}_m1"])
+    assert np.array_equal(mhh.numpy(), g[f"d{d}_h{H}_mhh"])
+    assert np.array_equal(m2.numpy(), g[f"d{d}_h{H}_m2"])
+
+
+def test_made_degrees_linspace_sweep():
+    """The float64 restatement equals numpy.linspace flooring over a wide (d, H) sweep, where
+    the integer form i*(d-1)//(H-1) is known to fail."""
+    for d in range(3, 800, 7):
+        for H in (8, 16, 32, 48, 64, 100, 128, 256):
+            ref = np.floor(np.linspace(0, d - 1, H)).astype(int).tolist()
+            assert oracle.made_degrees(d, H) == ref, (d, H)
+
+
+def test_realnvp_g2():
+    g = load_golden("g2_realnvp.npz")
+    sd = oracle_sd(g)
+    x, z = torch.from_numpy(g["x"]), torch.from_numpy(g["z"])
+    spec = oracle.realnvp_spec(8)
+    with torch.no_grad():
+        zi, ldi = oracle.flow_model(sd, spec, x, -1)
+        xf, ldf = oracle.flow_model(sd, spec, z, 1)
+        lp = oracle.gauss_log_prob(zi, ldi)
+    close(zi, g["inv_z"])
+    close(ldi, g["inv_ld"])
+    close(xf, g["fwd_x"])
+    close(ldf, g["fwd_ld"])
+    close(lp, g["log_prob"])
+    assert abs(oracle.nll_f64(lp) - float(g["nll_f64"])) < 1e-9
+    y0, l0 = oracle.coupling(sd, "flow.flows.0.", x, -1)
+    close(y0, g["l0_inv_z"])
+    close(l0, g["l0_inv_ld"])
+
+
+@pytest.mark.parametrize("tag,K", [("k8.", 8), ("k10.", 10)])
+def test_spline_g3(tag, K):
+    g = load_golden("g3_spline.npz")
+    sd = oracle_sd(g, tag)
+    x, z = torch.from_numpy(g["x"]), torch.from_numpy(g["z"])
+    spec = [("spline", f"{'flow.' if K == 10 else ''}flows.{i}.", {"K": K}) for i in range(8)]
+    with torch.no_grad():
+        zi, ldi = oracle.flow_model(sd, spec, x, -1)
+        xf, ldf = oracle.flow_model(sd, spec, z, 1)
+    close(zi, g[tag + "inv_z"])
+    close(ldi, g[tag + "inv_ld"], rtol=1e-6, atol=2e-6)
+    close(xf, g[tag + "fwd_x"])
+    close(ldf, g[tag + "fwd_ld"], rtol=1e-6, atol=2e-6)
+
+
+def test_rqs_unit_g4():
+    g = load_golden("g4_rqs_unit.npz")
+    x, uw, uh, ud = (torch.from_numpy(g[k]) for k in ("x", "uw", "uh", "ud"))
+    yf, lf = oracle.rqs_unit(x, uw, uh, ud, inverse=False)
+    yi, li = oracle.rqs_unit(x, uw, uh, ud, inverse=True)
+    close(yf, g["fwd_y"])
+    close(lf, g["fwd_ld"])
+    np.testing.assert_array_equal(np.isnan(yi.numpy()), np.isnan(g["inv_y"]))
+    close(np.nan_to_num(yi.numpy()), np.nan_to_num(g["inv_y"]))
+    close(np.nan_to_num(li.numpy()), np.nan_to_num(g["inv_ld"]))
+
+
+def test_maf63_g5():
+    g = load_golden("g5_maf63.npz")
+    sd = oracle_sd(g)
+    x, z = torch.from_numpy(g["x"]), torch.from_numpy(g["z"])
+    spec = oracle.maf_spec(5)
+    with torch.no_grad():
+        zi, ldi = oracle.flow_model(sd, spec, x, -1)
+        xf, ldf = oracle.flow_model(sd, spec, z, 1)
+    close(zi, g["inv_z"], rtol=1e-5, atol=1e-5)
+    close(ldi, g["inv_ld"], rtol=1e-5, atol=1e-4)
+    close(xf, g["fwd_x"], rtol=1e-5, atol=1e-5)
+    close(ldf, g["fwd_ld"], rtol=1e-5, atol=1e-4)
+
+
+def test_iaf784_g6():
+    g = load_golden("g6_iaf784.npz")
+    sd = oracle_sd(g)
+    z, x = torch.from_numpy(g["z"]), torch.from_numpy(g["x"])
+    with torch.no_grad():
+        xf, ldf = oracle.iaf(sd, "", z, 1)
+        zi, ldi = oracle.iaf(sd, "", x, -1)
+    close(xf, g["fwd_x"], rtol=1e-5, atol=1e-5)
+    close(ldf, g["fwd_ld"], rtol=1e-5, atol=1e-4)
+    close(zi, g["inv_z"], rtol=1e-5, atol=1e-5)
+    close(ldi, g["inv_ld"], rtol=1e-5, atol=1e-4)
+
+
+def test_moons_g7():
+    g = load_golden("g7_moons.npz")
+    sd = oracle_sd(g)
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        zi, ldi = oracle.flow_model(sd, oracle.realnvp_spec(8), x, -1)
+        lp = oracle.gauss_log_prob(zi, ldi)
+    close(lp, g["log_prob"], rtol=1e-5, atol=1e-5)
+    assert abs(oracle.nll_f64(lp) - float(g["nll_f64"])) < 1e-6
+    assert g["train_curve"][-1] < g["train_curve"][0]
+
+
+SMALL = [("cpl_alt", "coupling"), ("cpl_half", "coupling"), ("cpl_d3", "coupling"),
+         ("cpl_d1", "coupling"), ("spl_alt", "spline"), ("spl_half", "spline"),
+         ("spl_d3", "spline"), ("maf4", "maf"), ("iaf4", "iaf"), ("maf10", "maf"),
+         ("iaf10", "iaf"), ("maf2", "maf"), ("iaf3", "iaf")]
+
+
+@pytest.mark.parametrize("name,kind", SMALL)
+def test_small_layers_g9(name, kind):
+    g = load_golden("g9_small.npz")
+    sd = oracle_sd(g, name + ".")
+    x = torch.from_numpy(g[name + ".x"])
+    fn = {"coupling": oracle.coupling, "spline": oracle.spline_coupling, "maf": oracle.maf, "iaf": oracle.iaf}[kind]
+    with torch.no_grad():
+        yf, lf = fn(sd, "", x, 1)
+        yi, li = fn(sd, "", x, -1)
+    close(yf, g[name + ".fwd_y"], rtol=1e-5, atol=1e-5)
+    close(lf, g[name + ".fwd_ld"], rtol=1e-5, atol=1e-5)
+    close(yi, g[name + ".inv_y"], rtol=1e-5, atol=1e-5)
+    close(li, g[name + ".inv_ld"], rtol=1e-5, atol=1e-5)
