@@ -1,0 +1,182 @@
+// MADE affine flows: weight pack, sequential-kernel instantiations and the C-ABI.
+// Kernels: nfx_made_kernel.h (parallel instantiations in nfx_made_par.hip).
+#include "nfx_made_kernel.h"
+#include "nfx_pack.h"
+
+namespace nfx {
+
+// Degree of hidden unit a from the input->hidden mask: M1[a][j] = (j <= deg(a)) (made.py:56).
+__device__ inline int made_unit_degree(const NfxMlpRaw& net, int d, int a) {
+    if (!net.mask[0]) return 0;
+    int n = 0;
+    for (int j = 0; j < d; ++j) n += net.mask[0][(size_t)a * d + j] != 0.f ? 1 : 0;
+    return n - 1;
+}
+
+__global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
+    const int Hp = L.Hp, G1 = 4 * L.NKC;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
+        if (i >= L.s_deg + Hp) continue;  // completion-order tables are scattered below
+        float v = 0.f;
+        if (i < L.b1) {
+            int t = i - L.w1, rr = t & 3, lane = (t >> 2) & 63, g = (t >> 8) % G1, ht = (t >> 8) / G1;
+            int row = 32 * ht + (lane & 31), col = 2 * (4 * g + rr) + (lane >> 5);
+            v = (row < H && col < d) ? mlp_weight(net, 0, d, row, col) : 0.f;
+        } else if (i < L.w2) {
+            int t = i - L.b1, h = t & 1, r = (t >> 1) & 15, ht = t >> 5, row = 32 * ht + crow(r, h);
+            v = row < H ? mlp_bias(net, 0, row) : 0.f;
+        } else if (i < L.b2 || (i >= L.w3 && i < L.b3)) {
+            const int layer = i < L.b2 ? 1 : 2;
+            int t = i - (layer == 1 ? L.w2 : L.w3), rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+            int kt = (t >> 10) % HT, hto = (t >> 10) / HT;
+            int row = 32 * hto + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
+            v = (row < H && col < H) ? mlp_weight(net, layer, H, row, col) : 0.f;
+        } else if (i < L.w3 || (i >= L.b3 && i < L.w4)) {
+            const int layer = i < L.w3 ? 1 : 2;
+            int t = i - (layer == 1 ? L.b2 : L.b3), h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+            int row = 32 * ht + crow(r, h);
+            v = row < H ? mlp_bias(net, layer, row) : 0.f;
+        } else if (i < L.b4) {
+            int t = i - L.w4, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+            int kt = (t >> 10) % HT, jw = (t >> 10) / HT, which = jw & 1, j = jw >> 1;
+            int orow = 32 * j + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
+            v = (orow < d && col < H) ? mlp_weight(net, 3, H, which * d + orow, col) : 0.f;
+        } else if (i < L.par_total) {
+            int t = i - L.b4, h = t & 1, r = (t >> 1) & 15, jw = t >> 5, which = jw & 1, j = jw >> 1;
+            int orow = 32 * j + crow(r, h);
+            v = orow < d ? mlp_bias(net, 3, which * d + orow) : 0.f;
+        } else if (i < L.s_b1) {
+            int t = i - L.s_w1t, ii = t / Hp, a = t % Hp;
+            v = (ii < d && a < H) ? mlp_weight(net, 0, d, a, ii) : 0.f;
+        } else if (i < L.s_w2) {
+            int a = i - L.s_b1;
+            v = a < H ? mlp_bias(net, 0, a) : 0.f;
+        } else if (i < L.s_b2 || (i >= L.s_w3 && i < L.s_b3)) {
+            const int layer = i < L.s_b2 ? 1 : 2;
+            int t = i - (layer == 1 ? L.s_w2 : L.s_w3), a = t / Hp, b = t % Hp;
+            v = (a < H && b < H) ? mlp_weight(net, layer, H, a, b) : 0.f;
+        } else if (i < L.s_w3 || (i >= L.s_b3 && i < L.s_w4)) {
+            const int layer = i < L.s_w3 ? 1 : 2;
+            int a = i - (layer == 1 ? L.s_b2 : L.s_b3);
+            v = a < H ? mlp_bias(net, layer, a) : 0.f;
+        } else if (i < L.s_b4) {
+            int t = i - L.s_w4, row = t / Hp, a = t % Hp;
+            v = (row < 2 * d && a < H) ? mlp_weight(net, 3, H, row, a) : 0.f;
+        } else if (i < L.s_deg) {
+            int row = i - L.s_b4;
+            v = row < 2 * d ? mlp_bias(net, 3, row) : 0.f;
+        } else {
+            // unit a: degree, and its position in the stable by-degree completion order
+            const int a = i - L.s_deg;
+            const int da = a < H ? made_unit_degree(net, d, a) : 1000000000;
+            int rank = 0;
+            for (int b = 0; b < Hp; ++b) {
+                const int db = b < H ? made_unit_degree(net, d, b) : 1000000000;
+                rank += (db < da || (db == da && b < a)) ? 1 : 0;
+            }
+            packed[L.s_deg + Hp + rank] = (float)da;
+            packed[L.s_deg + 2 * Hp + rank] = (float)a;
+            v = (float)da;
+        }
+        packed[i] = v;
+    }
+}
+
+template <int HT, int VAR>
+static made_seq_kernel_t seq_var() {
+    return made_seq_kernel<HT, VAR>;
+}
+
+template <int HT>
+made_seq_kernel_t made_seq_pick_ht(int variant) {
+    return variant == NFX_MAF_FORWARD ? seq_var<HT, NFX_MAF_FORWARD>() : seq_var<HT, NFX_IAF_INVERSE>();
+}
+template made_seq_kernel_t made_seq_pick_ht<1>(int);
+template made_seq_kernel_t made_seq_pick_ht<2>(int);
+template made_seq_kernel_t made_seq_pick_ht<3>(int);
+template made_seq_kernel_t made_seq_pick_ht<4>(int);
+
+static made_par_kernel_t pick_par(int HT, bool wlds, int variant) {
+    switch (HT) {
+        case 1: return made_pick_ht<1>(wlds, variant);
+        case 2: return made_pick_ht<2>(wlds, variant);
+        case 3: return made_pick_ht<3>(wlds, variant);
+        case 4: return made_pick_ht<4>(wlds, variant);
+        default: return nullptr;
+    }
+}
+
+static made_seq_kernel_t pick_seq(int HT, int variant) {
+    switch (HT) {
+        case 1: return made_seq_pick_ht<1>(variant);
+        case 2: return made_seq_pick_ht<2>(variant);
+        case 3: return made_seq_pick_ht<3>(variant);
+        case 4: return made_seq_pick_ht<4>(variant);
+        default: return nullptr;
+    }
+}
+
+constexpr size_t kLdsBytes = 160 * 1024;
+
+}  // namespace nfx
+
+using namespace nfx;
+
+extern "C" size_t nfx_made_packed_floats(int d, int H) {
+    if (d <= 0 || H <= 0) return 0;
+    return (size_t)made_layout(d, (H + 31) / 32).total;
+}
+
+extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
+    if (!net || !packed) return set_error(NFX_EINVAL, "made_pack: null pointer");
+    if (d <= 0 || d > 4096 || H <= 0 || H > 128)
+        return set_error(NFX_EUNSUPPORTED, "made_pack: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (net->n_layers != 4) return set_error(NFX_EINVAL, "made_pack: MADE has 4 masked layers (got %d)", net->n_layers);
+    for (int l = 0; l < 4; ++l)
+        if (!net->w[l]) return set_error(NFX_EINVAL, "made_pack: layer %d weight is null", l);
+    const int total = (int)nfx_made_packed_floats(d, H);
+    int blocks = (total + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    made_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
+    return check_launch("made_pack_kernel");
+}
+
+extern "C" int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
+                               int64_t B, int d, int H, int variant, int accumulate, void* stream) {
+    if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine: bad shape");
+    if (d > 4096 || H > 128) return set_error(NFX_EUNSUPPORTED, "made_affine: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (variant < NFX_MAF_INVERSE || variant > NFX_IAF_INVERSE)
+        return set_error(NFX_EINVAL, "made_affine: unknown variant %d", variant);
+    if (B == 0) return NFX_OK;
+    if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "made_affine: null pointer");
+    if (in == out) return set_error(NFX_EINVAL, "made_affine: in and out must not alias");
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
+    hipStream_t s = (hipStream_t)stream;
+    if (variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) {
+        const size_t wbytes = (size_t)L.par_total * sizeof(float);
+        const size_t stage8 = 8 * (size_t)kStageFloats * sizeof(float);
+        const bool wlds = wbytes + stage8 <= kLdsBytes;
+        made_par_kernel_t k = pick_par(HT, wlds, variant);
+        if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no kernel for H=%d", H);
+        const int threads = wlds ? 512 : 256;
+        const size_t lds = wlds ? wbytes + stage8 : 4 * (size_t)kStageFloats * sizeof(float);
+        int rc = prepare_lds((const void*)k, lds);
+        if (rc) return rc;
+        const int64_t nchunks = (B + 63) / 64;
+        const int nw = threads / 64;
+        const int grid = resident_grid((const void*)k, threads, lds, (nchunks + nw - 1) / nw);
+        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks);
+        return check_launch("made_parallel_kernel");
+    }
+    made_seq_kernel_t k = pick_seq(HT, variant);
+    if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no sequential kernel for H=%d", H);
+    const size_t lds = 2 * 64 * (size_t)(L.Hp + 4) * sizeof(float);
+    int rc = prepare_lds((const void*)k, lds);
+    if (rc) return rc;
+    const int64_t grid = (B + 63) / 64;
+    k<<<(unsigned)grid, 64, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate);
+    return check_launch("made_seq_kernel");
+}

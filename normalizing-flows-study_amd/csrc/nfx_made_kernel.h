@@ -1,0 +1,428 @@
+// MADE-masked autoregressive affine flows (MAF / IAF) for gfx950.
+//
+// Reference: src/flows/autoregressive/made.py:81-140 (4 MaskedLinear, ReLU between, output
+// order [mu_0..mu_{d-1} | alpha_0..alpha_{d-1}]), masked_linear.py:14-18 (W * mask),
+// masked_autoregressive_flow.py:18-78, inverse_autoregressive_flow.py:30-103.
+//
+// Parallel directions (MAF.inverse = density, IAF.forward = sampling): the dense masked MADE
+// is a genuine GEMM chain under a static mask (W*M folded once at pack time — bit-identical to
+// the per-call weight*mask because the mask is 0/1). One wave owns 64 samples (two 32-column
+// MFMA tiles); hidden activations stay in accumulator registers between layers; the input layer
+// streams x through a wave-private LDS tile in 32-dimension chunks (coalesced 128-byte rows in,
+// conflict-free stride-33 column reads out); the output layer is produced in (mu, alpha) tile
+// pairs so mu_i and alpha_i land in the same lane/register, and the affine epilogue runs on the
+// same LDS tile before a coalesced store. Weights are read by A-operand-ordered 16-byte loads
+// from LDS when the whole image fits (small d, e.g. the d=63 MAF of BASELINE cfg4) and from
+// global/L2 otherwise (e.g. d=784 IAF).
+#pragma once
+#include "nfx_common.h"
+
+namespace nfx {
+
+// Packed image (floats), A-operand order, 4 consecutive k-steps per lane as one float4:
+//   w1 [HT][G1][64][4]    G1 = 4 * NKC k-step groups, NKC = ceil(d/32) input chunks
+//   b1 [HT][16][2]
+//   w2 [HT][HT][4][64][4], b2 [HT][16][2], w3 (same), b3
+//   w4 [NJ][2][HT][4][64][4]  NJ = ceil(d/32) output tile pairs (0 = mu rows, 1 = alpha rows)
+//   b4 [NJ][2][16][2]
+// then, for the sequential kernels, plain row-major copies (Hp = 32*HT):
+//   s_w1t [d][Hp]  (W1m transposed: column i = the inputs' contributions of x_i)
+//   s_b1 [Hp], s_w2 [Hp][Hp], s_b2 [Hp], s_w3 [Hp][Hp], s_b3 [Hp]
+//   s_w4 [2d][Hp], s_b4 [2d(up4)],
+//   s_deg [3][Hp]: unit degree (padded units 1e9) | degrees in completion order | unit index in
+//   completion order (units sorted by degree, stable)
+struct MadeLayout {
+    int d, HT, Hp, NKC, NJ;
+    int w1, b1, w2, b2, w3, b3, w4, b4;  // parallel image
+    int par_total;                       // floats of the parallel image (LDS-resident prefix)
+    int s_w1t, s_b1, s_w2, s_b2, s_w3, s_b3, s_w4, s_b4, s_deg, total;
+};
+
+__host__ __device__ constexpr int made_up4(int v) { return (v + 3) & ~3; }
+
+__host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
+    MadeLayout L{};
+    L.d = d;
+    L.HT = HT;
+    L.Hp = 32 * HT;
+    L.NKC = (d + 31) / 32;
+    L.NJ = (d + 31) / 32;
+    int o = 0;
+    L.w1 = o; o += HT * 4 * L.NKC * 256;
+    L.b1 = o; o += HT * 32;
+    L.w2 = o; o += HT * HT * 1024;
+    L.b2 = o; o += HT * 32;
+    L.w3 = o; o += HT * HT * 1024;
+    L.b3 = o; o += HT * 32;
+    L.w4 = o; o += L.NJ * 2 * HT * 1024;
+    L.b4 = o; o += L.NJ * 2 * 32;
+    L.par_total = o;
+    L.s_w1t = o; o += made_up4(d * L.Hp);
+    L.s_b1 = o; o += L.Hp;
+    L.s_w2 = o; o += L.Hp * L.Hp;
+    L.s_b2 = o; o += L.Hp;
+    L.s_w3 = o; o += L.Hp * L.Hp;
+    L.s_b3 = o; o += L.Hp;
+    L.s_w4 = o; o += made_up4(2 * d * L.Hp);
+    L.s_b4 = o; o += made_up4(2 * d);
+    L.s_deg = o; o += 3 * L.Hp;
+    L.total = o;
+    return L;
+}
+
+constexpr int kStageStride = 33;              // wave-private x tile [64][33] (conflict-free)
+constexpr int kStageFloats = 64 * kStageStride;
+
+// Affine epilogues (exact reference op order and clamps).
+template <int VAR>
+__device__ __forceinline__ float made_affine(float xv, float mu, float al, float& acc) {
+    if constexpr (VAR == NFX_MAF_INVERSE) {
+        // masked_autoregressive_flow.py:25-31: alpha = clamp(alpha,-3,3);
+        // z = (x - mu) * exp(clamp(-alpha, -5, 5)); guard z -> 0 (:35)
+        const float a = tclamp(al, -3.f, 3.f);
+        acc = acc + a;
+        const float z = (xv - mu) * expf(tclamp(-a, -5.f, 5.f));
+        return nonfinite(z) ? 0.f : z;
+    } else {
+        // inverse_autoregressive_flow.py:40-53: alpha = clamp(alpha,-2,2); mu = clamp(mu,-10,10);
+        // x = z * exp(clamp(alpha,-3,3)) + mu; guard x -> z
+        const float a = tclamp(al, -2.f, 2.f);
+        const float m = tclamp(mu, -10.f, 10.f);
+        acc = acc + a;
+        const float y = xv * expf(tclamp(a, -3.f, 3.f)) + m;
+        return nonfinite(y) ? xv : y;
+    }
+}
+
+// Stage x[64 samples][32 dims] (dims dim0..dim0+31) of a chunk into the wave's LDS tile.
+__device__ __forceinline__ void stage_in(const float* __restrict__ in, int64_t base, int d, int64_t B,
+                                         int dim0, float* st) {
+    const int lane = lane_id();
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+        const int idx = i * 64 + lane;
+        const int s = idx >> 5, dd = idx & 31;
+        const int64_t row = base + s;
+        const int dim = dim0 + dd;
+        st[s * kStageStride + dd] = (row < B && dim < d) ? in[row * d + dim] : 0.f;
+    }
+}
+
+__device__ __forceinline__ void stage_out(float* __restrict__ out, int64_t base, int d, int64_t B,
+                                          int dim0, const float* st) {
+    const int lane = lane_id();
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+        const int idx = i * 64 + lane;
+        const int s = idx >> 5, dd = idx & 31;
+        const int64_t row = base + s;
+        const int dim = dim0 + dd;
+        if (row < B && dim < d) out[row * d + dim] = st[s * kStageStride + dd];
+    }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // A wave's DS operations execute in order; this only stops the compiler from moving LDS
+    // accesses across the point (the tile is wave-private, no workgroup barrier needed).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int HT>
+__device__ __forceinline__ void made_hidden(const float* __restrict__ W, int woff, int boff,
+                                            const f32x16 (&hin)[HT][2], f32x16 (&hout)[HT][2]) {
+    const int lane = lane_id(), h = lane >> 5;
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a0, a1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a0[r] = a1[r] = W[boff + (hto * 16 + r) * 2 + h];
+#pragma unroll
+        for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(W + woff + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    a0 = mfma32(w[rr], hin[kt][0][4 * rq + rr], a0);
+                    a1 = mfma32(w[rr], hin[kt][1][4 * rq + rr], a1);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            a1[r] = trelu(a1[r]);
+        }
+        hout[hto][0] = a0;
+        hout[hto][1] = a1;
+    }
+}
+
+template <int HT, bool WLDS, int VAR>
+__global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t nchunks) {
+    constexpr int NWAVE = WLDS ? 8 : 4;
+    const MadeLayout L = made_layout(d, HT);
+    extern __shared__ f32x4 lds4[];
+    float* lds = reinterpret_cast<float*>(lds4);
+    const int wave = threadIdx.x >> 6;
+    float* stg;
+    if constexpr (WLDS) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(packed);
+        for (int i = threadIdx.x; i < L.par_total / 4; i += NWAVE * 64) lds4[i] = src[i];
+        stg = lds + L.par_total + wave * kStageFloats;
+        __syncthreads();
+    } else {
+        stg = lds + wave * kStageFloats;
+    }
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int64_t nwaves = (int64_t)gridDim.x * NWAVE;
+
+    for (int64_t c = (int64_t)blockIdx.x * NWAVE + wave; c < nchunks; c += nwaves) {
+        const int64_t base = c * 64;
+        const float* W = (WLDS ? lds : packed) + opaque_zero();
+
+        // ---- layer 1: h1 = relu(W1m x + b1), K streamed in 32-dim chunks through LDS ----
+        f32x16 h1[HT][2];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h1[ht][0][r] = h1[ht][1][r] = W[L.b1 + (ht * 16 + r) * 2 + h];
+        }
+        for (int kc = 0; kc < L.NKC; ++kc) {
+            stage_in(in, base, d, B, 32 * kc, stg);
+            wave_lds_sync();
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 w[HT];
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht)
+                    w[ht] = *reinterpret_cast<const f32x4*>(W + L.w1 + ((ht * 4 * L.NKC + kc * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int k = 8 * g + 2 * rr + h;
+                    const float b0 = stg[col * kStageStride + k];
+                    const float b1 = stg[(32 + col) * kStageStride + k];
+#pragma unroll
+                    for (int ht = 0; ht < HT; ++ht) {
+                        h1[ht][0] = mfma32(w[ht][rr], b0, h1[ht][0]);
+                        h1[ht][1] = mfma32(w[ht][rr], b1, h1[ht][1]);
+                    }
+                }
+            }
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                h1[ht][0][r] = trelu(h1[ht][0][r]);
+                h1[ht][1][r] = trelu(h1[ht][1][r]);
+            }
+        }
+        // ---- layers 2, 3 ----
+        f32x16 h2[HT][2];
+        made_hidden<HT>(W, L.w2, L.b2, h1, h2);
+        made_hidden<HT>(W, L.w3, L.b3, h2, h1);  // h3 -> h1 registers
+
+        // ---- layer 4 in (mu, alpha) tile pairs + affine epilogue ----
+        float acc0 = 0.f, acc1 = 0.f;
+        for (int j = 0; j < L.NJ; ++j) {
+            f32x16 mu0, mu1, al0, al1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                mu0[r] = mu1[r] = W[L.b4 + ((j * 2 + 0) * 16 + r) * 2 + h];
+                al0[r] = al1[r] = W[L.b4 + ((j * 2 + 1) * 16 + r) * 2 + h];
+            }
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 wm = *reinterpret_cast<const f32x4*>(
+                        W + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                    const f32x4 wa = *reinterpret_cast<const f32x4*>(
+                        W + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const float b0 = h1[kt][0][4 * rq + rr], b1 = h1[kt][1][4 * rq + rr];
+                        mu0 = mfma32(wm[rr], b0, mu0);
+                        mu1 = mfma32(wm[rr], b1, mu1);
+                        al0 = mfma32(wa[rr], b0, al0);
+                        al1 = mfma32(wa[rr], b1, al1);
+                    }
+                }
+            }
+            stage_in(in, base, d, B, 32 * j, stg);
+            wave_lds_sync();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = crow(r, h);
+                if (32 * j + row < d) {
+                    float* p0 = stg + col * kStageStride + row;
+                    float* p1 = stg + (32 + col) * kStageStride + row;
+                    *p0 = made_affine<VAR>(*p0, mu0[r], al0[r], acc0);
+                    *p1 = made_affine<VAR>(*p1, mu1[r], al1[r], acc1);
+                }
+            }
+            wave_lds_sync();
+            stage_out(out, base, d, B, 32 * j, stg);
+            wave_lds_sync();
+        }
+        // per-sample alpha sum: lane l <-> sample base + l
+        float s = halves_sum(acc0, acc1);
+        const int64_t so = base + lane;
+        if (so < B) {
+            float ld;
+            if constexpr (VAR == NFX_MAF_INVERSE) {
+                ld = -s;
+                if (nonfinite(ld)) ld = 0.f;
+                ld = tclamp(ld, -100.f, 100.f);
+            } else {
+                ld = s;
+                if (nonfinite(ld)) ld = 0.f;
+                ld = tclamp(ld, -50.f, 50.f);
+            }
+            logdet[so] = accumulate ? logdet[so] + ld : ld;
+        }
+    }
+}
+
+
+// Sequential directions (MAF.forward = sampling, IAF.inverse = density): the reference runs d
+// full MADE evaluations on the partially filled vector (masked_autoregressive_flow.py:55-67,
+// inverse_autoregressive_flow.py:74-90). Output i only depends on hidden units of degree < i,
+// and a hidden unit of degree m only on inputs 0..m, so with the masked weights multiplying
+// exact zeros every MADE output equals its value on the final vector: this kernel computes each
+// hidden unit ONCE, as soon as the input of its degree is known, and each output once — one
+// MADE evaluation per sample instead of d. Layer-1 pre-activations are accumulated by a rank-1
+// update per step (register-resident), completed units go through layers 2-3 (dots over the
+// wave-private LDS rows of h1/h2), outputs are dots over the register-resident h3. Weights are
+// wave-uniform (scalar loads). One lane = one sample.
+// The reference's NaN contamination is reproduced: once an x_j is non-finite, every later MADE
+// call sees 0*inf = NaN through the masked weights, so all later (mu, alpha) are NaN (`poison`).
+template <int HT, int VAR>
+__global__ __launch_bounds__(64) void made_seq_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int d, int H, int accumulate) {
+    constexpr int Hp = 32 * HT;
+    constexpr int RS = Hp + 4;  // LDS row stride (conflict-free ds_read_b128 across lanes)
+    const MadeLayout L = made_layout(d, HT);
+    extern __shared__ f32x4 lds4[];
+    float* h1s = reinterpret_cast<float*>(lds4);
+    float* h2s = h1s + 64 * RS;
+    const int lane = threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x * 64 + lane;
+    const bool valid = s < B;
+    const float* P = packed;
+
+    float pre1[Hp], h3[Hp];
+#pragma unroll
+    for (int a = 0; a < Hp; ++a) {
+        pre1[a] = P[L.s_b1 + a];
+        h3[a] = 0.f;
+        h1s[lane * RS + a] = 0.f;
+        h2s[lane * RS + a] = 0.f;
+    }
+    float ld = 0.f;
+    bool poison = false;
+    int p = 0;  // next unit (in degree order) to complete
+    const float* ord = P + L.s_deg;  // s_deg holds [unit degree] ; order is implicit below
+
+    for (int i = 0; i < d; ++i) {
+        // output i from units of degree < i (incomplete units hold h3 = 0 and masked weights)
+        float mu = 0.f, al = 0.f;
+        const float* w_mu = P + L.s_w4 + (size_t)i * Hp;
+        const float* w_al = P + L.s_w4 + (size_t)(d + i) * Hp;
+#pragma unroll
+        for (int a = 0; a < Hp; ++a) {
+            mu = fmaf(w_mu[a], h3[a], mu);
+            al = fmaf(w_al[a], h3[a], al);
+        }
+        mu = mu + P[L.s_b4 + i];
+        al = al + P[L.s_b4 + d + i];
+        if (poison) { mu = __builtin_nanf(""); al = mu; }
+        const float xin = valid ? in[s * d + i] : 0.f;
+        float xi;
+        if constexpr (VAR == NFX_MAF_FORWARD) {
+            // masked_autoregressive_flow.py:57-65
+            const float a = tclamp(al, -3.f, 3.f);
+            xi = xin * expf(tclamp(a, -5.f, 5.f)) + mu;
+            ld = ld + a;
+            if (valid) out[s * d + i] = nonfinite(xi) ? 0.f : xi;
+        } else {
+            // inverse_autoregressive_flow.py:79-88
+            const float a = tclamp(al, -2.f, 2.f);
+            const float m = tclamp(mu, -10.f, 10.f);
+            xi = (xin - m) * expf(tclamp(-a, -3.f, 3.f));
+            ld = ld - a;
+            if (valid) out[s * d + i] = nonfinite(xi) ? xin : xi;
+        }
+        if (nonfinite(xi)) poison = true;
+        // rank-1 update of the layer-1 pre-activations with the new input x_i
+        const float* w1c = P + L.s_w1t + (size_t)i * Hp;
+#pragma unroll
+        for (int a = 0; a < Hp; ++a) pre1[a] = fmaf(w1c[a], xi, pre1[a]);
+        // hidden units of degree i are now complete: layer 1, then 2, then 3 of the level
+        int q = p;
+        while (q < H && (int)ord[Hp + q] == i) ++q;  // ord[Hp + k] = degree of k-th unit in order
+        if (q > p) {
+            for (int k = p; k < q; ++k) {
+                const int a = (int)ord[2 * Hp + k];   // unit index of the k-th completion
+                float v = 0.f;
+#pragma unroll
+                for (int b = 0; b < Hp; ++b) v = (b == a) ? pre1[b] : v;
+                h1s[lane * RS + a] = trelu(v);
+            }
+            for (int k = p; k < q; ++k) {
+                const int a = (int)ord[2 * Hp + k];
+                const float* w = P + L.s_w2 + (size_t)a * Hp;
+                float v = 0.f;
+#pragma unroll
+                for (int b = 0; b < Hp; b += 4) {
+                    const f32x4 hv = *reinterpret_cast<const f32x4*>(h1s + lane * RS + b);
+                    v = fmaf(w[b], hv[0], v);
+                    v = fmaf(w[b + 1], hv[1], v);
+                    v = fmaf(w[b + 2], hv[2], v);
+                    v = fmaf(w[b + 3], hv[3], v);
+                }
+                h2s[lane * RS + a] = trelu(v + P[L.s_b2 + a]);
+            }
+            for (int k = p; k < q; ++k) {
+                const int a = (int)ord[2 * Hp + k];
+                const float* w = P + L.s_w3 + (size_t)a * Hp;
+                float v = 0.f;
+#pragma unroll
+                for (int b = 0; b < Hp; b += 4) {
+                    const f32x4 hv = *reinterpret_cast<const f32x4*>(h2s + lane * RS + b);
+                    v = fmaf(w[b], hv[0], v);
+                    v = fmaf(w[b + 1], hv[1], v);
+                    v = fmaf(w[b + 2], hv[2], v);
+                    v = fmaf(w[b + 3], hv[3], v);
+                }
+                v = trelu(v + P[L.s_b3 + a]);
+#pragma unroll
+                for (int b = 0; b < Hp; ++b) h3[b] = (b == a) ? v : h3[b];
+            }
+            p = q;
+        }
+    }
+    if (valid) {
+        if (nonfinite(ld)) ld = 0.f;
+        ld = (VAR == NFX_MAF_FORWARD) ? tclamp(ld, -100.f, 100.f) : tclamp(ld, -50.f, 50.f);
+        logdet[s] = accumulate ? logdet[s] + ld : ld;
+    }
+}
+
+typedef void (*made_seq_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int);
+
+typedef void (*made_par_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t);
+
+template <int HT>
+made_par_kernel_t made_pick_ht(bool wlds, int variant);
+template <int HT>
+made_seq_kernel_t made_seq_pick_ht(int variant);
+
+}  // namespace nfx

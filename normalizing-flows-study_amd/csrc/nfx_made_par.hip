@@ -1,0 +1,22 @@
+// Instantiations of the parallel MADE-affine kernel (MAF.inverse / IAF.forward):
+// hidden tiles HT = 1..4, weights LDS-resident or L2-streamed.
+#include "nfx_made_kernel.h"
+
+namespace nfx {
+
+template <int HT, bool WLDS>
+static made_par_kernel_t par_var(int variant) {
+    return variant == NFX_MAF_INVERSE ? made_parallel_kernel<HT, WLDS, NFX_MAF_INVERSE>
+                                      : made_parallel_kernel<HT, WLDS, NFX_IAF_FORWARD>;
+}
+
+template <int HT>
+made_par_kernel_t made_pick_ht(bool wlds, int variant) {
+    return wlds ? par_var<HT, true>(variant) : par_var<HT, false>(variant);
+}
+template made_par_kernel_t made_pick_ht<1>(bool, int);
+template made_par_kernel_t made_pick_ht<2>(bool, int);
+template made_par_kernel_t made_pick_ht<3>(bool, int);
+template made_par_kernel_t made_pick_ht<4>(bool, int);
+
+}  // namespace nfx

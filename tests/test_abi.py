@@ -1,0 +1,63 @@
+"""The C-ABI library (libnfx.so) loads without a GPU and exports every symbol include/nfx.h
+declares; host-only entry points (sizes, version, argument validation) behave."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+import nfs_amd
+from nfs_amd import _lib
+
+HEADER = os.path.join(ROOT, "include", "nfx.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(nfx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) >= 14
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(_lib.EXPORTED_SYMBOLS) == syms
+
+
+def test_abi_version_and_sizes():
+    L = _lib.lib()
+    assert L.nfx_abi_version() == 1
+    assert L.nfx_affine_packed_floats(2, 64) > 0
+    assert L.nfx_affine_packed_floats(2, 64) % 4 == 0
+    assert L.nfx_spline_packed_floats(2, 64, 8) % 4 == 0
+    assert L.nfx_made_packed_floats(63, 64) % 4 == 0
+    assert L.nfx_affine_packed_floats(0, 64) == 0
+    assert L.nfx_gauss_workspace_bytes(1 << 20) >= 8
+
+
+def test_invalid_arguments_fail_before_any_launch():
+    """Argument validation happens on the host: no device pointer is touched."""
+    L = _lib.lib()
+    rc = L.nfx_affine_coupling(None, None, None, None, 16, 2, 64, 0, 0, None)
+    assert rc == -1 and b"direction" in L.nfx_last_error()
+    rc = L.nfx_affine_coupling(None, None, None, None, 16, 9, 64, 1, 0, None)
+    assert rc in (-1, -2)
+    rc = L.nfx_spline_coupling(None, None, None, None, 16, 2, 64, 12, 5.0, 1e-3, 1e-3, 1e-3, 0, 0.0, 0.0, 1, 0, None)
+    assert rc == -2 and b"K=12" in L.nfx_last_error()
+    rc = L.nfx_made_affine(None, None, None, None, 16, 63, 64, 7, 0, None)
+    assert rc == -1
+    rc = L.nfx_rqs_unit(None, None, None, None, None, None, 16, 40, 1e-3, 1e-3, 1e-3, 0, None)
+    assert rc == -2
+    # B == 0 is a valid no-op
+    assert L.nfx_affine_coupling(None, None, None, None, 0, 2, 64, 1, 0, None) == 0
+
+
+def test_product_raises_without_library(monkeypatch, tmp_path):
+    """No silent eager fallback: a missing libnfx.so is a loud error."""
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.NfxLibraryError):
+        _lib.load(str(tmp_path / "missing.so"))

@@ -1,0 +1,173 @@
+"""GPU parity of the MADE-affine kernels (csrc/nfx_made*.hip): MAF.inverse / IAF.forward
+(parallel, fp32 MFMA) and MAF.forward / IAF.inverse (sequential over d, one MADE evaluation
+per sample) against the reference's golden outputs and the CPU oracle.
+
+Tolerances: z/x |d| <= 2e-5 * (1 + |ref|); log-det <= 2e-4 (d = 63), 1e-3 (d = 784: a sum of
+784 clamped alphas); NLL relative <= 1e-6 at cfg4.
+"""
+import numpy as np
+import pytest
+import torch
+
+import nfs_amd
+import oracle
+from conftest import golden_json, load_golden, oracle_sd, state_dict_from
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_y(y, ref, tol=2e-5):
+    y, ref = np.asarray(y, np.float64), np.asarray(ref, np.float64)
+    err = np.abs(y - ref) / (1 + np.abs(ref))
+    assert err.max() <= tol, f"max rel err {err.max():.3g} at {np.unravel_index(err.argmax(), err.shape)}"
+
+
+def assert_ld(ld, ref, tol=2e-4):
+    d = np.abs(np.asarray(ld, np.float64) - np.asarray(ref, np.float64))
+    assert d.max() <= tol, f"max |dld| {d.max():.3g} at {d.argmax()}"
+
+
+def maf63(dev):
+    g = load_golden("g5_maf63.npz")
+    m = nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(63, 64) for _ in range(5)])
+    m.load_state_dict(state_dict_from(g, "", m))
+    return m.to(dev).eval(), g
+
+
+def test_maf63_inverse_parallel_vs_reference(cuda_device):
+    m, g = maf63(cuda_device)
+    nfs_amd.reset_stats()
+    with torch.no_grad():
+        z, ld = m.inverse(torch.from_numpy(g["x"]).to(cuda_device))
+        lp = m.log_prob(torch.from_numpy(g["x"]).to(cuda_device))
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] >= 5
+    assert_y(z.cpu(), g["inv_z"])
+    assert_ld(ld.cpu(), g["inv_ld"])
+    nll = -float(lp.double().mean())
+    assert abs(nll - float(g["nll_f64"])) <= 1e-6 * abs(float(g["nll_f64"]))
+
+
+def test_maf63_forward_sequential_vs_reference(cuda_device):
+    m, g = maf63(cuda_device)
+    with torch.no_grad():
+        x, ld = m.forward(torch.from_numpy(g["z"]).to(cuda_device))
+    assert_y(x.cpu(), g["fwd_x"])
+    assert_ld(ld.cpu(), g["fwd_ld"])
+
+
+def test_iaf784_vs_reference(cuda_device):
+    g = load_golden("g6_iaf784.npz")
+    f = nfs_amd.InverseAutoregressiveFlow(784, 64)
+    f.load_state_dict(state_dict_from(g, "", f))
+    f = f.to(cuda_device).eval()
+    with torch.no_grad():
+        x, ldf = f.forward(torch.from_numpy(g["z"]).to(cuda_device))
+        z, ldi = f.inverse(torch.from_numpy(g["x"]).to(cuda_device))
+    assert_y(x.cpu(), g["fwd_x"])
+    assert_ld(ldf.cpu(), g["fwd_ld"], 1e-3)
+    assert_y(z.cpu(), g["inv_z"])
+    assert_ld(ldi.cpu(), g["inv_ld"], 1e-3)
+
+
+@pytest.mark.parametrize("name,kind", [("maf4", "maf"), ("iaf4", "iaf"), ("maf10", "maf"),
+                                       ("iaf10", "iaf"), ("maf2", "maf"), ("iaf3", "iaf")])
+def test_small_made_flows(cuda_device, name, kind):
+    g = load_golden("g9_small.npz")
+    sd = oracle_sd(g, name + ".")
+    d = sd["conditioner.net.0.weight"].shape[1]
+    H = sd["conditioner.net.0.weight"].shape[0]
+    cls = nfs_amd.MaskedAutoregressiveFlow if kind == "maf" else nfs_amd.InverseAutoregressiveFlow
+    f = cls(d, H)
+    f.load_state_dict(state_dict_from(g, name + ".", f))
+    f = f.to(cuda_device).eval()
+    x = torch.from_numpy(g[name + ".x"]).to(cuda_device)
+    with torch.no_grad():
+        yf, lf = f.forward(x)
+        yi, li = f.inverse(x)
+    assert_y(yf.cpu(), g[name + ".fwd_y"])
+    assert_ld(lf.cpu(), g[name + ".fwd_ld"])
+    assert_y(yi.cpu(), g[name + ".inv_y"])
+    assert_ld(li.cpu(), g[name + ".inv_ld"])
+
+
+@pytest.mark.parametrize("d,H,B", [(5, 16, 1), (33, 32, 65), (63, 96, 130), (100, 128, 257), (7, 64, 1000)])
+def test_made_shapes_vs_oracle(cuda_device, d, H, B):
+    torch.manual_seed(d * 31 + H)
+    for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
+        f = cls(d, H)
+        with torch.no_grad():
+            for p in f.parameters():
+                p.add_(0.05 * torch.randn_like(p))
+        sd = {k: v.clone() for k, v in f.state_dict().items()}
+        f = f.to(cuda_device).eval()
+        x = torch.randn(B, d)
+        for direction in (1, -1):
+            with torch.no_grad():
+                yg, lg = (f.forward if direction > 0 else f.inverse)(x.to(cuda_device))
+                yr, lr = fn(sd, "", x, direction)
+            assert_y(yg.cpu(), yr)
+            assert_ld(lg.cpu(), lr, 5e-4)
+
+
+def test_made_nonfinite_inputs(cuda_device):
+    """inf/NaN rows: parallel directions propagate 0*inf = NaN through the dense masked weights;
+    sequential directions reproduce the reference's contamination of every later step."""
+    torch.manual_seed(3)
+    d, H = 6, 16
+    for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
+        f = cls(d, H)
+        with torch.no_grad():
+            for p in f.parameters():
+                p.add_(0.1 * torch.randn_like(p))
+        sd = {k: v.clone() for k, v in f.state_dict().items()}
+        f = f.to(cuda_device).eval()
+        x = torch.randn(8, d)
+        x[0, 0] = float("inf")
+        x[1, 3] = float("nan")
+        x[2, 5] = -float("inf")
+        x[3, :] = 1e30
+        for direction in (1, -1):
+            with torch.no_grad():
+                yg, lg = (f.forward if direction > 0 else f.inverse)(x.to(cuda_device))
+                yr, lr = fn(sd, "", x, direction)
+            yg, yr = yg.cpu().numpy(), yr.numpy()
+            assert np.array_equal(np.isnan(yg), np.isnan(yr)) and np.array_equal(np.isinf(yg), np.isinf(yr))
+            fin = np.isfinite(yr)
+            assert_y(yg[fin], yr[fin])
+            assert_ld(lg.cpu(), lr)
+
+
+def test_made_batchnorm_eval(cuda_device):
+    """MADE(use_batch_norm=True) in eval mode: BatchNorm folded from running stats."""
+    torch.manual_seed(9)
+    f = nfs_amd.MaskedAutoregressiveFlow(12, 32, use_batch_norm=True)
+    with torch.no_grad():
+        for m in f.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.normal_(0, 0.1)
+                m.running_var.uniform_(0.5, 1.5)
+                m.weight.normal_(1, 0.1)
+                m.bias.normal_(0, 0.1)
+    f.eval()
+    x = torch.randn(300, 12)
+    with torch.no_grad():
+        zc, lc = f.inverse(x)
+        xc, lfc = f.forward(x)
+    f = f.to(cuda_device)
+    with torch.no_grad():
+        zg, lg = f.inverse(x.to(cuda_device))
+        xg, lfg = f.forward(x.to(cuda_device))
+    assert_y(zg.cpu(), zc)
+    assert_ld(lg.cpu(), lc)
+    assert_y(xg.cpu(), xc)
+    assert_ld(lfg.cpu(), lfc)
+
+
+def test_full_scale_nll_cfg4(cuda_device):
+    """BASELINE cfg4 at full size on one GPU: 5x MAF(63,64), B=4M, NLL vs the reference (G8)."""
+    meta = golden_json("g8_full_nll.json")["cfg4_maf_d63_B4M"]
+    x = torch.randn(meta["B"], meta["d"], generator=torch.Generator().manual_seed(meta["seed"]))
+    assert abs(float(x.double().sum()) - meta["input_sum_f64"]) < 1e-3
+    m, _ = maf63(cuda_device)
+    nll = m.nll(x.to(cuda_device))
+    assert abs(nll - meta["nll_f64"]) <= 1e-6 * abs(meta["nll_f64"]), (nll, meta["nll_f64"])
