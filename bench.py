@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4"])
     ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default 1M; 500k for cfg4)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: split ONE global batch (default 1M) over the ranks")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -130,7 +132,14 @@ def main():
 
     model, d, f_layer, spec, desc = build(a.config)
     model = model.to(dev).eval()
-    B = a.batch or (500_000 if a.config == "cfg4" else 1_000_000)
+    from nfs_amd.distributed import broadcast_parameters, shard_range
+    broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
+    B_unit = a.batch or (500_000 if a.config == "cfg4" else 1_000_000)
+    if a.strong:
+        lo, hi = shard_range(B_unit, rank, world)
+        B, B_global = hi - lo, B_unit
+    else:
+        B, B_global = B_unit, B_unit * world
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn(B, d, device=dev, generator=g)
     flow = model.flow if hasattr(model, "flow") else model
@@ -187,19 +196,19 @@ def main():
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         result = {
             "metric": METRIC,
-            "value": world * B * a.steps / t_max,
+            "value": B_global * a.steps / t_max,
             "unit": "samples/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": 1e3 * t_max / a.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.strong else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic: x ~ N(0,1) generated on device (seed 1234+rank); seeded random-init "
                     "weights perturbed N(0, 0.1^2) with non-trivial BatchNorm running stats",
-            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": world * B,
+            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B_global,
                        "parallelism": f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"},
             "nll_f64": nll,
             "roofline": {"bound": "mfma", "kernel": kname, "achieved": achieved,

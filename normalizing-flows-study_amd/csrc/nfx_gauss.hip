@@ -44,6 +44,52 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
     if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
+// d > 8: a thread-per-sample walk over [B, d] rows is uncoalesced (64 lanes hit 64 lines per
+// load) and thrashes L2 at d = 63 (measured 6x the algorithmic bytes). Instead each wave stages
+// its 64-sample tile through LDS in 32-dimension chunks with coalesced 128-byte row segments,
+// then every lane sums its own row from LDS (stride-33 rows: conflict-free).
+__global__ __launch_bounds__(kGaussThreads) void gauss_logprob_tiled_kernel(
+    const float* __restrict__ z, const float* __restrict__ ld, float* __restrict__ logp,
+    double* __restrict__ partials, int64_t B, int d, float c) {
+    __shared__ float stage[kGaussThreads / 64][64 * 33];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* st = stage[wave];
+    double acc = 0.0;
+    const int64_t ntiles = (B + 63) / 64;
+    for (int64_t t = (int64_t)blockIdx.x * (kGaussThreads / 64) + wave; t < ntiles;
+         t += (int64_t)gridDim.x * (kGaussThreads / 64)) {
+        const int64_t base = t * 64;
+        float m = 0.f;
+        for (int dim0 = 0; dim0 < d; dim0 += 32) {
+#pragma unroll 8
+            for (int i = 0; i < 32; ++i) {
+                const int idx = i * 64 + lane, s = idx >> 5, dd = idx & 31;
+                const int64_t row = base + s;
+                st[s * 33 + dd] = (row < B && dim0 + dd < d) ? z[row * d + dim0 + dd] : 0.f;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int n = (d - dim0) < 32 ? (d - dim0) : 32;
+            for (int j = 0; j < n; ++j) {
+                const float v = st[lane * 33 + j];
+                m = (dim0 == 0 && j == 0) ? v * v : m + v * v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const int64_t i = base + lane;
+        if (i < B) {
+            const float lp = -0.5f * (m + c) + ld[i];
+            if (logp) logp[i] = lp;
+            acc += (double)lp;
+        }
+    }
+    const double tsum = block_sum_f64(acc);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+}
+
 __global__ __launch_bounds__(kGaussThreads) void gauss_finish_kernel(const double* __restrict__ partials,
                                                                      int n, double* __restrict__ sums,
                                                                      int64_t B) {
@@ -76,7 +122,13 @@ extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* lo
     if (blocks < 1) blocks = 1;
     const float c = (float)((double)d * log(2.0 * M_PI));
     double* partials = reinterpret_cast<double*>(workspace);
-    if (B > 0) {
+    if (B > 0 && d > 8) {
+        int64_t tb = ((B + 63) / 64 + 3) / 4;
+        blocks = (int)(tb < kGaussMaxBlocks ? tb : kGaussMaxBlocks);
+        gauss_logprob_tiled_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, B, d, c);
+        int rc = check_launch("gauss_logprob_tiled_kernel");
+        if (rc) return rc;
+    } else if (B > 0) {
         gauss_logprob_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, B, d, c);
         int rc = check_launch("gauss_logprob_kernel");
         if (rc) return rc;

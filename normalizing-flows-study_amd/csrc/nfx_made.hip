@@ -108,6 +108,16 @@ static made_par_kernel_t pick_par(int HT, bool wlds, int variant) {
     }
 }
 
+static made_par_kernel_t pick_tile(int HT, bool wlds, int variant) {
+    switch (HT) {
+        case 1: return made_tile_pick_ht<1>(wlds, variant);
+        case 2: return made_tile_pick_ht<2>(wlds, variant);
+        case 3: return made_tile_pick_ht<3>(wlds, variant);
+        case 4: return made_tile_pick_ht<4>(wlds, variant);
+        default: return nullptr;
+    }
+}
+
 static made_seq_kernel_t pick_seq(int HT, int variant) {
     switch (HT) {
         case 1: return made_seq_pick_ht<1>(variant);
@@ -119,6 +129,7 @@ static made_seq_kernel_t pick_seq(int HT, int variant) {
 }
 
 constexpr size_t kLdsBytes = 160 * 1024;
+constexpr int kTileMaxD = 64;  // made_tile_kernel: whole [32 x d] x tile per wave in LDS
 
 }  // namespace nfx
 
@@ -155,6 +166,20 @@ extern "C" int nfx_made_affine(const float* packed, const float* in, float* out,
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
     hipStream_t s = (hipStream_t)stream;
+    if ((variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) && d <= kTileMaxD) {
+        const size_t wbytes = (size_t)L.par_total * sizeof(float);
+        const size_t tiles8 = 8 * 32 * (size_t)(d | 1) * sizeof(float);
+        const bool wlds = wbytes + tiles8 <= kLdsBytes;
+        made_par_kernel_t k = pick_tile(HT, wlds, variant);
+        if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no kernel for H=%d", H);
+        const size_t lds = (wlds ? wbytes : 0) + tiles8;
+        int rc = prepare_lds((const void*)k, lds);
+        if (rc) return rc;
+        const int64_t ntiles = (B + 31) / 32;
+        const int grid = resident_grid((const void*)k, 512, lds, (ntiles + 7) / 8);
+        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles);
+        return check_launch("made_tile_kernel");
+    }
     if (variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
         const size_t stage8 = 8 * (size_t)kStageFloats * sizeof(float);

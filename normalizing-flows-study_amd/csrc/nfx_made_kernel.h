@@ -418,10 +418,186 @@ __global__ __launch_bounds__(64) void made_seq_kernel(
 
 typedef void (*made_seq_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int);
 
+
+// Small-d parallel kernel (d <= 64, e.g. the UCI-shaped d=63 MAF of cfg4). One wave owns a
+// 32-sample tile: its whole [32 x d] x block sits in a wave-private LDS tile (row stride d|1,
+// conflict-free column reads), loaded row by row with coalesced <=256-byte loads — and the NEXT
+// tile's rows are prefetched into registers while layer 4 runs, so HBM latency hides behind
+// MFMA work. Layer 1 reads its B operands from the tile, the epilogue reads x and writes z in
+// place, the tile is stored row by row. Weights in LDS (512-thread workgroups, 1 per CU) when
+// they fit beside the eight tiles, otherwise read from L2.
+template <int HT>
+__device__ __forceinline__ void made_hidden1(const float* __restrict__ W, int woff, int boff,
+                                             const f32x16 (&hin)[HT], f32x16 (&hout)[HT]) {
+    // All HT output tiles advance together: HT independent MFMA accumulator chains per k-step.
+    const int lane = lane_id(), h = lane >> 5;
+    f32x16 a[HT];
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[hto][r] = W[boff + (hto * 16 + r) * 2 + h];
+    }
+#pragma unroll
+    for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            f32x4 w[HT];
+#pragma unroll
+            for (int hto = 0; hto < HT; ++hto)
+                w[hto] = *reinterpret_cast<const f32x4*>(W + woff + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll
+                for (int hto = 0; hto < HT; ++hto) a[hto] = mfma32(w[hto][rr], hin[kt][4 * rq + rr], a[hto]);
+            }
+        }
+    }
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[hto][r] = trelu(a[hto][r]);
+        hout[hto] = a[hto];
+    }
+}
+
+template <int HT, bool WLDS, int VAR>
+__global__ __launch_bounds__(512) void made_tile_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles) {
+    const MadeLayout L = made_layout(d, HT);
+    const int S = d | 1;
+    extern __shared__ f32x4 lds4[];
+    float* lds = reinterpret_cast<float*>(lds4);
+    const int wave = threadIdx.x >> 6;
+    if constexpr (WLDS) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(packed);
+        for (int i = threadIdx.x; i < L.par_total / 4; i += 512) lds4[i] = src[i];
+    }
+    float* xt = lds + (WLDS ? L.par_total : 0) + wave * 32 * S;
+    if constexpr (WLDS) __syncthreads();
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int64_t nwaves = (int64_t)gridDim.x * 8;
+
+    int64_t t = (int64_t)blockIdx.x * 8 + wave;
+    float pf[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const int64_t row = t * 32 + r;
+        pf[r] = (t < ntiles && row < B && lane < d) ? in[row * d + lane] : 0.f;
+    }
+    for (; t < ntiles; t += nwaves) {
+        const int64_t base = t * 32;
+        const float* W = (WLDS ? lds : packed) + opaque_zero();
+        if (lane < d) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) xt[r * S + lane] = pf[r];
+        }
+        wave_lds_sync();
+
+        f32x16 h1[HT];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h1[ht][r] = W[L.b1 + (ht * 16 + r) * 2 + h];
+        }
+        for (int kc = 0; kc < L.NKC; ++kc) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 w[HT];
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht)
+                    w[ht] = *reinterpret_cast<const f32x4*>(W + L.w1 + ((ht * 4 * L.NKC + kc * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int k = 32 * kc + 8 * g + 2 * rr + h;
+                    const float b = (k < d) ? xt[col * S + k] : 0.f;
+#pragma unroll
+                    for (int ht = 0; ht < HT; ++ht) h1[ht] = mfma32(w[ht][rr], b, h1[ht]);
+                }
+            }
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
+        }
+        f32x16 h2[HT];
+        made_hidden1<HT>(W, L.w2, L.b2, h1, h2);
+        made_hidden1<HT>(W, L.w3, L.b3, h2, h1);  // h3 -> h1
+
+        // prefetch the next tile's rows while layer 4 runs
+        const int64_t tn = t + nwaves;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const int64_t row = tn * 32 + r;
+            pf[r] = (tn < ntiles && row < B && lane < d) ? in[row * d + lane] : 0.f;
+        }
+
+        float acc = 0.f;
+        for (int j = 0; j < L.NJ; ++j) {
+            f32x16 mu, al;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                mu[r] = W[L.b4 + ((j * 2 + 0) * 16 + r) * 2 + h];
+                al[r] = W[L.b4 + ((j * 2 + 1) * 16 + r) * 2 + h];
+            }
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 wm = *reinterpret_cast<const f32x4*>(
+                        W + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                    const f32x4 wa = *reinterpret_cast<const f32x4*>(
+                        W + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        mu = mfma32(wm[rr], h1[kt][4 * rq + rr], mu);
+                        al = mfma32(wa[rr], h1[kt][4 * rq + rr], al);
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int dim = 32 * j + crow(r, h);
+                if (dim < d) {
+                    float* p = xt + col * S + dim;
+                    *p = made_affine<VAR>(*p, mu[r], al[r], acc);
+                }
+            }
+        }
+        const float ssum = halves_sum(acc, acc);  // both halves of sample `col`
+        wave_lds_sync();
+        if (lane < d) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const int64_t row = base + r;
+                if (row < B) out[row * d + lane] = xt[r * S + lane];
+            }
+        }
+        const int64_t so = base + col;
+        if (lane < 32 && so < B) {
+            float ldv;
+            if constexpr (VAR == NFX_MAF_INVERSE) {
+                ldv = -ssum;
+                if (nonfinite(ldv)) ldv = 0.f;
+                ldv = tclamp(ldv, -100.f, 100.f);
+            } else {
+                ldv = ssum;
+                if (nonfinite(ldv)) ldv = 0.f;
+                ldv = tclamp(ldv, -50.f, 50.f);
+            }
+            logdet[so] = accumulate ? logdet[so] + ldv : ldv;
+        }
+        wave_lds_sync();
+    }
+}
+
 typedef void (*made_par_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t);
 
 template <int HT>
 made_par_kernel_t made_pick_ht(bool wlds, int variant);
+template <int HT>
+made_par_kernel_t made_tile_pick_ht(bool wlds, int variant);
 template <int HT>
 made_seq_kernel_t made_seq_pick_ht(int variant);
 

@@ -1,0 +1,41 @@
+"""Data-parallel log_prob over the GPUs of one node (one process per GPU).
+
+The reference has no distributed code. Its hot path shards by sample with no
+per-layer communication: samples are independent in eval mode (the per-sample results of a
+half batch are bit-identical to the full batch). The ONLY exchange is the mean NLL: each rank
+reduces its shard to a float64 [sum log p, count] pair on device (fused in nfx_gauss_logprob)
+and one all-reduce of those 16 bytes runs over RCCL/xGMI (torch.distributed backend "nccl" is
+RCCL on ROCm). Weights are replicated once with a broadcast from rank 0.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n, rank, world):
+    """Contiguous, balanced [start, stop) of n samples for `rank` of `world`."""
+    q, r = divmod(n, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def broadcast_parameters(module, src=0, group=None):
+    """Replicate every parameter and buffer of `module` from rank `src` (one-time, <1 MB)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
+def sharded_nll(model, x_local, group=None, return_log_prob=False):
+    """Global mean NLL of the samples spread over all ranks; x_local is this rank's shard.
+
+    `model` is a NormalizingFlowModel / RealNVP / RealNVPSpline (anything with
+    log_prob(x, return_sums=True)). Returns a python float (identical on every rank)."""
+    flow = model.flow if hasattr(model, "flow") and hasattr(model.flow, "log_prob") else model
+    logp, sums = flow.log_prob(x_local, return_sums=True)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(sums, group=group)
+    s = sums.detach().cpu()
+    nll = -(s[0] / s[1]).item() if float(s[1]) > 0 else float("nan")
+    return (nll, logp) if return_log_prob else nll

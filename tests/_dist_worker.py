@@ -1,0 +1,47 @@
+"""Process entry of tests/test_dist_gloo.py (importable by spawned children: sets sys.path)."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "normalizing-flows-study_amd"), HERE):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import nfs_amd  # noqa: E402
+from nfs_amd.distributed import broadcast_parameters, shard_range, sharded_nll  # noqa: E402
+
+
+def _model(seed, kind):
+    torch.manual_seed(seed)
+    if kind == "realnvp":
+        m = nfs_amd.RealNVP(2, 4, 16)
+    elif kind == "spline":
+        m = nfs_amd.RealNVPSpline(2, 2, 16)
+    else:
+        m = nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(5, 16) for _ in range(2)])
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    return m.eval()
+
+
+def _worker(rank, world, port, kind, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = _model(1000 + rank, kind)          # different init per rank ...
+        broadcast_parameters(m, src=0)          # ... replicated from rank 0
+        d = 2 if kind != "maf" else 5
+        x = torch.randn(n, d, generator=torch.Generator().manual_seed(7))
+        a, b = shard_range(n, rank, world)
+        with torch.no_grad():
+            nll = sharded_nll(m, x[a:b])
+        sd = {k: v.numpy().copy() for k, v in m.state_dict().items()}
+        q.put((rank, nll, sd))
+    finally:
+        dist.destroy_process_group()
+
+
