@@ -40,7 +40,7 @@ __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float
                 int row = 32 * ht + (lane & 31), col = 2 * ks + (lane >> 5);
                 v = (row < H && col < d) ? mlp_weight(P, 0, d, row, col) : 0.f;
             } else if (o < L.w2) {
-                int t = o - L.b1, h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+                int t = o - L.b1, r = t & 15, h = (t >> 4) & 1, ht = t >> 5;
                 int row = 32 * ht + crow(r, h);
                 v = row < H ? mlp_bias(P, 0, row) : 0.f;
             } else if (o < L.b2) {
@@ -49,11 +49,11 @@ __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float
                 int row = 32 * hto + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
                 v = (row < H && col < H) ? mlp_weight(P, 1, H, row, col) : 0.f;
             } else if (o < L.w3) {
-                int t = o - L.b2, h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+                int t = o - L.b2, r = t & 15, h = (t >> 4) & 1, ht = t >> 5;
                 int row = 32 * ht + crow(r, h);
                 v = row < H ? mlp_bias(P, 1, row) : 0.f;
             } else if (o < L.b3) {
-                int t = o - L.w3, h = t & 1, r = (t >> 1) & 15, ht = (t >> 5) % HT, j = (t >> 5) / HT;
+                int t = o - L.w3, r = t & 15, h = (t >> 4) & 1, ht = (t >> 5) % HT, j = (t >> 5) / HT;
                 int col = 32 * ht + crow(r, h);
                 v = col < H ? mlp_weight(P, 2, H, j, col) : 0.f;
             } else {

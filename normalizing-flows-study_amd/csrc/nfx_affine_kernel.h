@@ -8,10 +8,10 @@ __host__ __device__ constexpr int up4(int v) { return (v + 3) & ~3; }
 
 // Packed weight image (floats). Per net (s_net = 0, b_net = 1):
 //   w1 [HT][KS1][64]        A operand of layer 1 (BN folded)
-//   b1 [HT][16][2]          bias of layer 1 at accumulator row crow(r,h) (BN folded)
+//   b1 [HT][2][16]          bias of layer 1 at accumulator register r of half h (BN folded)
 //   w2 [HT][HT][4][64][4]   A operand of layer 2: [out tile][k tile][r/4][lane][r%4]
-//   b2 [HT][16][2]
-//   w3 [d][HT][16][2]       output layer, by (j, k tile, r, half) for the VALU dot
+//   b2 [HT][2][16]
+//   w3 [d][HT][2][16]       output layer, by (j, k tile, half, r) for the VALU dot
 //   b3 [up4(d)]
 // then mask [up4(d)].
 struct AffineLayout {
@@ -76,8 +76,7 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) {
         f32x16 a0, a1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b1 + (ht * 16 + r) * 2 + h];
+        a0 = a1 = load_bias16(P + L.b1 + ht * 32, h);
 #pragma unroll
         for (int ks = 0; ks < KS1; ++ks) {
             const float w = P[L.w1 + (ht * KS1 + ks) * 64 + lane];
@@ -101,8 +100,7 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 #pragma unroll
     for (int hto = 0; hto < HT; ++hto) {
         f32x16 a0, a1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b2 + (hto * 16 + r) * 2 + h];
+        a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
 #pragma unroll
         for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -118,11 +116,11 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
         }
 #pragma unroll
         for (int j = 0; j < D; ++j) {
+            const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + hto) * 32, h);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float w3 = P[L.w3 + ((j * HT + hto) * 16 + r) * 2 + h];
-                part[j][0] = fmaf(w3, trelu(a0[r]), part[j][0]);
-                part[j][1] = fmaf(w3, trelu(a1[r]), part[j][1]);
+                part[j][0] = fmaf(w3[r], trelu(a0[r]), part[j][0]);
+                part[j][1] = fmaf(w3[r], trelu(a1[r]), part[j][1]);
             }
         }
     }

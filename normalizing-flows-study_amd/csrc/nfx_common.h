@@ -59,6 +59,15 @@ __device__ __forceinline__ float halves_other(float p0, float p1) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// 16 bias values of one accumulator tile for lane-half h: 4 x 16-byte reads, same address for
+// every lane of the half (broadcast), straight into the accumulator registers.
+__device__ __forceinline__ f32x16 load_bias16(const float* __restrict__ tile, int h) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(tile + 16 * h);
+    const f32x4 a = p[0], b = p[1], c = p[2], e = p[3];
+    return f32x16{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], c[0], c[1], c[2], c[3], e[0], e[1], e[2], e[3]};
+}
+
+
 // A zero the compiler cannot see through. Offsetting the LDS weight pointer by it inside a
 // grid-stride loop stops LICM from hoisting every (loop-invariant) weight read out of the
 // loop into registers, which would otherwise blow the VGPR budget and spill.

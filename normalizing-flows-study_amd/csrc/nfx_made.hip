@@ -25,7 +25,7 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
             int row = 32 * ht + (lane & 31), col = 2 * (4 * g + rr) + (lane >> 5);
             v = (row < H && col < d) ? mlp_weight(net, 0, d, row, col) : 0.f;
         } else if (i < L.w2) {
-            int t = i - L.b1, h = t & 1, r = (t >> 1) & 15, ht = t >> 5, row = 32 * ht + crow(r, h);
+            int t = i - L.b1, r = t & 15, h = (t >> 4) & 1, ht = t >> 5, row = 32 * ht + crow(r, h);
             v = row < H ? mlp_bias(net, 0, row) : 0.f;
         } else if (i < L.b2 || (i >= L.w3 && i < L.b3)) {
             const int layer = i < L.b2 ? 1 : 2;
@@ -35,7 +35,7 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
             v = (row < H && col < H) ? mlp_weight(net, layer, H, row, col) : 0.f;
         } else if (i < L.w3 || (i >= L.b3 && i < L.w4)) {
             const int layer = i < L.w3 ? 1 : 2;
-            int t = i - (layer == 1 ? L.b2 : L.b3), h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+            int t = i - (layer == 1 ? L.b2 : L.b3), r = t & 15, h = (t >> 4) & 1, ht = t >> 5;
             int row = 32 * ht + crow(r, h);
             v = row < H ? mlp_bias(net, layer, row) : 0.f;
         } else if (i < L.b4) {
@@ -44,7 +44,7 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
             int orow = 32 * j + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
             v = (orow < d && col < H) ? mlp_weight(net, 3, H, which * d + orow, col) : 0.f;
         } else if (i < L.par_total) {
-            int t = i - L.b4, h = t & 1, r = (t >> 1) & 15, jw = t >> 5, which = jw & 1, j = jw >> 1;
+            int t = i - L.b4, r = t & 15, h = (t >> 4) & 1, jw = t >> 5, which = jw & 1, j = jw >> 1;
             int orow = 32 * j + crow(r, h);
             v = orow < d ? mlp_bias(net, 3, which * d + orow) : 0.f;
         } else if (i < L.s_b1) {
@@ -168,7 +168,7 @@ extern "C" int nfx_made_affine(const float* packed, const float* in, float* out,
     hipStream_t s = (hipStream_t)stream;
     if ((variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) && d <= kTileMaxD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
-        const size_t tiles8 = 8 * 32 * (size_t)(d | 1) * sizeof(float);
+        const size_t tiles8 = 8 * 32 * (size_t)kTileStride * sizeof(float);
         const bool wlds = wbytes + tiles8 <= kLdsBytes;
         made_par_kernel_t k = pick_tile(HT, wlds, variant);
         if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no kernel for H=%d", H);

@@ -21,10 +21,10 @@ namespace nfx {
 
 // Packed image (floats), A-operand order, 4 consecutive k-steps per lane as one float4:
 //   w1 [HT][G1][64][4]    G1 = 4 * NKC k-step groups, NKC = ceil(d/32) input chunks
-//   b1 [HT][16][2]
-//   w2 [HT][HT][4][64][4], b2 [HT][16][2], w3 (same), b3
+//   b1 [HT][2][16]        bias at accumulator register r of lane-half h (row crow(r, h))
+//   w2 [HT][HT][4][64][4], b2 [HT][2][16], w3 (same), b3
 //   w4 [NJ][2][HT][4][64][4]  NJ = ceil(d/32) output tile pairs (0 = mu rows, 1 = alpha rows)
-//   b4 [NJ][2][16][2]
+//   b4 [NJ][2][2][16]
 // then, for the sequential kernels, plain row-major copies (Hp = 32*HT):
 //   s_w1t [d][Hp]  (W1m transposed: column i = the inputs' contributions of x_i)
 //   s_b1 [Hp], s_w2 [Hp][Hp], s_b2 [Hp], s_w3 [Hp][Hp], s_b3 [Hp]
@@ -71,6 +71,7 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
 }
 
 constexpr int kStageStride = 33;              // wave-private x tile [64][33] (conflict-free)
+constexpr int kTileStride = 65;               // made_tile_kernel x tile [32][65] (d <= 64)
 constexpr int kStageFloats = 64 * kStageStride;
 
 // Affine epilogues (exact reference op order and clamps).
@@ -136,8 +137,7 @@ __device__ __forceinline__ void made_hidden(const float* __restrict__ W, int wof
 #pragma unroll
     for (int hto = 0; hto < HT; ++hto) {
         f32x16 a0, a1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a0[r] = a1[r] = W[boff + (hto * 16 + r) * 2 + h];
+        a0 = a1 = load_bias16(W + boff + hto * 32, h);
 #pragma unroll
         for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -188,10 +188,7 @@ __global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
         // ---- layer 1: h1 = relu(W1m x + b1), K streamed in 32-dim chunks through LDS ----
         f32x16 h1[HT][2];
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) h1[ht][0][r] = h1[ht][1][r] = W[L.b1 + (ht * 16 + r) * 2 + h];
-        }
+        for (int ht = 0; ht < HT; ++ht) h1[ht][0] = h1[ht][1] = load_bias16(W + L.b1 + ht * 32, h);
         for (int kc = 0; kc < L.NKC; ++kc) {
             stage_in(in, base, d, B, 32 * kc, stg);
             wave_lds_sync();
@@ -232,11 +229,8 @@ __global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
         float acc0 = 0.f, acc1 = 0.f;
         for (int j = 0; j < L.NJ; ++j) {
             f32x16 mu0, mu1, al0, al1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                mu0[r] = mu1[r] = W[L.b4 + ((j * 2 + 0) * 16 + r) * 2 + h];
-                al0[r] = al1[r] = W[L.b4 + ((j * 2 + 1) * 16 + r) * 2 + h];
-            }
+            mu0 = mu1 = load_bias16(W + L.b4 + (j * 2 + 0) * 32, h);
+            al0 = al1 = load_bias16(W + L.b4 + (j * 2 + 1) * 32, h);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -434,8 +428,7 @@ __device__ __forceinline__ void made_hidden1(const float* __restrict__ W, int wo
     f32x16 a[HT];
 #pragma unroll
     for (int hto = 0; hto < HT; ++hto) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a[hto][r] = W[boff + (hto * 16 + r) * 2 + h];
+        a[hto] = load_bias16(W + boff + hto * 32, h);
     }
 #pragma unroll
     for (int kt = 0; kt < HT; ++kt) {
@@ -465,10 +458,10 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles) {
     const MadeLayout L = made_layout(d, HT);
-    const int S = d | 1;
+    constexpr int S = kTileStride;
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if constexpr (WLDS) {
         const f32x4* src = reinterpret_cast<const f32x4*>(packed);
         for (int i = threadIdx.x; i < L.par_total / 4; i += 512) lds4[i] = src[i];
@@ -477,29 +470,33 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
     if constexpr (WLDS) __syncthreads();
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
     const int64_t nwaves = (int64_t)gridDim.x * 8;
+    // Rows move through raw buffer loads/stores: the per-tile descriptor's range check returns 0
+    // for (and drops stores to) lanes >= d and rows >= B, so no per-row branches or 64-bit
+    // address arithmetic; the row offset r*d*4 rides in the scalar soffset.
+    const int voff = lane < d ? lane * 4 : (1 << 30);
+    const int rowb = d * 4;
 
     int64_t t = (int64_t)blockIdx.x * 8 + wave;
     float pf[32];
+    {
+        const int64_t rows = t < ntiles ? (B - t * 32 < 32 ? B - t * 32 : 32) : 0;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + (t < ntiles ? t * 32 * d : 0), 0,
+                                                          (int)(rows * rowb), 0x00020000);
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
-        const int64_t row = t * 32 + r;
-        pf[r] = (t < ntiles && row < B && lane < d) ? in[row * d + lane] : 0.f;
+        for (int r = 0; r < 32; ++r)
+            pf[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, r * rowb, 0));
     }
     for (; t < ntiles; t += nwaves) {
         const int64_t base = t * 32;
+        const int rows = (int)(B - base < 32 ? B - base : 32);
         const float* W = (WLDS ? lds : packed) + opaque_zero();
-        if (lane < d) {
 #pragma unroll
-            for (int r = 0; r < 32; ++r) xt[r * S + lane] = pf[r];
-        }
+        for (int r = 0; r < 32; ++r) xt[r * S + lane] = pf[r];
         wave_lds_sync();
 
         f32x16 h1[HT];
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) h1[ht][r] = W[L.b1 + (ht * 16 + r) * 2 + h];
-        }
+        for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(W + L.b1 + ht * 32, h);
         for (int kc = 0; kc < L.NKC; ++kc) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
@@ -509,8 +506,7 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
                     w[ht] = *reinterpret_cast<const f32x4*>(W + L.w1 + ((ht * 4 * L.NKC + kc * 4 + g) * 64 + lane) * 4);
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
-                    const int k = 32 * kc + 8 * g + 2 * rr + h;
-                    const float b = (k < d) ? xt[col * S + k] : 0.f;
+                    const float b = xt[col * S + 32 * kc + 8 * g + 2 * rr + h];
 #pragma unroll
                     for (int ht = 0; ht < HT; ++ht) h1[ht] = mfma32(w[ht][rr], b, h1[ht]);
                 }
@@ -526,21 +522,22 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
         made_hidden1<HT>(W, L.w3, L.b3, h2, h1);  // h3 -> h1
 
         // prefetch the next tile's rows while layer 4 runs
-        const int64_t tn = t + nwaves;
+        {
+            const int64_t tn = t + nwaves;
+            const int64_t rn = tn < ntiles ? (B - tn * 32 < 32 ? B - tn * 32 : 32) : 0;
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + (tn < ntiles ? tn * 32 * d : 0), 0,
+                                                              (int)(rn * rowb), 0x00020000);
 #pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            const int64_t row = tn * 32 + r;
-            pf[r] = (tn < ntiles && row < B && lane < d) ? in[row * d + lane] : 0.f;
+            for (int r = 0; r < 32; ++r)
+                pf[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, r * rowb, 0));
         }
 
+        // Layer 4 + affine epilogue. Padded output rows (dim >= d) have zero weights and bias:
+        // their alpha is 0 (adds nothing to the log-det) and their z lands in the tile padding.
         float acc = 0.f;
         for (int j = 0; j < L.NJ; ++j) {
-            f32x16 mu, al;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                mu[r] = W[L.b4 + ((j * 2 + 0) * 16 + r) * 2 + h];
-                al[r] = W[L.b4 + ((j * 2 + 1) * 16 + r) * 2 + h];
-            }
+            f32x16 mu = load_bias16(W + L.b4 + (j * 2 + 0) * 32, h);
+            f32x16 al = load_bias16(W + L.b4 + (j * 2 + 1) * 32, h);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -558,24 +555,19 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int dim = 32 * j + crow(r, h);
-                if (dim < d) {
-                    float* p = xt + col * S + dim;
-                    *p = made_affine<VAR>(*p, mu[r], al[r], acc);
-                }
+                float* p = xt + col * S + 32 * j + crow(r, h);
+                *p = made_affine<VAR>(*p, mu[r], al[r], acc);
             }
         }
         const float ssum = halves_sum(acc, acc);  // both halves of sample `col`
         wave_lds_sync();
-        if (lane < d) {
+        {
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + base * d, 0, rows * rowb, 0x00020000);
 #pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                const int64_t row = base + r;
-                if (row < B) out[row * d + lane] = xt[r * S + lane];
-            }
+            for (int r = 0; r < 32; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xt[r * S + lane]), rs, voff, r * rowb, 0);
         }
-        const int64_t so = base + col;
-        if (lane < 32 && so < B) {
+        if (lane < 32 && col < rows) {
             float ldv;
             if constexpr (VAR == NFX_MAF_INVERSE) {
                 ldv = -ssum;
@@ -586,6 +578,7 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
                 if (nonfinite(ldv)) ldv = 0.f;
                 ldv = tclamp(ldv, -50.f, 50.f);
             }
+            const int64_t so = base + col;
             logdet[so] = accumulate ? logdet[so] + ldv : ldv;
         }
         wave_lds_sync();

@@ -29,7 +29,7 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
             int row = 32 * ht + (lane & 31), col = 2 * ks + (lane >> 5);
             v = (row < H && col < d) ? mlp_weight(net, 0, d, row, col) : 0.f;
         } else if (i < L.w2) {
-            int t = i - L.b1, h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+            int t = i - L.b1, r = t & 15, h = (t >> 4) & 1, ht = t >> 5;
             int row = 32 * ht + crow(r, h);
             v = row < H ? mlp_bias(net, 0, row) : 0.f;
         } else if (i < L.b2) {
@@ -38,7 +38,7 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
             int row = 32 * hto + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
             v = (row < H && col < H) ? mlp_weight(net, 1, H, row, col) : 0.f;
         } else if (i < L.w3) {
-            int t = i - L.b2, h = t & 1, r = (t >> 1) & 15, ht = t >> 5;
+            int t = i - L.b2, r = t & 15, h = (t >> 4) & 1, ht = t >> 5;
             int row = 32 * ht + crow(r, h);
             v = row < H ? mlp_bias(net, 1, row) : 0.f;
         } else if (i < L.b3) {
@@ -48,7 +48,7 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
             int col = 32 * kt + crow(4 * rq + rr, lane >> 5);
             v = (dt >= 0 && p < P && col < H) ? mlp_weight(net, 2, H, dt * P + p, col) : 0.f;
         } else if (i < L.mask) {
-            int t = i - L.b3, h = t & 1, r = (t >> 1) & 15, tile = t >> 5;
+            int t = i - L.b3, r = t & 15, h = (t >> 4) & 1, tile = t >> 5;
             int dt = spline_tdim(mask, d, tile), p = crow(r, h);
             v = (dt >= 0 && p < P) ? mlp_bias(net, 2, dt * P + p) : 0.f;
         } else if (i < L.tdim) {

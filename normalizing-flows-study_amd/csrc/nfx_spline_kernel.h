@@ -22,11 +22,11 @@ __host__ __device__ constexpr int sp_up4(int v) { return (v + 3) & ~3; }
 
 // Packed image (floats):
 //   w1 [HT][4][64]         layer-1 A operand, k-steps padded to 4 (d <= 8)
-//   b1 [HT][16][2]
+//   b1 [HT][2][16]         (bias of accumulator register r, lane-half h)
 //   w2 [HT][HT][4][64][4]
-//   b2 [HT][16][2]
+//   b2 [HT][2][16]
 //   w3 [d][HT][4][64][4]   output tile t = t-th transformed dim: row i = parameter i
-//   b3 [d][16][2]
+//   b3 [d][2][16]
 //   mask [8], tdim [8] (indices of the transformed dims, as floats), meta [4] (meta[0] = NT)
 struct SplineLayout {
     int HT, NT;  // NT here = capacity (d); the live count is meta[0]
@@ -229,8 +229,7 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
             f32x16 a0, a1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b1 + (ht * 16 + r) * 2 + h];
+            a0 = a1 = load_bias16(P + L.b1 + ht * 32, h);
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 if (ks < KS1) {
@@ -252,8 +251,7 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
 #pragma unroll
         for (int hto = 0; hto < HT; ++hto) {
             f32x16 a0, a1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b2 + (hto * 16 + r) * 2 + h];
+            a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -283,8 +281,7 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
         for (int t = 0; t < NT; ++t) {
             // Layer 3, tile t: the 3K-1 parameters of transformed dim tdim[t].
             f32x16 a0, a1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a0[r] = a1[r] = P[L.b3 + (t * 16 + r) * 2 + h];
+            a0 = a1 = load_bias16(P + L.b3 + t * 32, h);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll

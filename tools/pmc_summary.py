@@ -17,7 +17,7 @@ import shutil
 import statistics
 import sys
 
-HOT = ("affine_coupling_kernel", "spline_coupling_kernel", "made_parallel_kernel", "made_seq_kernel",
+HOT = ("affine_coupling_kernel", "spline_coupling_kernel", "made_parallel_kernel", "made_tile_kernel", "made_seq_kernel",
        "gauss_logprob_kernel", "rqs_unit_kernel")
 
 
@@ -90,7 +90,7 @@ def main():
                 json.dump(res, f, indent=1)
             for p in glob.glob(os.path.join(d, cfg, "trace", "*", "*_kernel_stats.csv")):
                 shutil.copy(p, f"{dest}_{cfg}_kernel_stats.csv")
-            dom = {"affine_coupling_kernel": "cfg2", "spline_coupling_kernel": "cfg3", "made_parallel_kernel": "cfg4"}
+            dom = {"affine_coupling_kernel": "cfg2", "spline_coupling_kernel": "cfg3", "made_tile_kernel": "cfg4"}
             for k, s in res.items():
                 for tag, c in dom.items():
                     if tag in k and c == cfg and "hbm_bytes_per_launch" in s:
