@@ -478,7 +478,9 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
 
     int64_t t = (int64_t)blockIdx.x * 8 + wave;
     float pf[32];
+    float ldpf = 0.f;  // incoming log-det of the lane's sample (accumulate), prefetched too
     {
+        if (accumulate && t < ntiles && lane < 32 && t * 32 + col < B) ldpf = logdet[t * 32 + col];
         const int64_t rows = t < ntiles ? (B - t * 32 < 32 ? B - t * 32 : 32) : 0;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + (t < ntiles ? t * 32 * d : 0), 0,
                                                           (int)(rows * rowb), 0x00020000);
@@ -521,9 +523,11 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
         made_hidden1<HT>(W, L.w2, L.b2, h1, h2);
         made_hidden1<HT>(W, L.w3, L.b3, h2, h1);  // h3 -> h1
 
-        // prefetch the next tile's rows while layer 4 runs
+        // prefetch the next tile's rows (and incoming log-det) while layer 4 runs
+        const float ldin = ldpf;
         {
             const int64_t tn = t + nwaves;
+            ldpf = (accumulate && tn < ntiles && lane < 32 && tn * 32 + col < B) ? logdet[tn * 32 + col] : 0.f;
             const int64_t rn = tn < ntiles ? (B - tn * 32 < 32 ? B - tn * 32 : 32) : 0;
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + (tn < ntiles ? tn * 32 * d : 0), 0,
                                                               (int)(rn * rowb), 0x00020000);
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
                 ldv = tclamp(ldv, -50.f, 50.f);
             }
             const int64_t so = base + col;
-            logdet[so] = accumulate ? logdet[so] + ldv : ldv;
+            logdet[so] = accumulate ? ldin + ldv : ldv;
         }
         wave_lds_sync();
     }

@@ -197,32 +197,58 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
     const int KS1 = (d + 1) / 2;
     const int NT = (int)sm[L.meta];
 
-    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nchunks; c += nwaves) {
+    // Software pipeline: chunk c + nwaves's x rows and incoming log-det load while chunk c runs.
+    struct Fetch {
+        float xb[2][4];  // raw layer-1 operands x[sample base+32st+col][2ks+h]
+        float xr[8];     // the lane's own sample row
+        float ldin;
+    };
+    auto fetch = [&](int64_t c, Fetch& f) {
         const int64_t base = c * 64;
-        const float* P = sm + opaque_zero();
-
-        // Layer-1 B operands (x rescaled, times mask), k-steps padded to 4.
-        float xb[2][4];
+        const bool live = c < nchunks;
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
             const int64_t s = base + 32 * st + col;
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 const int k = 2 * ks + h;
-                float v = 0.f;
-                if (ks < KS1 && k < d && s < B) {
-                    float xv = in[s * d + k];
-                    if (C.rescale) xv = C.rs_to_scale * (xv - C.rs_lo) - C.bound;
-                    v = xv * P[L.mask + k];
-                }
-                xb[st][ks] = v;
+                f.xb[st][ks] = (live && ks < KS1 && k < d && s < B) ? in[s * d + k] : 0.f;
             }
         }
-        // Own sample row (lane l <-> sample base + l).
+        const int64_t so = base + lane;
+        const bool row = live && so < B;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f.xr[j] = (row && j < d) ? in[so * d + j] : 0.f;
+        f.ldin = (row && accumulate) ? logdet[so] : 0.f;
+    };
+    float mkb[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) mkb[ks] = (2 * ks + h < d) ? sm[L.mask + 2 * ks + h] : 0.f;
+
+    int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    Fetch cur;
+    fetch(c, cur);
+    for (; c < nchunks; c += nwaves) {
+        const int64_t base = c * 64;
+        const float* P = sm + opaque_zero();
+        Fetch nxt;
+        fetch(c + nwaves, nxt);
+
+        // Layer-1 B operands (x rescaled, times mask), k-steps padded to 4.
+        float xb[2][4];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                float xv = cur.xb[st][ks];
+                if (C.rescale) xv = C.rs_to_scale * (xv - C.rs_lo) - C.bound;
+                xb[st][ks] = xv * mkb[ks];
+            }
+        }
         const int64_t so = base + lane;
         float xr[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xr[j] = (j < d && so < B) ? in[so * d + j] : 0.f;
+        for (int j = 0; j < 8; ++j) xr[j] = cur.xr[j];
 
         // Layer 1 + ReLU
         f32x16 h1[HT][2];
@@ -322,8 +348,9 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
                 if (j < d) out[so * d + j] = nonfinite(y[j]) ? 0.f : y[j];
             }
             if (nonfinite(ld)) ld = 0.f;
-            logdet[so] = accumulate ? logdet[so] + ld : ld;
+            logdet[so] = accumulate ? cur.ldin + ld : ld;
         }
+        cur = nxt;
     }
 }
 
