@@ -83,6 +83,12 @@ int nfx_affine_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, const float*
                     int H, float* packed, void* stream);
 int nfx_affine_coupling(const float* packed, const float* in, float* out, float* log_det,
                         int64_t B, int d, int H, int direction, int accumulate, void* stream);
+/* Inverse + fused log_prob epilogue (the last layer of an inverse chain): also writes
+ * logp[i] = -0.5*(fp32(d log 2pi) + sum_j out[i,j]^2) + log_det[i] and sums[2] as
+ * nfx_gauss_logprob does; `workspace` holds nfx_gauss_workspace_bytes(B) bytes. */
+int nfx_affine_coupling_logprob(const float* packed, const float* in, float* out, float* log_det,
+                                float* logp, double* sums, void* workspace, int64_t B, int d,
+                                int H, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Rational-quadratic spline coupling — SplineCouplingLayer
@@ -99,6 +105,12 @@ int nfx_spline_coupling(const float* packed, const float* in, float* out, float*
                         float min_bin_height, float min_derivative, int rescale,
                         float data_min, float data_max, int direction, int accumulate,
                         void* stream);
+/* Inverse + fused log_prob epilogue (see nfx_affine_coupling_logprob). */
+int nfx_spline_coupling_logprob(const float* packed, const float* in, float* out, float* log_det,
+                                float* logp, double* sums, void* workspace, int64_t B, int d,
+                                int H, int K, float bound, float min_bin_width,
+                                float min_bin_height, float min_derivative, int rescale,
+                                float data_min, float data_max, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Unit-interval RQ spline — rational_quadratic_spline
@@ -123,6 +135,11 @@ size_t nfx_made_packed_floats(int d, int H);
 int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
 int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
                     int64_t B, int d, int H, int variant, int accumulate, void* stream);
+/* NFX_MAF_INVERSE (d <= 64) + fused log_prob epilogue (see nfx_affine_coupling_logprob);
+ * NFX_EUNSUPPORTED otherwise (use nfx_gauss_logprob after nfx_made_affine). */
+int nfx_made_affine_logprob(const float* packed, const float* in, float* out, float* log_det,
+                            float* logp, double* sums, void* workspace, int64_t B, int d, int H,
+                            int variant, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Gaussian base log-density + NLL partial sums — the log_prob glue of the callers

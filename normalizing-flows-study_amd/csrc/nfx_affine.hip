@@ -65,14 +65,41 @@ __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float
     }
 }
 
-static affine_kernel_t pick_affine(int HT, int d, int dir) {
+static affine_kernel_t pick_affine(int HT, int d, int dir, bool logp) {
     switch (HT) {
-        case 1: return affine_pick_ht<1>(d, dir);
-        case 2: return affine_pick_ht<2>(d, dir);
-        case 3: return affine_pick_ht<3>(d, dir);
-        case 4: return affine_pick_ht<4>(d, dir);
+        case 1: return affine_pick_ht<1>(d, dir, logp);
+        case 2: return affine_pick_ht<2>(d, dir, logp);
+        case 3: return affine_pick_ht<3>(d, dir, logp);
+        case 4: return affine_pick_ht<4>(d, dir, logp);
         default: return nullptr;
     }
+}
+
+static int affine_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
+                         int d, int H, int direction, int accumulate, float* logp, double* sums,
+                         void* workspace, hipStream_t stream) {
+    const bool fused = sums != nullptr;
+    if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "affine_coupling: bad shape B=%lld d=%d H=%d", (long long)B, d, H);
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE)
+        return set_error(NFX_EINVAL, "affine_coupling: direction must be +1 or -1");
+    if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "affine_coupling_logprob: null logp/workspace");
+    const int HT = (H + 31) / 32;
+    affine_kernel_t k = pick_affine(HT, d, direction, fused);
+    if (!k) return set_error(NFX_EUNSUPPORTED, "affine_coupling: d=%d H=%d outside the compiled family (d<=8, H<=128)", d, H);
+    if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, stream) : NFX_OK;
+    if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "affine_coupling: null pointer");
+    if (in == out) return set_error(NFX_EINVAL, "affine_coupling: in and out must not alias");
+    const size_t lds = (size_t)affine_layout(d, HT).total * sizeof(float);
+    int rc = prepare_lds((const void*)k, lds);
+    if (rc) return rc;
+    const int64_t nchunks = (B + 63) / 64;
+    int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
+    if (grid > kMaxPartials) grid = kMaxPartials;
+    double* partials = reinterpret_cast<double*>(workspace);
+    k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, accumulate, nchunks, logp, partials, gauss_const(d));
+    rc = check_launch("affine_coupling_kernel");
+    if (rc || !fused) return rc;
+    return gauss_finish(partials, grid, sums, B, stream);
 }
 
 // Grid: enough resident workgroups to fill every CU (occupancy from the runtime), never more
@@ -123,20 +150,14 @@ extern "C" int nfx_affine_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, c
 extern "C" int nfx_affine_coupling(const float* packed, const float* in, float* out, float* log_det,
                                    int64_t B, int d, int H, int direction, int accumulate,
                                    void* stream) {
-    if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "affine_coupling: bad shape B=%lld d=%d H=%d", (long long)B, d, H);
-    if (direction != NFX_FORWARD && direction != NFX_INVERSE)
-        return set_error(NFX_EINVAL, "affine_coupling: direction must be +1 or -1");
-    if (B == 0) return NFX_OK;
-    if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "affine_coupling: null pointer");
-    if (in == out) return set_error(NFX_EINVAL, "affine_coupling: in and out must not alias");
-    const int HT = (H + 31) / 32;
-    affine_kernel_t k = pick_affine(HT, d, direction);
-    if (!k) return set_error(NFX_EUNSUPPORTED, "affine_coupling: d=%d H=%d outside the compiled family (d<=8, H<=128)", d, H);
-    const size_t lds = (size_t)affine_layout(d, HT).total * sizeof(float);
-    int rc = prepare_lds((const void*)k, lds);
-    if (rc) return rc;
-    const int64_t nchunks = (B + 63) / 64;
-    const int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
-    k<<<grid, 256, lds, (hipStream_t)stream>>>(packed, in, out, log_det, B, accumulate, nchunks);
-    return check_launch("affine_coupling_kernel");
+    return affine_launch(packed, in, out, log_det, B, d, H, direction, accumulate, nullptr, nullptr,
+                         nullptr, (hipStream_t)stream);
+}
+
+extern "C" int nfx_affine_coupling_logprob(const float* packed, const float* in, float* out,
+                                           float* log_det, float* logp, double* sums, void* workspace,
+                                           int64_t B, int d, int H, int accumulate, void* stream) {
+    if (!sums) return set_error(NFX_EINVAL, "affine_coupling_logprob: null sums");
+    return affine_launch(packed, in, out, log_det, B, d, H, NFX_INVERSE, accumulate, logp, sums,
+                         workspace, (hipStream_t)stream);
 }

@@ -1,25 +1,26 @@
 // Explicit instantiations of the affine-coupling kernel for hidden tiles HT = 2
-// (one translation unit per HT so the build compiles them in parallel).
+// (d = 1..8, both directions, + the fused-log_prob inverse; one TU per HT for a parallel build).
 #include "nfx_affine_kernel.h"
 
 namespace nfx {
 
-template <int HT, int D>
-static affine_kernel_t pick_dir(int dir) {
-    return dir < 0 ? affine_coupling_kernel<HT, D, -1> : affine_coupling_kernel<HT, D, 1>;
+template <int D>
+static affine_kernel_t pick_2(int dir, bool logp) {
+    if (dir > 0) return affine_coupling_kernel<2, D, 1, false>;
+    return logp ? affine_coupling_kernel<2, D, -1, true> : affine_coupling_kernel<2, D, -1, false>;
 }
 
 template <>
-affine_kernel_t affine_pick_ht<2>(int d, int dir) {
+affine_kernel_t affine_pick_ht<2>(int d, int dir, bool logp) {
     switch (d) {
-        case 1: return pick_dir<2, 1>(dir);
-        case 2: return pick_dir<2, 2>(dir);
-        case 3: return pick_dir<2, 3>(dir);
-        case 4: return pick_dir<2, 4>(dir);
-        case 5: return pick_dir<2, 5>(dir);
-        case 6: return pick_dir<2, 6>(dir);
-        case 7: return pick_dir<2, 7>(dir);
-        case 8: return pick_dir<2, 8>(dir);
+        case 1: return pick_2<1>(dir, logp);
+        case 2: return pick_2<2>(dir, logp);
+        case 3: return pick_2<3>(dir, logp);
+        case 4: return pick_2<4>(dir, logp);
+        case 5: return pick_2<5>(dir, logp);
+        case 6: return pick_2<6>(dir, logp);
+        case 7: return pick_2<7>(dir, logp);
+        case 8: return pick_2<8>(dir, logp);
         default: return nullptr;
     }
 }

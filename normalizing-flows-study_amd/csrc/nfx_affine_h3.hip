@@ -1,25 +1,26 @@
 // Explicit instantiations of the affine-coupling kernel for hidden tiles HT = 3
-// (one translation unit per HT so the build compiles them in parallel).
+// (d = 1..8, both directions, + the fused-log_prob inverse; one TU per HT for a parallel build).
 #include "nfx_affine_kernel.h"
 
 namespace nfx {
 
-template <int HT, int D>
-static affine_kernel_t pick_dir(int dir) {
-    return dir < 0 ? affine_coupling_kernel<HT, D, -1> : affine_coupling_kernel<HT, D, 1>;
+template <int D>
+static affine_kernel_t pick_3(int dir, bool logp) {
+    if (dir > 0) return affine_coupling_kernel<3, D, 1, false>;
+    return logp ? affine_coupling_kernel<3, D, -1, true> : affine_coupling_kernel<3, D, -1, false>;
 }
 
 template <>
-affine_kernel_t affine_pick_ht<3>(int d, int dir) {
+affine_kernel_t affine_pick_ht<3>(int d, int dir, bool logp) {
     switch (d) {
-        case 1: return pick_dir<3, 1>(dir);
-        case 2: return pick_dir<3, 2>(dir);
-        case 3: return pick_dir<3, 3>(dir);
-        case 4: return pick_dir<3, 4>(dir);
-        case 5: return pick_dir<3, 5>(dir);
-        case 6: return pick_dir<3, 6>(dir);
-        case 7: return pick_dir<3, 7>(dir);
-        case 8: return pick_dir<3, 8>(dir);
+        case 1: return pick_3<1>(dir, logp);
+        case 2: return pick_3<2>(dir, logp);
+        case 3: return pick_3<3>(dir, logp);
+        case 4: return pick_3<4>(dir, logp);
+        case 5: return pick_3<5>(dir, logp);
+        case 6: return pick_3<6>(dir, logp);
+        case 7: return pick_3<7>(dir, logp);
+        case 8: return pick_3<8>(dir, logp);
         default: return nullptr;
     }
 }

@@ -131,10 +131,13 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
         res[j] = tclamp(halves_sum(part[j][0], part[j][1]) + P[L.b3 + j], -10.f, 10.f);
 }
 
-template <int HT, int D, int DIR>
+// LOGP: fused log_prob epilogue for the last layer of an inverse chain — logp = -0.5*(c +
+// sum_j z_j^2) + total log-det per sample, and one float64 partial sum per workgroup.
+template <int HT, int D, int DIR, bool LOGP>
 __global__ __launch_bounds__(256) void affine_coupling_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
-    float* __restrict__ logdet, int64_t B, int accumulate, int64_t nchunks) {
+    float* __restrict__ logdet, int64_t B, int accumulate, int64_t nchunks,
+    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
     extern __shared__ f32x4 lds4[];
@@ -186,6 +189,7 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
     int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     Fetch cur;
     fetch(c, cur);
+    double lpacc = 0.0;
     for (; c < nchunks; c += nwaves) {
         const int64_t base = c * 64;
         const float* smi = sm + opaque_zero();
@@ -204,6 +208,7 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
 
         const int64_t so = base + lane;
         if (so < B) {
+#pragma clang fp contract(off)  // separate mul/add roundings, as the reference's torch ops
             float y[D];
             float ld = 0.f;
 #pragma unroll
@@ -223,15 +228,29 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
             }
             if (nonfinite(ld)) ld = 0.f;
             store_row<D>(out + so * D, y);
-            logdet[so] = accumulate ? cur.ldin + ld : ld;
+            const float ldt = accumulate ? cur.ldin + ld : ld;
+            logdet[so] = ldt;
+            if constexpr (LOGP) {
+                float m = gauss_sq0(y[0]);
+#pragma unroll
+                for (int j = 1; j < D; ++j) m = gauss_sq(m, y[j]);
+                const float lp = gauss_lp(m, cgauss, ldt);
+                logp[so] = lp;
+                lpacc += (double)lp;
+            }
         }
         cur = nxt;
     }
+    if constexpr (LOGP) {
+        const double t = block_sum_f64<256>(lpacc);
+        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+    }
 }
 
-typedef void (*affine_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int64_t);
+typedef void (*affine_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int64_t,
+                                float*, double*, float);
 
 template <int HT>
-affine_kernel_t affine_pick_ht(int d, int dir);
+affine_kernel_t affine_pick_ht(int d, int dir, bool logp);
 
 }  // namespace nfx

@@ -77,6 +77,42 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
+// Workgroup sum of a float64 (NT threads, wave64 shuffles then one LDS hop). Result valid in
+// thread 0. Deterministic order.
+template <int NT>
+__device__ __forceinline__ double block_sum_f64(double v) {
+    __shared__ double red[NT / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < NT / 64; ++w) t += red[w];
+    return t;
+}
+
+// fp32(d * log(2*pi)) exactly as torch's MultivariateNormal.log_prob rounds it.
+inline float gauss_const(int d) { return (float)((double)d * 1.8378770664093453); }
+
+// Gaussian log-density pieces with every rounding explicit (no FMA contraction), so the fused
+// epilogues and nfx_gauss_logprob produce bit-identical logp: m = sum_j z_j^2 in order, then
+// logp = -0.5 * (m + c) + log_det (separate mul/add, as torch's CPU kernels round).
+// (__fadd_rn/__fmul_rn alone do not stop the backend from fusing; the pragma does.)
+__device__ __forceinline__ float gauss_sq0(float v) { return v * v; }
+__device__ __forceinline__ float gauss_sq(float m, float v) {
+#pragma clang fp contract(off)
+    return m + v * v;
+}
+__device__ __forceinline__ float gauss_lp(float m, float c, float ld) {
+#pragma clang fp contract(off)
+    return -0.5f * (m + c) + ld;
+}
+
+// Capacity (doubles) of the partial-sum workspace shared by nfx_gauss_logprob and the fused
+// *_logprob layer epilogues; every launch that writes partials uses at most this many blocks.
+constexpr int kMaxPartials = 4096;
+
 }  // namespace nfx
 
 // Error reporting shared by the C-ABI translation units (nfx_abi.hip).
@@ -88,4 +124,6 @@ int num_cus();
 int resident_grid(const void* kernel, int threads, size_t lds_bytes, int64_t work_groups);
 // Raise the dynamic-LDS limit of `kernel` when it needs more than 64 KiB.
 int prepare_lds(const void* kernel, size_t bytes);
+// Reduce n float64 partials into sums[0] = total, sums[1] = (double)B (one 256-thread block).
+int gauss_finish(const double* partials, int n, double* sums, int64_t B, hipStream_t s);
 }  // namespace nfx

@@ -14,18 +14,9 @@ namespace nfx {
 
 constexpr int kGaussThreads = 256;
 constexpr int kGaussMaxBlocks = 1024;
+static_assert(kGaussMaxBlocks <= kMaxPartials, "partials capacity");
 
-__device__ __forceinline__ double block_sum_f64(double v) {
-    __shared__ double red[kGaussThreads / 64];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double t = 0.0;
-    if (threadIdx.x == 0)
-        for (int w = 0; w < kGaussThreads / 64; ++w) t += red[w];
-    return t;
-}
+__device__ __forceinline__ double block_sum_f64(double v) { return block_sum_f64<kGaussThreads>(v); }
 
 __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
     const float* __restrict__ z, const float* __restrict__ ld, float* __restrict__ logp,
@@ -34,9 +25,9 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
     for (int64_t i = (int64_t)blockIdx.x * kGaussThreads + threadIdx.x; i < B;
          i += (int64_t)gridDim.x * kGaussThreads) {
         const float* zr = z + i * d;
-        float m = zr[0] * zr[0];
-        for (int j = 1; j < d; ++j) m = m + zr[j] * zr[j];
-        const float lp = -0.5f * (m + c) + ld[i];
+        float m = gauss_sq0(zr[0]);
+        for (int j = 1; j < d; ++j) m = gauss_sq(m, zr[j]);
+        const float lp = gauss_lp(m, c, ld[i]);
         if (logp) logp[i] = lp;
         acc += (double)lp;
     }
@@ -73,7 +64,7 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_tiled_kernel(
             const int n = (d - dim0) < 32 ? (d - dim0) : 32;
             for (int j = 0; j < n; ++j) {
                 const float v = st[lane * 33 + j];
-                m = (dim0 == 0 && j == 0) ? v * v : m + v * v;
+                m = (dim0 == 0 && j == 0) ? gauss_sq0(v) : gauss_sq(m, v);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -81,7 +72,7 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_tiled_kernel(
         }
         const int64_t i = base + lane;
         if (i < B) {
-            const float lp = -0.5f * (m + c) + ld[i];
+            const float lp = gauss_lp(m, c, ld[i]);
             if (logp) logp[i] = lp;
             acc += (double)lp;
         }
@@ -102,13 +93,18 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_finish_kernel(const doubl
     }
 }
 
+int gauss_finish(const double* partials, int n, double* sums, int64_t B, hipStream_t s) {
+    gauss_finish_kernel<<<1, kGaussThreads, 0, s>>>(partials, n, sums, B);
+    return check_launch("gauss_finish_kernel");
+}
+
 }  // namespace nfx
 
 using namespace nfx;
 
 extern "C" size_t nfx_gauss_workspace_bytes(int64_t B) {
     (void)B;
-    return (size_t)kGaussMaxBlocks * sizeof(double);
+    return (size_t)kMaxPartials * sizeof(double);
 }
 
 extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
@@ -120,7 +116,7 @@ extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* lo
     int blocks = (int)((B + kGaussThreads - 1) / kGaussThreads);
     if (blocks > kGaussMaxBlocks) blocks = kGaussMaxBlocks;
     if (blocks < 1) blocks = 1;
-    const float c = (float)((double)d * log(2.0 * M_PI));
+    const float c = gauss_const(d);
     double* partials = reinterpret_cast<double*>(workspace);
     if (B > 0 && d > 8) {
         int64_t tb = ((B + 63) / 64 + 3) / 4;
@@ -135,6 +131,5 @@ extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* lo
     } else {
         blocks = 0;
     }
-    gauss_finish_kernel<<<1, kGaussThreads, 0, s>>>(partials, blocks, sums, B);
-    return check_launch("gauss_finish_kernel");
+    return gauss_finish(partials, blocks, sums, B, s);
 }

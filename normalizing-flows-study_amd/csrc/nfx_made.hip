@@ -108,12 +108,12 @@ static made_par_kernel_t pick_par(int HT, bool wlds, int variant) {
     }
 }
 
-static made_par_kernel_t pick_tile(int HT, bool wlds, int variant) {
+static made_par_kernel_t pick_tile(int HT, bool wlds, int variant, bool logp) {
     switch (HT) {
-        case 1: return made_tile_pick_ht<1>(wlds, variant);
-        case 2: return made_tile_pick_ht<2>(wlds, variant);
-        case 3: return made_tile_pick_ht<3>(wlds, variant);
-        case 4: return made_tile_pick_ht<4>(wlds, variant);
+        case 1: return made_tile_pick_ht<1>(wlds, variant, logp);
+        case 2: return made_tile_pick_ht<2>(wlds, variant, logp);
+        case 3: return made_tile_pick_ht<3>(wlds, variant, logp);
+        case 4: return made_tile_pick_ht<4>(wlds, variant, logp);
         default: return nullptr;
     }
 }
@@ -154,31 +154,40 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     return check_launch("made_pack_kernel");
 }
 
-extern "C" int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
-                               int64_t B, int d, int H, int variant, int accumulate, void* stream) {
+static int made_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
+                       int d, int H, int variant, int accumulate, float* logp, double* sums,
+                       void* workspace, hipStream_t s) {
+    const bool fused = sums != nullptr;
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine: bad shape");
     if (d > 4096 || H > 128) return set_error(NFX_EUNSUPPORTED, "made_affine: d=%d H=%d outside d<=4096, H<=128", d, H);
     if (variant < NFX_MAF_INVERSE || variant > NFX_IAF_INVERSE)
         return set_error(NFX_EINVAL, "made_affine: unknown variant %d", variant);
-    if (B == 0) return NFX_OK;
+    if (fused && (variant != NFX_MAF_INVERSE || d > kTileMaxD))
+        return set_error(NFX_EUNSUPPORTED, "made_affine_logprob: fused log_prob needs MAF inverse with d <= %d", kTileMaxD);
+    if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "made_affine_logprob: null logp/workspace");
+    if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, s) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "made_affine: null pointer");
     if (in == out) return set_error(NFX_EINVAL, "made_affine: in and out must not alias");
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
-    hipStream_t s = (hipStream_t)stream;
+    double* partials = reinterpret_cast<double*>(workspace);
     if ((variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) && d <= kTileMaxD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
         const size_t tiles8 = 8 * 32 * (size_t)kTileStride * sizeof(float);
         const bool wlds = wbytes + tiles8 <= kLdsBytes;
-        made_par_kernel_t k = pick_tile(HT, wlds, variant);
+        made_par_kernel_t k = pick_tile(HT, wlds, variant, fused);
         if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no kernel for H=%d", H);
         const size_t lds = (wlds ? wbytes : 0) + tiles8;
         int rc = prepare_lds((const void*)k, lds);
         if (rc) return rc;
         const int64_t ntiles = (B + 31) / 32;
-        const int grid = resident_grid((const void*)k, 512, lds, (ntiles + 7) / 8);
-        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles);
-        return check_launch("made_tile_kernel");
+        int grid = resident_grid((const void*)k, 512, lds, (ntiles + 7) / 8);
+        if (grid > kMaxPartials) grid = kMaxPartials;
+        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials,
+                                 gauss_const(d));
+        rc = check_launch("made_tile_kernel");
+        if (rc || !fused) return rc;
+        return gauss_finish(partials, grid, sums, B, s);
     }
     if (variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
@@ -193,7 +202,7 @@ extern "C" int nfx_made_affine(const float* packed, const float* in, float* out,
         const int64_t nchunks = (B + 63) / 64;
         const int nw = threads / 64;
         const int grid = resident_grid((const void*)k, threads, lds, (nchunks + nw - 1) / nw);
-        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks);
+        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, nullptr, nullptr, 0.f);
         return check_launch("made_parallel_kernel");
     }
     made_seq_kernel_t k = pick_seq(HT, variant);
@@ -204,4 +213,18 @@ extern "C" int nfx_made_affine(const float* packed, const float* in, float* out,
     const int64_t grid = (B + 63) / 64;
     k<<<(unsigned)grid, 64, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate);
     return check_launch("made_seq_kernel");
+}
+
+extern "C" int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
+                               int64_t B, int d, int H, int variant, int accumulate, void* stream) {
+    return made_launch(packed, in, out, log_det, B, d, H, variant, accumulate, nullptr, nullptr, nullptr,
+                       (hipStream_t)stream);
+}
+
+extern "C" int nfx_made_affine_logprob(const float* packed, const float* in, float* out, float* log_det,
+                                       float* logp, double* sums, void* workspace, int64_t B, int d,
+                                       int H, int variant, int accumulate, void* stream) {
+    if (!sums) return set_error(NFX_EINVAL, "made_affine_logprob: null sums");
+    return made_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, sums, workspace,
+                       (hipStream_t)stream);
 }

@@ -77,6 +77,7 @@ constexpr int kStageFloats = 64 * kStageStride;
 // Affine epilogues (exact reference op order and clamps).
 template <int VAR>
 __device__ __forceinline__ float made_affine(float xv, float mu, float al, float& acc) {
+#pragma clang fp contract(off)  // separate mul/add roundings, as the reference's torch ops
     if constexpr (VAR == NFX_MAF_INVERSE) {
         // masked_autoregressive_flow.py:25-31: alpha = clamp(alpha,-3,3);
         // z = (x - mu) * exp(clamp(-alpha, -5, 5)); guard z -> 0 (:35)
@@ -163,7 +164,8 @@ __device__ __forceinline__ void made_hidden(const float* __restrict__ W, int wof
 template <int HT, bool WLDS, int VAR>
 __global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
-    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t nchunks) {
+    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t nchunks,
+    float* __restrict__ /*logp*/, double* __restrict__ /*partials*/, float /*cgauss*/) {
     constexpr int NWAVE = WLDS ? 8 : 4;
     const MadeLayout L = made_layout(d, HT);
     extern __shared__ f32x4 lds4[];
@@ -453,10 +455,11 @@ __device__ __forceinline__ void made_hidden1(const float* __restrict__ W, int wo
     }
 }
 
-template <int HT, bool WLDS, int VAR>
+template <int HT, bool WLDS, int VAR, bool LOGP>
 __global__ __launch_bounds__(512) void made_tile_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
-    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles) {
+    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles,
+    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
     const MadeLayout L = made_layout(d, HT);
     constexpr int S = kTileStride;
     extern __shared__ f32x4 lds4[];
@@ -477,6 +480,7 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
     const int rowb = d * 4;
 
     int64_t t = (int64_t)blockIdx.x * 8 + wave;
+    double lpacc = 0.0;
     float pf[32];
     float ldpf = 0.f;  // incoming log-det of the lane's sample (accumulate), prefetched too
     {
@@ -565,6 +569,15 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
         }
         const float ssum = halves_sum(acc, acc);  // both halves of sample `col`
         wave_lds_sync();
+        float zsq = 0.f;  // fused log_prob: sum_j z_j^2 of sample `col`, in dimension order
+        if constexpr (LOGP) {
+            if (lane < 32) {
+                for (int jd = 0; jd < d; ++jd) {
+                    const float v = xt[col * S + jd];
+                    zsq = (jd == 0) ? gauss_sq0(v) : gauss_sq(zsq, v);
+                }
+            }
+        }
         {
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + base * d, 0, rows * rowb, 0x00020000);
 #pragma unroll
@@ -583,18 +596,29 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
                 ldv = tclamp(ldv, -50.f, 50.f);
             }
             const int64_t so = base + col;
-            logdet[so] = accumulate ? ldin + ldv : ldv;
+            const float ldt = accumulate ? ldin + ldv : ldv;
+            logdet[so] = ldt;
+            if constexpr (LOGP) {
+                const float lp = gauss_lp(zsq, cgauss, ldt);
+                logp[so] = lp;
+                lpacc += (double)lp;
+            }
         }
         wave_lds_sync();
     }
+    if constexpr (LOGP) {
+        const double tsum = block_sum_f64<512>(lpacc);
+        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    }
 }
 
-typedef void (*made_par_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t);
+typedef void (*made_par_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t,
+                                  float*, double*, float);
 
 template <int HT>
 made_par_kernel_t made_pick_ht(bool wlds, int variant);
 template <int HT>
-made_par_kernel_t made_tile_pick_ht(bool wlds, int variant);
+made_par_kernel_t made_tile_pick_ht(bool wlds, int variant, bool logp);
 template <int HT>
 made_seq_kernel_t made_seq_pick_ht(int variant);
 

@@ -20,18 +20,18 @@ template made_par_kernel_t made_pick_ht<3>(bool, int);
 template made_par_kernel_t made_pick_ht<4>(bool, int);
 
 template <int HT, bool WLDS>
-static made_par_kernel_t tile_var(int variant) {
-    return variant == NFX_MAF_INVERSE ? made_tile_kernel<HT, WLDS, NFX_MAF_INVERSE>
-                                      : made_tile_kernel<HT, WLDS, NFX_IAF_FORWARD>;
+static made_par_kernel_t tile_var(int variant, bool logp) {
+    if (variant != NFX_MAF_INVERSE) return made_tile_kernel<HT, WLDS, NFX_IAF_FORWARD, false>;
+    return logp ? made_tile_kernel<HT, WLDS, NFX_MAF_INVERSE, true> : made_tile_kernel<HT, WLDS, NFX_MAF_INVERSE, false>;
 }
 
 template <int HT>
-made_par_kernel_t made_tile_pick_ht(bool wlds, int variant) {
-    return wlds ? tile_var<HT, true>(variant) : tile_var<HT, false>(variant);
+made_par_kernel_t made_tile_pick_ht(bool wlds, int variant, bool logp) {
+    return wlds ? tile_var<HT, true>(variant, logp) : tile_var<HT, false>(variant, logp);
 }
-template made_par_kernel_t made_tile_pick_ht<1>(bool, int);
-template made_par_kernel_t made_tile_pick_ht<2>(bool, int);
-template made_par_kernel_t made_tile_pick_ht<3>(bool, int);
-template made_par_kernel_t made_tile_pick_ht<4>(bool, int);
+template made_par_kernel_t made_tile_pick_ht<1>(bool, int, bool);
+template made_par_kernel_t made_tile_pick_ht<2>(bool, int, bool);
+template made_par_kernel_t made_tile_pick_ht<3>(bool, int, bool);
+template made_par_kernel_t made_tile_pick_ht<4>(bool, int, bool);
 
 }  // namespace nfx

@@ -66,12 +66,12 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
     }
 }
 
-static spline_kernel_t pick_spline(int HT, int K, int dir) {
+static spline_kernel_t pick_spline(int HT, int K, int dir, bool logp) {
     switch (HT) {
-        case 1: return spline_pick_ht<1>(K, dir);
-        case 2: return spline_pick_ht<2>(K, dir);
-        case 3: return spline_pick_ht<3>(K, dir);
-        case 4: return spline_pick_ht<4>(K, dir);
+        case 1: return spline_pick_ht<1>(K, dir, logp);
+        case 2: return spline_pick_ht<2>(K, dir, logp);
+        case 3: return spline_pick_ht<3>(K, dir, logp);
+        case 4: return spline_pick_ht<4>(K, dir, logp);
         default: return nullptr;
     }
 }
@@ -99,21 +99,23 @@ extern "C" int nfx_spline_pack(const NfxMlpRaw* net, const float* mask, int d, i
     return check_launch("spline_pack_kernel");
 }
 
-extern "C" int nfx_spline_coupling(const float* packed, const float* in, float* out, float* log_det,
-                                   int64_t B, int d, int H, int K, float bound, float min_bin_width,
-                                   float min_bin_height, float min_derivative, int rescale,
-                                   float data_min, float data_max, int direction, int accumulate,
-                                   void* stream) {
+static int spline_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
+                         int d, int H, int K, float bound, float min_bin_width, float min_bin_height,
+                         float min_derivative, int rescale, float data_min, float data_max,
+                         int direction, int accumulate, float* logp, double* sums, void* workspace,
+                         hipStream_t stream) {
+    const bool fused = sums != nullptr;
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "spline_coupling: bad shape");
     if (direction != NFX_FORWARD && direction != NFX_INVERSE)
         return set_error(NFX_EINVAL, "spline_coupling: direction must be +1 or -1");
     if (d > 8 || H > 128 || K < 2 || K > 11)
         return set_error(NFX_EUNSUPPORTED, "spline_coupling: d=%d H=%d K=%d outside d<=8, H<=128, 2<=K<=11", d, H, K);
-    if (B == 0) return NFX_OK;
+    if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "spline_coupling_logprob: null logp/workspace");
+    if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, stream) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "spline_coupling: null pointer");
     if (in == out) return set_error(NFX_EINVAL, "spline_coupling: in and out must not alias");
     const int HT = (H + 31) / 32;
-    spline_kernel_t k = pick_spline(HT, K, direction);
+    spline_kernel_t k = pick_spline(HT, K, direction, fused);
     if (!k) return set_error(NFX_EUNSUPPORTED, "spline_coupling: no kernel for H=%d K=%d", H, K);
     // Scalars exactly as the reference's Python-float expressions round them into fp32 ops.
     SplineConsts C;
@@ -132,7 +134,34 @@ extern "C" int nfx_spline_coupling(const float* packed, const float* in, float* 
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
     const int64_t nchunks = (B + 63) / 64;
-    const int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
-    k<<<grid, 256, lds, (hipStream_t)stream>>>(packed, in, out, log_det, B, d, C, accumulate, nchunks);
-    return check_launch("spline_coupling_kernel");
+    int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
+    if (grid > kMaxPartials) grid = kMaxPartials;
+    double* partials = reinterpret_cast<double*>(workspace);
+    k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, d, C, accumulate, nchunks, logp, partials,
+                                  gauss_const(d));
+    rc = check_launch("spline_coupling_kernel");
+    if (rc || !fused) return rc;
+    return gauss_finish(partials, grid, sums, B, stream);
+}
+
+extern "C" int nfx_spline_coupling(const float* packed, const float* in, float* out, float* log_det,
+                                   int64_t B, int d, int H, int K, float bound, float min_bin_width,
+                                   float min_bin_height, float min_derivative, int rescale,
+                                   float data_min, float data_max, int direction, int accumulate,
+                                   void* stream) {
+    return spline_launch(packed, in, out, log_det, B, d, H, K, bound, min_bin_width, min_bin_height,
+                         min_derivative, rescale, data_min, data_max, direction, accumulate, nullptr,
+                         nullptr, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int nfx_spline_coupling_logprob(const float* packed, const float* in, float* out,
+                                           float* log_det, float* logp, double* sums, void* workspace,
+                                           int64_t B, int d, int H, int K, float bound,
+                                           float min_bin_width, float min_bin_height,
+                                           float min_derivative, int rescale, float data_min,
+                                           float data_max, int accumulate, void* stream) {
+    if (!sums) return set_error(NFX_EINVAL, "spline_coupling_logprob: null sums");
+    return spline_launch(packed, in, out, log_det, B, d, H, K, bound, min_bin_width, min_bin_height,
+                         min_derivative, rescale, data_min, data_max, NFX_INVERSE, accumulate, logp,
+                         sums, workspace, (hipStream_t)stream);
 }

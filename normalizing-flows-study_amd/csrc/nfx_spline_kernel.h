@@ -178,11 +178,11 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
     if (nonfinite(lad)) lad = 0.f;    // :307
 }
 
-template <int HT, int K, int DIR>
+template <int HT, int K, int DIR, bool LOGP>
 __global__ __launch_bounds__(256) void spline_coupling_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, SplineConsts C, int accumulate,
-    int64_t nchunks) {
+    int64_t nchunks, float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
 #pragma clang fp contract(off)
     const SplineLayout L = spline_layout(HT, d);
     extern __shared__ f32x4 lds4[];
@@ -228,6 +228,7 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
     int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     Fetch cur;
     fetch(c, cur);
+    double lpacc = 0.0;
     for (; c < nchunks; c += nwaves) {
         const int64_t base = c * 64;
         const float* P = sm + opaque_zero();
@@ -343,21 +344,36 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
             ld = (t == 0) ? l : ld + l;
         }
         if (so < B) {
+            float m = 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if (j < d) out[so * d + j] = nonfinite(y[j]) ? 0.f : y[j];
+                const float v = nonfinite(y[j]) ? 0.f : y[j];
+                if (j < d) {
+                    out[so * d + j] = v;
+                    m = (j == 0) ? gauss_sq0(v) : gauss_sq(m, v);
+                }
             }
             if (nonfinite(ld)) ld = 0.f;
-            logdet[so] = accumulate ? cur.ldin + ld : ld;
+            const float ldt = accumulate ? cur.ldin + ld : ld;
+            logdet[so] = ldt;
+            if constexpr (LOGP) {
+                const float lp = gauss_lp(m, cgauss, ldt);
+                logp[so] = lp;
+                lpacc += (double)lp;
+            }
         }
         cur = nxt;
+    }
+    if constexpr (LOGP) {
+        const double t = block_sum_f64<256>(lpacc);
+        if (threadIdx.x == 0) partials[blockIdx.x] = t;
     }
 }
 
 typedef void (*spline_kernel_t)(const float*, const float*, float*, float*, int64_t, int,
-                                SplineConsts, int, int64_t);
+                                SplineConsts, int, int64_t, float*, double*, float);
 
 template <int HT>
-spline_kernel_t spline_pick_ht(int K, int dir);
+spline_kernel_t spline_pick_ht(int K, int dir, bool logp);
 
 }  // namespace nfx

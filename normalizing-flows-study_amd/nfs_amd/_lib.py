@@ -23,10 +23,10 @@ NFX_IAF_INVERSE = 3
 # Every symbol include/nfx.h declares (tests check the built library exports all of them).
 EXPORTED_SYMBOLS = (
     "nfx_abi_version", "nfx_last_error",
-    "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling",
-    "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling",
+    "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
+    "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
     "nfx_rqs_unit",
-    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine",
+    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob",
 )
 
@@ -66,14 +66,18 @@ _SIGNATURES = {
     "nfx_affine_packed_floats": (_sz, [_int, _int]),
     "nfx_affine_pack": (_int, [ctypes.POINTER(NfxMlpRaw), ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _vp, _vp]),
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
+    "nfx_affine_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_spline_packed_floats": (_sz, [_int, _int, _int]),
     "nfx_spline_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _int, _vp, _vp]),
     "nfx_spline_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _f,
                                    _int, _f, _f, _int, _int, _vp]),
+    "nfx_spline_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f,
+                                           _f, _f, _int, _f, _f, _int, _vp]),
     "nfx_rqs_unit": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int, _vp]),
     "nfx_made_packed_floats": (_sz, [_int, _int]),
     "nfx_made_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
     "nfx_made_affine": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
+    "nfx_made_affine_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_gauss_workspace_bytes": (_sz, [_i64]),
     "nfx_gauss_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _vp]),
 }

@@ -100,3 +100,11 @@ class CouplingLayer(HipFlow):
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), x.shape[0],
             self.data_dim, self._hidden(), int(direction), int(bool(accumulate)),
             _lib.stream_of(x)), "nfx_affine_coupling")
+
+    def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
+        packed = self._packed(x.device, self._build_pack)
+        _lib.check(_lib.lib().nfx_affine_coupling_logprob(
+            _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), _lib.ptr(logp),
+            _lib.ptr(sums), _lib.ptr(workspace), x.shape[0], self.data_dim, self._hidden(),
+            int(bool(accumulate)), _lib.stream_of(x)), "nfx_affine_coupling_logprob")
+        return True

@@ -143,6 +143,12 @@ class HipFlow(Flow):
         STATS["hip"] += 1
         self._hip_launch(x, out, log_det, direction, accumulate)
 
+    def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
+        """Inverse + fused Gaussian log_prob epilogue (last layer of a log_prob chain).
+        Returns False when this layer has no fused variant (the caller then runs
+        nfx_gauss_logprob after the plain inverse)."""
+        return False
+
     # -- packed-weight cache -------------------------------------------------------------
     def _state_key(self, device):
         key = [str(device)]

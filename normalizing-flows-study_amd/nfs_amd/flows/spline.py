@@ -211,6 +211,17 @@ class SplineCouplingLayer(HipFlow):
             rescale, lo, hi, int(direction), int(bool(accumulate)), _lib.stream_of(x)),
             "nfx_spline_coupling")
 
+    def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
+        packed = self._packed(x.device, self._build_pack)
+        rescale, lo, hi = self._rescale_scalars()
+        _lib.check(_lib.lib().nfx_spline_coupling_logprob(
+            _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), _lib.ptr(logp),
+            _lib.ptr(sums), _lib.ptr(workspace), x.shape[0], self.data_dim, self._hidden(),
+            self.num_bins, float(self.bound), float(self.min_bin_width),
+            float(self.min_bin_height), float(self.min_derivative), rescale, lo, hi,
+            int(bool(accumulate)), _lib.stream_of(x)), "nfx_spline_coupling_logprob")
+        return True
+
 
 def _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,
                     min_bin_height, min_derivative):

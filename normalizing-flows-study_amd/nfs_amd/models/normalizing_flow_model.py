@@ -101,14 +101,18 @@ class NormalizingFlowModel(nn.Module):
                 return False
         return True
 
-    def _hip_chain(self, x, direction):
+    def _hip_chain(self, x, direction, logprob=None):
+        """Run every layer's kernel back to back. With logprob=(logp, sums, workspace) (an
+        inverse chain), the last layer also writes the Gaussian log-density and float64 NLL
+        partials in its epilogue when it has a fused variant; `fused` in the return says
+        whether it did."""
         x = x.contiguous()
         B = x.shape[0]
         ld = torch.empty(B, device=x.device, dtype=torch.float32)
         bufs = [torch.empty_like(x), torch.empty_like(x)]
         n = len(self.flows)
         order = range(n) if direction > 0 else reversed(range(n))
-        cur, k, first = x, 0, True
+        cur, k, first, fused = x, 0, True, False
         for i in order:
             if direction < 0 and self.batch_norm_between_layers and i < n - 1:
                 bn = self.batch_norms[i]
@@ -125,7 +129,12 @@ class NormalizingFlowModel(nn.Module):
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            self.flows[i]._hip_launch_counted(cur, out, ld, direction, accumulate=not first)
+            if logprob is not None and i == 0 and self.flows[i]._hip_launch_logprob(
+                    cur, out, ld, *logprob, accumulate=not first):
+                STATS["hip"] += 1
+                fused = True
+            else:
+                self.flows[i]._hip_launch_counted(cur, out, ld, direction, accumulate=not first)
             if ev is not None:
                 e1.record()
                 ev.append((type(self.flows[i]).__name__, e0, e1))
@@ -135,6 +144,8 @@ class NormalizingFlowModel(nn.Module):
                 bn = self.batch_norms[i]
                 cur = self._apply_batch_norm(bn, cur).contiguous()
                 ld.add_(self._batch_norm_log_det_jacobian(bn, cur))
+        if logprob is not None:
+            return cur, ld, fused
         return cur, ld
 
     # -- log-density -------------------------------------------------------------------------
@@ -143,6 +154,15 @@ class NormalizingFlowModel(nn.Module):
 
         With return_sums=True also returns a float64 tensor [sum_i log p(x_i), B] on x's device
         (the partial a data-parallel NLL all-reduces)."""
+        if self._hip_chain_ok(x) and len(self.flows) > 0:
+            B = x.shape[0]
+            logp = torch.empty(B, device=x.device, dtype=torch.float32)
+            sums = torch.empty(2, device=x.device, dtype=torch.float64)
+            ws = gauss_workspace(B, x.device)
+            z, ld, fused = self._hip_chain(x, -1, logprob=(logp, sums, ws))
+            if not fused:
+                gauss_logprob(z, ld, logp, sums, ws)
+            return (logp, sums) if return_sums else logp
         z, ld = self.inverse(x)
         if z.device.type == "cuda" and z.dtype == torch.float32 and not self._needs_grad(x):
             logp, sums = gauss_logprob(z, ld)
@@ -160,15 +180,22 @@ class NormalizingFlowModel(nn.Module):
         return -(s[0] / s[1]).item()
 
 
-def gauss_logprob(z, ld, logp=None):
+def gauss_workspace(B, device):
+    """Scratch for the per-workgroup float64 partial sums (nfx_gauss_workspace_bytes)."""
+    return torch.empty(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
+
+
+def gauss_logprob(z, ld, logp=None, sums=None, ws=None):
     """Fused `MultivariateNormal(0,I).log_prob(z) + ld` and float64 [sum, count] (nfx_gauss_logprob)."""
     z = z.contiguous()
     B, d = z.shape
     if logp is None:
         logp = torch.empty(B, device=z.device, dtype=torch.float32)
-    sums = torch.empty(2, device=z.device, dtype=torch.float64)
+    if sums is None:
+        sums = torch.empty(2, device=z.device, dtype=torch.float64)
     L = _lib.lib()
-    ws = torch.empty(L.nfx_gauss_workspace_bytes(B), device=z.device, dtype=torch.uint8)
+    if ws is None:
+        ws = gauss_workspace(B, z.device)
     _lib.check(L.nfx_gauss_logprob(_lib.ptr(z), _lib.ptr(ld), _lib.ptr(logp), _lib.ptr(sums),
                                    _lib.ptr(ws), B, d, _lib.stream_of(z)), "nfx_gauss_logprob")
     STATS["hip"] += 1

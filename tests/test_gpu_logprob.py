@@ -1,0 +1,120 @@
+"""GPU: fused Gaussian log_prob epilogue in the last inverse layer (nfx_*_logprob).
+
+NormalizingFlowModel.log_prob runs the last layer of the inverse chain through its
+`*_logprob` entry point when it has one (affine coupling, spline coupling, MAF inverse d<=64)
+and through nfx_gauss_logprob otherwise. Both evaluate
+    logp = -0.5 * (fp32(d log 2pi) + sum_j z_j^2) + log_det
+with the same sequential fp32 sum, so the fused per-sample logp must be BIT-identical to
+inverse() + nfx_gauss_logprob; the float64 [sum, B] partials differ only by summation grouping
+(|rel| <= 1e-12). Parity of inverse()/log_prob against the reference itself is covered in
+test_gpu_affine.py / test_gpu_spline.py / test_gpu_made.py.
+"""
+import pytest
+import torch
+
+import nfs_amd
+from nfs_amd.models.normalizing_flow_model import gauss_logprob
+
+pytestmark = pytest.mark.gpu
+
+
+def _perturb(m, sigma, seed):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(sigma * torch.randn(p.shape, generator=g))
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.copy_(0.1 * torch.randn(mod.running_mean.shape, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(mod.running_var.shape, generator=g))
+    return m
+
+
+def _alt_mask(d, i):
+    m = torch.zeros(d)
+    m[(i % 2)::2] = 1
+    return m
+
+
+def _model(kind):
+    torch.manual_seed(7)
+    if kind == "realnvp":
+        return _perturb(nfs_amd.RealNVP(2, 4, 64), 0.1, 1), 2, True
+    if kind == "realnvp_bn_between":
+        return _perturb(nfs_amd.RealNVP(2, 4, 64, batch_norm_between_layers=True), 0.1, 2), 2, True
+    if kind == "affine_d5_h96":
+        fl = [nfs_amd.CouplingLayer(5, 96, _alt_mask(5, i)) for i in range(3)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.1, 3), 5, True
+    if kind == "spline_k5":
+        fl = [nfs_amd.SplineCouplingLayer(3, 64, _alt_mask(3, i), num_bins=5) for i in range(3)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.1, 4), 3, True
+    if kind == "maf63":
+        fl = [nfs_amd.MaskedAutoregressiveFlow(63, 64) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 5), 63, True
+    if kind == "maf80_chunked":
+        fl = [nfs_amd.MaskedAutoregressiveFlow(80, 64) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 6), 80, False
+    if kind == "iaf10_sequential":
+        fl = [nfs_amd.InverseAutoregressiveFlow(10, 32) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 7), 10, False
+    raise ValueError(kind)
+
+
+KINDS = ["realnvp", "realnvp_bn_between", "affine_d5_h96", "spline_k5", "maf63",
+         "maf80_chunked", "iaf10_sequential"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("B", [0, 1, 77, 4099, 300_001])
+def test_fused_logprob_matches_unfused(cuda_device, kind, B):
+    if kind == "iaf10_sequential" and B > 4099:
+        pytest.skip("sequential IAF inverse: small batches only")
+    m, d, fused_expected = _model(kind)
+    m = m.to(cuda_device).eval()
+    g = torch.Generator().manual_seed(100 + B)
+    x = (1.5 * torch.randn(B, d, generator=g)).to(cuda_device)
+    with torch.no_grad():
+        lp, sums = m.log_prob(x, return_sums=True)
+        z, ld = m.inverse(x)
+        lp_ref, sums_ref = gauss_logprob(z, ld)
+        torch.cuda.synchronize()
+    assert lp.shape == (B,) and sums.dtype == torch.float64
+    assert torch.equal(lp, lp_ref), (lp - lp_ref).abs().max()
+    s, sr = sums.cpu(), sums_ref.cpu()
+    assert s[1].item() == B
+    assert abs(s[0].item() - sr[0].item()) <= 1e-12 * max(1.0, abs(sr[0].item()))
+    if B:
+        assert abs(s[0].item() - lp.double().sum().item()) <= 1e-9 * max(1.0, abs(s[0].item()))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_fused_path_taken(cuda_device, kind):
+    """Layers with a fused variant skip the separate Gaussian pass (one launch fewer)."""
+    m, d, fused_expected = _model(kind)
+    m = m.to(cuda_device).eval()
+    x = torch.randn(1000, d, device=cuda_device)
+    with torch.no_grad():
+        logp, sums = torch.empty(1000, device=cuda_device), torch.empty(2, device=cuda_device, dtype=torch.float64)
+        ws = torch.empty(1 << 16, device=cuda_device, dtype=torch.uint8)
+        chain = getattr(m, "flow", m)  # RealNVP wraps a NormalizingFlowModel
+        _, _, fused = chain._hip_chain(x, -1, logprob=(logp, sums, ws))
+    assert fused == fused_expected
+
+
+def test_fused_logprob_nonfinite_rows(cuda_device):
+    """Non-finite inputs go through the reference guards first (z, log-det zeroed), so the
+    fused and unfused logp agree on them too."""
+    m, d, _ = _model("realnvp")
+    m = m.to(cuda_device).eval()
+    x = torch.randn(256, 2)
+    x[3, 0] = float("nan")
+    x[10, 1] = float("inf")
+    x[20] = 1e10
+    x = x.to(cuda_device)
+    with torch.no_grad():
+        lp = m.log_prob(x)
+        z, ld = m.inverse(x)
+        lp_ref, _ = gauss_logprob(z, ld)
+    assert torch.equal(lp.isnan(), lp_ref.isnan())
+    ok = ~lp.isnan()
+    assert torch.equal(lp[ok], lp_ref[ok])
