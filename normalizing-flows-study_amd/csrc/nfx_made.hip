@@ -84,6 +84,80 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     }
 }
 
+// Structural zeros of the packed parallel image + the overflow-safe input bound (one block).
+// The MADE masks zero whole 32 x 32 weight blocks (hidden units of low degree never see
+// high-degree inputs); the tile kernel stops each output tile's k-loop after its last nonzero
+// block when the tile's 32 input rows are all finite with max|x| <= tsafe. Every activation is
+// finite then, so a skipped block would only have added exact zeros (a + 0*b == a for finite b,
+// and relu maps -0 to +0): bit-identical to the dense product. Rows failing the test
+// (non-finite or huge inputs, where the reference's 0*inf = NaN contamination matters) run the
+// dense product. tsafe: with n_l = max row sum |W'_l| and c_l = max |b'_l|, every partial sum
+// of layer l is bounded by A_l = n_l*A_{l-1} + c_l (A_0 = max|x|); tsafe is the largest A_0
+// keeping every A_l <= 1e37 (0 when a weight is non-finite: dense path always).
+__global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, int H, float* packed) {
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
+    int* nk = reinterpret_cast<int*>(packed);
+    const int n1 = HT * 4 * L.NKC, n23 = HT * HT * 4, n4 = L.NJ * 2 * HT * 4;
+    for (int i = threadIdx.x; i < 3 * HT + L.NJ; i += 256) nk[L.nk1 + i] = 0;
+    __syncthreads();
+    for (int gi = threadIdx.x; gi < n1 + 2 * n23 + n4; gi += 256) {
+        int off, word, ext;  // 256-float weight group (32 rows x 8 k-steps) -> its k-block extent
+        if (gi < n1) {
+            const int ht = gi / (4 * L.NKC), g = gi % (4 * L.NKC);
+            off = L.w1 + gi * 256;
+            word = L.nk1 + ht;
+            ext = g / 4 + 1;
+        } else if (gi < n1 + 2 * n23) {
+            const int t = (gi - n1) % n23, layer = (gi - n1) / n23;
+            off = (layer == 0 ? L.w2 : L.w3) + t * 256;
+            word = (layer == 0 ? L.nk2 : L.nk3) + t / (HT * 4);
+            ext = (t % (HT * 4)) / 4 + 1;
+        } else {
+            const int t = gi - n1 - 2 * n23;
+            off = L.w4 + t * 256;
+            word = L.nk4 + t / (2 * HT * 4);
+            ext = (t % (HT * 4)) / 4 + 1;
+        }
+        bool nz = false;
+        for (int e = 0; e < 256; ++e) nz |= packed[off + e] != 0.f;  // NaN != 0: kept
+        if (nz) atomicMax(&nk[word], ext);
+    }
+    // overflow bound
+    __shared__ double red[256];
+    double alpha = 1.0, beta = 0.0, tsafe = 3.0e38;  // A_l = alpha*X + beta
+    for (int l = 0; l < 4; ++l) {
+        const int rows = l < 3 ? H : 2 * d, cols = l == 0 ? d : H;
+        double nmax = 0.0, cmax = 0.0;
+        for (int r = threadIdx.x; r < rows; r += 256) {
+            double sum = 0.0;
+            for (int c = 0; c < cols; ++c) sum += fabs((double)mlp_weight(net, l, cols, r, c));
+            nmax = sum > nmax || sum != sum ? sum : nmax;
+            const double b = fabs((double)mlp_bias(net, l, r));
+            cmax = b > cmax || b != b ? b : cmax;
+        }
+        for (int k = 0; k < 2; ++k) {
+            red[threadIdx.x] = k == 0 ? nmax : cmax;
+            __syncthreads();
+            for (int w = 128; w > 0; w >>= 1) {
+                if (threadIdx.x < w) {
+                    const double a = red[threadIdx.x], b = red[threadIdx.x + w];
+                    red[threadIdx.x] = (b > a || b != b) ? b : a;
+                }
+                __syncthreads();
+            }
+            if (k == 0) nmax = red[0]; else cmax = red[0];
+            __syncthreads();
+        }
+        alpha = nmax * alpha;
+        beta = nmax * beta + cmax;
+        const double lim = 1.0e37;
+        if (!(beta < lim) || !(alpha < 1e300)) tsafe = 0.0;
+        else if (alpha > 0.0) tsafe = fmin(tsafe, (lim - beta) / alpha);
+    }
+    if (threadIdx.x == 0) packed[L.tsafe] = (float)fmin(tsafe, 3.0e38);
+}
+
 template <int HT, int VAR>
 static made_seq_kernel_t seq_var() {
     return made_seq_kernel<HT, VAR>;
@@ -151,7 +225,10 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     int blocks = (total + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     made_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
-    return check_launch("made_pack_kernel");
+    int rc = check_launch("made_pack_kernel");
+    if (rc) return rc;
+    made_live_kernel<<<1, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
+    return check_launch("made_live_kernel");
 }
 
 static int made_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,

@@ -31,11 +31,18 @@ namespace nfx {
 //   s_w4 [2d][Hp], s_b4 [2d(up4)],
 //   s_deg [3][Hp]: unit degree (padded units 1e9) | degrees in completion order | unit index in
 //   completion order (units sorted by degree, stable)
+// then the structural-zero extents of the parallel image (int32, written by made_live_kernel):
+// per output tile, 1 + the index of its last k-block holding a nonzero weight (every later
+// k-block of that tile's rows is exactly zero under the MADE masks)
+//   nk1 [HT]  in 32-input chunks (layer 1)      nk2 [HT], nk3 [HT]  in 32-unit tiles
+//   nk4 [NJ]  in 32-unit tiles (mu and alpha rows of output tile pair j)
+//   tsafe (float): inputs with max|x| <= tsafe cannot overflow any layer (made_live_kernel)
 struct MadeLayout {
     int d, HT, Hp, NKC, NJ;
     int w1, b1, w2, b2, w3, b3, w4, b4;  // parallel image
     int par_total;                       // floats of the parallel image (LDS-resident prefix)
-    int s_w1t, s_b1, s_w2, s_b2, s_w3, s_b3, s_w4, s_b4, s_deg, total;
+    int s_w1t, s_b1, s_w2, s_b2, s_w3, s_b3, s_w4, s_b4, s_deg;
+    int nk1, nk2, nk3, nk4, tsafe, total;
 };
 
 __host__ __device__ constexpr int made_up4(int v) { return (v + 3) & ~3; }
@@ -66,7 +73,12 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     L.s_w4 = o; o += made_up4(2 * d * L.Hp);
     L.s_b4 = o; o += made_up4(2 * d);
     L.s_deg = o; o += 3 * L.Hp;
-    L.total = o;
+    L.nk1 = o; o += HT;
+    L.nk2 = o; o += HT;
+    L.nk3 = o; o += HT;
+    L.nk4 = o; o += L.NJ;
+    L.tsafe = o; o += 1;
+    L.total = made_up4(o);
     return L;
 }
 
@@ -455,6 +467,90 @@ __device__ __forceinline__ void made_hidden1(const float* __restrict__ W, int wo
     }
 }
 
+// One output tile of a hidden layer over its first NK input tiles only (bias, MFMA chain, relu)
+// — the structurally-zero trailing blocks of a MADE mask are skipped.
+template <int HT, int NK>
+__device__ __forceinline__ f32x16 hidden_tile(const float* __restrict__ W, int woff, int boff, int hto,
+                                              const f32x16 (&hin)[HT]) {
+    const int lane = lane_id(), h = lane >> 5;
+    f32x16 a = load_bias16(W + boff + hto * 32, h);
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(W + woff + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], hin[kt][4 * rq + rr], a);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+    return a;
+}
+
+// hidden_tile<HT, n> for a wave-uniform runtime n in [0, N].
+template <int HT, int N>
+__device__ __forceinline__ f32x16 hidden_tile_n(int n, const float* __restrict__ W, int woff, int boff,
+                                                int hto, const f32x16 (&hin)[HT]) {
+    if constexpr (N == 0) {
+        return hidden_tile<HT, 0>(W, woff, boff, hto, hin);
+    } else {
+        if (n >= N) return hidden_tile<HT, N>(W, woff, boff, hto, hin);
+        return hidden_tile_n<HT, N - 1>(n, W, woff, boff, hto, hin);
+    }
+}
+
+// Hidden layer with per-output-tile k extents nk (all HT: the interleaved dense form).
+template <int HT>
+__device__ __forceinline__ void made_hidden_nk(const float* __restrict__ W, int woff, int boff,
+                                               const f32x16 (&hin)[HT], f32x16 (&hout)[HT],
+                                               const int (&nk)[HT], bool full) {
+    if (full) {
+        made_hidden1<HT>(W, woff, boff, hin, hout);
+        return;
+    }
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) hout[hto] = hidden_tile_n<HT, HT>(nk[hto], W, woff, boff, hto, hin);
+}
+
+// Layer-4 tile pair j (mu rows, alpha rows) over its first NK hidden tiles.
+template <int HT, int NK>
+__device__ __forceinline__ void out_pair(const float* __restrict__ W, const MadeLayout& L, int j,
+                                         const f32x16 (&hin)[HT], f32x16& mu, f32x16& al) {
+    const int lane = lane_id(), h = lane >> 5;
+    mu = load_bias16(W + L.b4 + (j * 2 + 0) * 32, h);
+    al = load_bias16(W + L.b4 + (j * 2 + 1) * 32, h);
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const f32x4 wm = *reinterpret_cast<const f32x4*>(
+                W + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+            const f32x4 wa = *reinterpret_cast<const f32x4*>(
+                W + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                mu = mfma32(wm[rr], hin[kt][4 * rq + rr], mu);
+                al = mfma32(wa[rr], hin[kt][4 * rq + rr], al);
+            }
+        }
+    }
+}
+
+template <int HT, int N>
+__device__ __forceinline__ void out_pair_n(int n, const float* __restrict__ W, const MadeLayout& L, int j,
+                                           const f32x16 (&hin)[HT], f32x16& mu, f32x16& al) {
+    if constexpr (N == 0) {
+        out_pair<HT, 0>(W, L, j, hin, mu, al);
+    } else {
+        if (n >= N) {
+            out_pair<HT, N>(W, L, j, hin, mu, al);
+            return;
+        }
+        out_pair_n<HT, N - 1>(n, W, L, j, hin, mu, al);
+    }
+}
+
 template <int HT, bool WLDS, int VAR, bool LOGP>
 __global__ __launch_bounds__(512) void made_tile_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
@@ -478,6 +574,19 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
     // address arithmetic; the row offset r*d*4 rides in the scalar soffset.
     const int voff = lane < d ? lane * 4 : (1 << 30);
     const int rowb = d * 4;
+    // Structural-zero extents (wave-uniform scalar loads) and the overflow-safe input bound.
+    const int* nkp = reinterpret_cast<const int*>(packed);
+    int nk1[HT], nk2[HT], nk3[HT];
+    bool full2 = true, full3 = true;
+#pragma unroll
+    for (int i = 0; i < HT; ++i) {
+        nk1[i] = nkp[L.nk1 + i];
+        nk2[i] = nkp[L.nk2 + i];
+        nk3[i] = nkp[L.nk3 + i];
+        full2 = full2 && nk2[i] >= HT;
+        full3 = full3 && nk3[i] >= HT;
+    }
+    const float tsafe = packed[L.tsafe];
 
     int64_t t = (int64_t)blockIdx.x * 8 + wave;
     double lpacc = 0.0;
@@ -496,36 +605,38 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
         const int64_t base = t * 32;
         const int rows = (int)(B - base < 32 ? B - base : 32);
         const float* W = (WLDS ? lds : packed) + opaque_zero();
+        // Skip the structurally-zero blocks only when every input of the tile is finite and
+        // within the overflow-safe bound (bit-identical then); the dense product otherwise.
+        float xmax = 0.f;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) xt[r * S + lane] = pf[r];
+        for (int r = 0; r < 32; ++r) {
+            xt[r * S + lane] = pf[r];
+            xmax = tmax(xmax, fabsf(pf[r]));  // NaN-propagating: a NaN fails the test
+        }
+        const bool dense = __builtin_amdgcn_ballot_w64(!(xmax <= tsafe)) != 0;
         wave_lds_sync();
 
         f32x16 h1[HT];
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(W + L.b1 + ht * 32, h);
-        for (int kc = 0; kc < L.NKC; ++kc) {
+        for (int ht = 0; ht < HT; ++ht) {
+            f32x16 a = load_bias16(W + L.b1 + ht * 32, h);
+            const int nkc = dense ? L.NKC : nk1[ht];
+            for (int kc = 0; kc < nkc; ++kc) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 w[HT];
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 w =
+                        *reinterpret_cast<const f32x4*>(W + L.w1 + ((ht * 4 * L.NKC + kc * 4 + g) * 64 + lane) * 4);
 #pragma unroll
-                for (int ht = 0; ht < HT; ++ht)
-                    w[ht] = *reinterpret_cast<const f32x4*>(W + L.w1 + ((ht * 4 * L.NKC + kc * 4 + g) * 64 + lane) * 4);
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const float b = xt[col * S + 32 * kc + 8 * g + 2 * rr + h];
-#pragma unroll
-                    for (int ht = 0; ht < HT; ++ht) h1[ht] = mfma32(w[ht][rr], b, h1[ht]);
+                    for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], xt[col * S + 32 * kc + 8 * g + 2 * rr + h], a);
                 }
             }
-        }
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
+            for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+            h1[ht] = a;
         }
         f32x16 h2[HT];
-        made_hidden1<HT>(W, L.w2, L.b2, h1, h2);
-        made_hidden1<HT>(W, L.w3, L.b3, h2, h1);  // h3 -> h1
+        made_hidden_nk<HT>(W, L.w2, L.b2, h1, h2, nk2, dense || full2);
+        made_hidden_nk<HT>(W, L.w3, L.b3, h2, h1, nk3, dense || full3);  // h3 -> h1
 
         // prefetch the next tile's rows (and incoming log-det) while layer 4 runs
         const float ldin = ldpf;
@@ -544,23 +655,8 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
         // their alpha is 0 (adds nothing to the log-det) and their z lands in the tile padding.
         float acc = 0.f;
         for (int j = 0; j < L.NJ; ++j) {
-            f32x16 mu = load_bias16(W + L.b4 + (j * 2 + 0) * 32, h);
-            f32x16 al = load_bias16(W + L.b4 + (j * 2 + 1) * 32, h);
-#pragma unroll
-            for (int kt = 0; kt < HT; ++kt) {
-#pragma unroll
-                for (int rq = 0; rq < 4; ++rq) {
-                    const f32x4 wm = *reinterpret_cast<const f32x4*>(
-                        W + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
-                    const f32x4 wa = *reinterpret_cast<const f32x4*>(
-                        W + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        mu = mfma32(wm[rr], h1[kt][4 * rq + rr], mu);
-                        al = mfma32(wa[rr], h1[kt][4 * rq + rr], al);
-                    }
-                }
-            }
+            f32x16 mu, al;
+            out_pair_n<HT, HT>(dense ? HT : nkp[L.nk4 + j], W, L, j, h1, mu, al);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 float* p = xt + col * S + 32 * j + crow(r, h);

@@ -171,3 +171,51 @@ def test_full_scale_nll_cfg4(cuda_device):
     m, _ = maf63(cuda_device)
     nll = m.nll(x.to(cuda_device))
     assert abs(nll - meta["nll_f64"]) <= 1e-6 * abs(meta["nll_f64"]), (nll, meta["nll_f64"])
+
+
+def _made_tables(packed, d, H):
+    """nk extents + tsafe of the packed MADE image (mirror of MadeLayout, nfx_made_kernel.h)."""
+    up4 = lambda v: (v + 3) & ~3
+    HT = (H + 31) // 32
+    Hp, NKC = 32 * HT, (d + 31) // 32
+    NJ = NKC
+    o = HT * 4 * NKC * 256 + HT * 32 + 2 * (HT * HT * 1024 + HT * 32) + NJ * 2 * HT * 1024 + NJ * 64
+    o += up4(d * Hp) + Hp + 2 * (Hp * Hp + Hp) + up4(2 * d * Hp) + up4(2 * d) + 3 * Hp
+    ints = packed.view(torch.int32).cpu()
+    nk = [ints[o + i * HT:o + (i + 1) * HT].tolist() for i in range(3)] + [ints[o + 3 * HT:o + 3 * HT + NJ].tolist()]
+    return nk, float(packed[o + 3 * HT + NJ].cpu())
+
+
+def test_made_structural_zero_tables(cuda_device):
+    """d=63, H=64 (cfg4): every 32x32 block above the MADE block diagonal is exactly zero."""
+    f = nfs_amd.MaskedAutoregressiveFlow(63, 64).to(cuda_device).eval()
+    with torch.no_grad():
+        f.inverse(torch.randn(64, 63, device=cuda_device))
+    packed = f._nfx_pack_cache[1]
+    nk, tsafe = _made_tables(packed, 63, 64)
+    assert nk == [[1, 2], [1, 2], [1, 2], [1, 2]], nk
+    assert 1e30 < tsafe < 1e37
+
+
+@pytest.mark.parametrize("d,H", [(5, 16), (33, 32), (63, 64), (64, 96), (40, 128), (2, 64)])
+def test_made_block_skip_bit_identical(cuda_device, d, H):
+    """Tiles whose inputs pass the finite/bound test skip structurally-zero blocks; a tile with
+    one huge row runs the dense product. The other rows of that tile must come out bit-identical
+    to the same rows computed on the skipping path."""
+    torch.manual_seed(d * 1000 + H)
+    for cls in (nfs_amd.MaskedAutoregressiveFlow, nfs_amd.InverseAutoregressiveFlow):
+        f = cls(d, H)
+        with torch.no_grad():
+            for p in f.parameters():
+                p.add_(0.1 * torch.randn_like(p))
+        f = f.to(cuda_device).eval()
+        x = torch.randn(96, d, device=cuda_device)
+        xd = x.clone()
+        xd[37, 0] = 1e38  # tile 1 (rows 32..63) -> dense path
+        fwd = f.forward if cls is nfs_amd.InverseAutoregressiveFlow else f.inverse
+        with torch.no_grad():
+            y, ld = fwd(x)
+            yd, ldd = fwd(xd)
+        keep = torch.ones(96, dtype=torch.bool, device=cuda_device)
+        keep[37] = False
+        assert torch.equal(y[keep], yd[keep]) and torch.equal(ld[keep], ldd[keep])
