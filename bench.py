@@ -1,6 +1,6 @@
 """Benchmark: log_prob throughput of the gfx950 flow-transform hot path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5f|cfg5i]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 One step = one log_prob pass over the per-GPU batch: every flow layer's fused kernel
@@ -8,6 +8,8 @@ One step = one log_prob pass over the per-GPU batch: every flow layer's fused ke
 with the float64 NLL partial sum, and (N > 1) ONE RCCL all-reduce of the 16-byte partial
 [sum log p, count] — the whole data-parallel exchange of the path.
 Weak scaling: each rank owns a fixed 1M-sample shard (configs[1] of BASELINE.json at N=1).
+cfg5f / cfg5i (BASELINE configs[4], IAF(784, 64)): one step = the sampling pass forward(z)
+(parallel MADE kernel) / the density pass log_prob(x) through the sequential IAF inverse.
 
 Rank 0 prints ONE JSON line with the throughput, the roofline of the dominant kernel (HIP
 events on the launch stream, over the timed steps) and, at N=1, the oracle CPU baseline timed on
@@ -82,32 +84,54 @@ def build(config):
         f = 2 * (d * H + 2 * H * H + 2 * d * H)
         import oracle
         return m, d, f, oracle.maf_spec(5), "cfg4 5x MaskedAutoregressiveFlow(63, 64) log_prob, eval"
+    if config in ("cfg5f", "cfg5i"):
+        torch.manual_seed(40)
+        m = nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)])
+        perturb(m, 0.01, 41)
+        d, H = 784, 64
+        # one MADE evaluation per sample in both directions: the sequential inverse kernel
+        # computes every hidden unit once, when the input of its degree is known
+        f = 2 * (d * H + 2 * H * H + 2 * d * H)
+        import oracle
+        spec = [("iaf", "flows.0.", {})]
+        if config == "cfg5f":
+            return m, d, f, spec, "cfg5f IAF(784, 64) forward (sampling, parallel), eval"
+        return m, d, f, spec, "cfg5i IAF(784, 64) log_prob (sequential inverse), eval"
     raise ValueError(config)
 
+# per-GPU batch of each config (weak scaling unit)
+DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 500_000, "cfg5f": 524_288, "cfg5i": 8_192}
 
-def cpu_baseline(model, spec, x_gpu, budget_s=12.0):
+
+def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=262144):
     """The oracle (op-for-op CPU restatement of the reference) timed on this host."""
     import oracle
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    n = min(x_gpu.shape[0], 262144)
+    n = min(x_gpu.shape[0], max_rows)
     x = x_gpu[:n].float().cpu()
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     times = []
+
+    def run():
+        if forward:
+            return oracle.flow_model(sd, spec, x, 1)
+        z, ld = oracle.flow_model(sd, spec, x, -1)
+        return z, oracle.gauss_log_prob(z, ld)
+
     with torch.no_grad():
-        z, ld = oracle.flow_model(sd, spec, x, -1)  # warm-up
-        lp = oracle.gauss_log_prob(z, ld)
+        _, lp = run()  # warm-up
         t_end = time.perf_counter() + budget_s
         while len(times) < 5 and (time.perf_counter() < t_end or len(times) < 2):
             t0 = time.perf_counter()
-            z, ld = oracle.flow_model(sd, spec, x, -1)
-            oracle.gauss_log_prob(z, ld)
+            run()
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
+    what = "forward (sampling)" if forward else "log_prob"
     return {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} rows of the same seeded batch, log_prob via oracle/flows_ref.py "
+            "sample": f"{n} rows of the same seeded batch, {what} via oracle/flows_ref.py "
                       f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}, \
-        oracle.nll_f64(lp), x
+        (None if forward else oracle.nll_f64(lp)), x
 
 
 def main():
@@ -115,8 +139,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4"])
-    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (default 1M; 500k for cfg4)")
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5f", "cfg5i"])
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: split ONE global batch (default 1M) over the ranks")
@@ -134,7 +159,8 @@ def main():
     model = model.to(dev).eval()
     from nfs_amd.distributed import broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
-    B_unit = a.batch or (500_000 if a.config == "cfg4" else 1_000_000)
+    B_unit = a.batch or DEFAULT_BATCH[a.config]
+    sampling = a.config == "cfg5f"
     if a.strong:
         lo, hi = shard_range(B_unit, rank, world)
         B, B_global = hi - lo, B_unit
@@ -145,6 +171,8 @@ def main():
     flow = model.flow if hasattr(model, "flow") else model
 
     def step():
+        if sampling:  # sampling pass: x = forward(z), no exchange
+            return flow.forward(x)
         logp, sums = flow.log_prob(x, return_sums=True)
         if world > 1:
             dist.all_reduce(sums)  # RCCL over xGMI: 16 bytes
@@ -185,7 +213,7 @@ def main():
     kname = events[0][0] if events else "?"
     mean_ms = sum(durs) / max(1, len(durs))
     achieved = f_layer * B / (mean_ms * 1e-3) / 1e12
-    nll = -float(sums[0] / sums[1])
+    nll = None if sampling else -float(sums[0] / sums[1])
 
     result = None
     if rank == 0:
@@ -211,16 +239,19 @@ def main():
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B_global,
                        "parallelism": f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"},
             "nll_f64": nll,
-            "roofline": {"bound": "mfma", "kernel": kname, "achieved": achieved,
+            "roofline": {"bound": "mfma", "pipe": "valu" if a.config == "cfg5i" else "mfma",
+                         "kernel": kname, "achieved": achieved,
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
                          "traffic": traffic, "flop_per_sample_per_launch": f_layer,
                          "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs)},
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu:
-            cb, cpu_nll, xs = cpu_baseline(model, spec, x)
-            gpu_nll = flow.nll(xs.to(dev))
-            cb["nll_abs_diff_vs_gpu"] = abs(cpu_nll - gpu_nll)
+            rows = {"cfg5f": 16384, "cfg5i": 256}.get(a.config, 262144)
+            cb, cpu_nll, xs = cpu_baseline(model, spec, x, forward=sampling, max_rows=rows)
+            if not sampling:
+                gpu_nll = flow.nll(xs.to(dev))
+                cb["nll_abs_diff_vs_gpu"] = abs(cpu_nll - gpu_nll)
             result["cpu_baseline"] = cb
         print(json.dumps(result), flush=True)
     if world > 1:
