@@ -1,6 +1,7 @@
 // MADE affine flows: weight pack, sequential-kernel instantiations and the C-ABI.
 // Kernels: nfx_made_kernel.h (parallel instantiations in nfx_made_par.hip).
 #include "nfx_made_kernel.h"
+#include "nfx_made_wide_kernel.h"
 #include "nfx_pack.h"
 
 namespace nfx {
@@ -239,15 +240,32 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     if (d > 4096 || H > 128) return set_error(NFX_EUNSUPPORTED, "made_affine: d=%d H=%d outside d<=4096, H<=128", d, H);
     if (variant < NFX_MAF_INVERSE || variant > NFX_IAF_INVERSE)
         return set_error(NFX_EINVAL, "made_affine: unknown variant %d", variant);
-    if (fused && (variant != NFX_MAF_INVERSE || d > kTileMaxD))
-        return set_error(NFX_EUNSUPPORTED, "made_affine_logprob: fused log_prob needs MAF inverse with d <= %d", kTileMaxD);
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
+    const bool parallel = variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD;
+    const size_t wide_lds_bytes = (size_t)wide_lds(L, HT).total * sizeof(float);
+    const bool wide = parallel && d > kTileMaxD && HT <= 2 && wide_lds_bytes <= kLdsBytes;
+    if (fused && (variant != NFX_MAF_INVERSE || (d > kTileMaxD && !wide)))
+        return set_error(NFX_EUNSUPPORTED,
+                         "made_affine_logprob: fused log_prob needs MAF inverse with d <= %d or H <= 64", kTileMaxD);
     if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "made_affine_logprob: null logp/workspace");
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, s) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "made_affine: null pointer");
     if (in == out) return set_error(NFX_EINVAL, "made_affine: in and out must not alias");
-    const int HT = (H + 31) / 32;
-    const MadeLayout L = made_layout(d, HT);
     double* partials = reinterpret_cast<double*>(workspace);
+    if (wide) {
+        made_par_kernel_t k = HT == 1 ? made_wide_pick_ht<1>(variant, fused) : made_wide_pick_ht<2>(variant, fused);
+        int rc = prepare_lds((const void*)k, wide_lds_bytes);
+        if (rc) return rc;
+        const int64_t nchunks = (B + 63) / 64;
+        int grid = resident_grid((const void*)k, 512, wide_lds_bytes, (nchunks + kWideWaves - 1) / kWideWaves);
+        if (grid > kMaxPartials) grid = kMaxPartials;
+        k<<<grid, 512, wide_lds_bytes, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, logp, partials,
+                                            gauss_const(d));
+        rc = check_launch("made_wide_kernel");
+        if (rc || !fused) return rc;
+        return gauss_finish(partials, grid, sums, B, s);
+    }
     if ((variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) && d <= kTileMaxD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
         const size_t tiles8 = 8 * 32 * (size_t)kTileStride * sizeof(float);

@@ -1,6 +1,7 @@
 // Instantiations of the parallel MADE-affine kernel (MAF.inverse / IAF.forward):
 // hidden tiles HT = 1..4, weights LDS-resident or L2-streamed.
 #include "nfx_made_kernel.h"
+#include "nfx_made_wide_kernel.h"
 
 namespace nfx {
 
@@ -33,5 +34,13 @@ template made_par_kernel_t made_tile_pick_ht<1>(bool, int, bool);
 template made_par_kernel_t made_tile_pick_ht<2>(bool, int, bool);
 template made_par_kernel_t made_tile_pick_ht<3>(bool, int, bool);
 template made_par_kernel_t made_tile_pick_ht<4>(bool, int, bool);
+
+template <int HT>
+made_par_kernel_t made_wide_pick_ht(int variant, bool logp) {
+    if (variant != NFX_MAF_INVERSE) return made_wide_kernel<HT, NFX_IAF_FORWARD, false>;
+    return logp ? made_wide_kernel<HT, NFX_MAF_INVERSE, true> : made_wide_kernel<HT, NFX_MAF_INVERSE, false>;
+}
+template made_par_kernel_t made_wide_pick_ht<1>(int, bool);
+template made_par_kernel_t made_wide_pick_ht<2>(int, bool);
 
 }  // namespace nfx

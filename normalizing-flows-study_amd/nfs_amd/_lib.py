@@ -13,6 +13,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NFX_LIB", os.path.join(_HERE, "libnfx.so"))
 
 NFX_OK = 0
+NFX_EINVAL = -1
+NFX_EUNSUPPORTED = -2
+NFX_ELAUNCH = -3
 NFX_FORWARD = 1
 NFX_INVERSE = -1
 NFX_MAF_INVERSE = 0

@@ -25,7 +25,6 @@ from .flow import HipFlow
 
 MAX_H = 128
 MAX_D = 4096
-FUSED_LOGPROB_MAX_D = 64  # made_tile_kernel range (csrc/nfx_made.hip kTileMaxD)
 
 
 def made_degrees(input_dim, hidden_dim):
@@ -154,14 +153,16 @@ class _MadeAffineFlow(HipFlow):
 
     def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
         variant = self._variant(-1)
-        if variant != _lib.NFX_MAF_INVERSE or self.dim > FUSED_LOGPROB_MAX_D:
-            return False  # sequential IAF inverse / chunked MADE kernel: separate Gaussian pass
+        if variant != _lib.NFX_MAF_INVERSE:
+            return False  # sequential IAF inverse: separate Gaussian pass
         packed = self._packed(x.device, self._build_pack)
-        _lib.check(_lib.lib().nfx_made_affine_logprob(
+        rc = _lib.lib().nfx_made_affine_logprob(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), _lib.ptr(logp),
             _lib.ptr(sums), _lib.ptr(workspace), x.shape[0], self.dim,
-            self.conditioner.hidden_dim, variant, int(bool(accumulate)), _lib.stream_of(x)),
-            "nfx_made_affine_logprob")
+            self.conditioner.hidden_dim, variant, int(bool(accumulate)), _lib.stream_of(x))
+        if rc == _lib.NFX_EUNSUPPORTED:
+            return False  # no fused kernel for this (d, H): nothing was launched
+        _lib.check(rc, "nfx_made_affine_logprob")
         return True
 
 

@@ -1,7 +1,8 @@
 """GPU: fused Gaussian log_prob epilogue in the last inverse layer (nfx_*_logprob).
 
 NormalizingFlowModel.log_prob runs the last layer of the inverse chain through its
-`*_logprob` entry point when it has one (affine coupling, spline coupling, MAF inverse d<=64)
+`*_logprob` entry point when it has one (affine coupling, spline coupling, MAF inverse with
+d <= 64 or H <= 64)
 and through nfx_gauss_logprob otherwise. Both evaluate
     logp = -0.5 * (fp32(d log 2pi) + sum_j z_j^2) + log_det
 with the same sequential fp32 sum, so the fused per-sample logp must be BIT-identical to
@@ -51,9 +52,12 @@ def _model(kind):
     if kind == "maf63":
         fl = [nfs_amd.MaskedAutoregressiveFlow(63, 64) for _ in range(2)]
         return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 5), 63, True
-    if kind == "maf80_chunked":
+    if kind == "maf80_wide":
         fl = [nfs_amd.MaskedAutoregressiveFlow(80, 64) for _ in range(2)]
-        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 6), 80, False
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 6), 80, True
+    if kind == "maf100_h128_chunked":
+        fl = [nfs_amd.MaskedAutoregressiveFlow(100, 128) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 8), 100, False
     if kind == "iaf10_sequential":
         fl = [nfs_amd.InverseAutoregressiveFlow(10, 32) for _ in range(2)]
         return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 7), 10, False
@@ -61,7 +65,7 @@ def _model(kind):
 
 
 KINDS = ["realnvp", "realnvp_bn_between", "affine_d5_h96", "spline_k5", "maf63",
-         "maf80_chunked", "iaf10_sequential"]
+         "maf80_wide", "maf100_h128_chunked", "iaf10_sequential"]
 
 
 @pytest.mark.parametrize("kind", KINDS)

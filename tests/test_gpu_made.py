@@ -90,7 +90,8 @@ def test_small_made_flows(cuda_device, name, kind):
     assert_ld(li.cpu(), g[name + ".inv_ld"])
 
 
-@pytest.mark.parametrize("d,H,B", [(5, 16, 1), (33, 32, 65), (63, 96, 130), (100, 128, 257), (7, 64, 1000)])
+@pytest.mark.parametrize("d,H,B", [(5, 16, 1), (33, 32, 65), (63, 96, 130), (100, 128, 257), (7, 64, 1000),
+                                   (65, 64, 129), (100, 32, 700), (200, 64, 1500), (784, 64, 77)])
 def test_made_shapes_vs_oracle(cuda_device, d, H, B):
     torch.manual_seed(d * 31 + H)
     for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
@@ -109,11 +110,11 @@ def test_made_shapes_vs_oracle(cuda_device, d, H, B):
             assert_ld(lg.cpu(), lr, 5e-4)
 
 
-def test_made_nonfinite_inputs(cuda_device):
+@pytest.mark.parametrize("d,H", [(6, 16), (100, 64)])
+def test_made_nonfinite_inputs(cuda_device, d, H):
     """inf/NaN rows: parallel directions propagate 0*inf = NaN through the dense masked weights;
     sequential directions reproduce the reference's contamination of every later step."""
     torch.manual_seed(3)
-    d, H = 6, 16
     for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
         f = cls(d, H)
         with torch.no_grad():
@@ -124,7 +125,7 @@ def test_made_nonfinite_inputs(cuda_device):
         x = torch.randn(8, d)
         x[0, 0] = float("inf")
         x[1, 3] = float("nan")
-        x[2, 5] = -float("inf")
+        x[2, d - 1] = -float("inf")
         x[3, :] = 1e30
         for direction in (1, -1):
             with torch.no_grad():
@@ -197,11 +198,13 @@ def test_made_structural_zero_tables(cuda_device):
     assert 1e30 < tsafe < 1e37
 
 
-@pytest.mark.parametrize("d,H", [(5, 16), (33, 32), (63, 64), (64, 96), (40, 128), (2, 64)])
+@pytest.mark.parametrize("d,H", [(5, 16), (33, 32), (63, 64), (64, 96), (40, 128), (2, 64),
+                                 (100, 32), (200, 64), (784, 64)])
 def test_made_block_skip_bit_identical(cuda_device, d, H):
     """Tiles whose inputs pass the finite/bound test skip structurally-zero blocks; a tile with
     one huge row runs the dense product. The other rows of that tile must come out bit-identical
-    to the same rows computed on the skipping path."""
+    to the same rows computed on the skipping path (32-row tiles for d <= 64, 64-row chunks of
+    the wide kernel above)."""
     torch.manual_seed(d * 1000 + H)
     for cls in (nfs_amd.MaskedAutoregressiveFlow, nfs_amd.InverseAutoregressiveFlow):
         f = cls(d, H)
