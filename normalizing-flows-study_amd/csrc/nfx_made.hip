@@ -2,6 +2,7 @@
 // Kernels: nfx_made_kernel.h (parallel instantiations in nfx_made_par.hip).
 #include "nfx_made_kernel.h"
 #include "nfx_made_wide_kernel.h"
+#include "nfx_made_seqg_kernel.h"
 #include "nfx_pack.h"
 
 namespace nfx {
@@ -159,6 +160,13 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
     if (threadIdx.x == 0) packed[L.tsafe] = (float)fmin(tsafe, 3.0e38);
 }
 
+template <int HT>
+made_seq_kernel_t made_seqg_pick_ht(int variant) {
+    return variant == NFX_MAF_FORWARD ? made_seqg_kernel<HT, NFX_MAF_FORWARD> : made_seqg_kernel<HT, NFX_IAF_INVERSE>;
+}
+template made_seq_kernel_t made_seqg_pick_ht<1>(int);
+template made_seq_kernel_t made_seqg_pick_ht<2>(int);
+
 template <int HT, int VAR>
 static made_seq_kernel_t seq_var() {
     return made_seq_kernel<HT, VAR>;
@@ -299,6 +307,15 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         const int grid = resident_grid((const void*)k, threads, lds, (nchunks + nw - 1) / nw);
         k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, nullptr, nullptr, 0.f);
         return check_launch("made_parallel_kernel");
+    }
+    if (HT <= 2) {
+        made_seq_kernel_t k = HT == 1 ? made_seqg_pick_ht<1>(variant) : made_seqg_pick_ht<2>(variant);
+        const size_t lds = (size_t)seqg_lds(L.Hp).total * sizeof(float);
+        int rc = prepare_lds((const void*)k, lds);
+        if (rc) return rc;
+        const int grid = resident_grid((const void*)k, 512, lds, (B + 4 * kSeqgWaves - 1) / (4 * kSeqgWaves));
+        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate);
+        return check_launch("made_seqg_kernel");
     }
     made_seq_kernel_t k = pick_seq(HT, variant);
     if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no sequential kernel for H=%d", H);
