@@ -127,36 +127,8 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
     }
     // overflow bound
     __shared__ double red[256];
-    double alpha = 1.0, beta = 0.0, tsafe = 3.0e38;  // A_l = alpha*X + beta
-    for (int l = 0; l < 4; ++l) {
-        const int rows = l < 3 ? H : 2 * d, cols = l == 0 ? d : H;
-        double nmax = 0.0, cmax = 0.0;
-        for (int r = threadIdx.x; r < rows; r += 256) {
-            double sum = 0.0;
-            for (int c = 0; c < cols; ++c) sum += fabs((double)mlp_weight(net, l, cols, r, c));
-            nmax = sum > nmax || sum != sum ? sum : nmax;
-            const double b = fabs((double)mlp_bias(net, l, r));
-            cmax = b > cmax || b != b ? b : cmax;
-        }
-        for (int k = 0; k < 2; ++k) {
-            red[threadIdx.x] = k == 0 ? nmax : cmax;
-            __syncthreads();
-            for (int w = 128; w > 0; w >>= 1) {
-                if (threadIdx.x < w) {
-                    const double a = red[threadIdx.x], b = red[threadIdx.x + w];
-                    red[threadIdx.x] = (b > a || b != b) ? b : a;
-                }
-                __syncthreads();
-            }
-            if (k == 0) nmax = red[0]; else cmax = red[0];
-            __syncthreads();
-        }
-        alpha = nmax * alpha;
-        beta = nmax * beta + cmax;
-        const double lim = 1.0e37;
-        if (!(beta < lim) || !(alpha < 1e300)) tsafe = 0.0;
-        else if (alpha > 0.0) tsafe = fmin(tsafe, (lim - beta) / alpha);
-    }
+    const int rows[4] = {H, H, H, 2 * d}, cols[4] = {d, H, H, H};
+    const double tsafe = block_mlp_tsafe(net, 4, rows, cols, 1.0e37, red);
     if (threadIdx.x == 0) packed[L.tsafe] = (float)fmin(tsafe, 3.0e38);
 }
 

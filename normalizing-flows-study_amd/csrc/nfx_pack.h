@@ -26,4 +26,42 @@ __device__ inline float mlp_bias(const NfxMlpRaw& net, int layer, int row) {
     return b;
 }
 
+// Overflow-safe input bound of an MLP, computed by one 256-thread block (every thread gets the
+// result). With n_l = max row sum |W'_l| and c_l = max |b'_l|, every partial sum of layer l is
+// bounded by A_l = n_l*A_{l-1} + c_l (A_0 = max|x|): returns the largest A_0 keeping every
+// A_l <= lim (0 when a weight or bias is non-finite). ReLU/clamps only shrink magnitudes, so
+// inputs within the bound produce finite activations everywhere.
+__device__ inline double block_mlp_tsafe(const NfxMlpRaw& net, int nl, const int* rows, const int* cols,
+                                         double lim, double* red /* [256] shared */) {
+    double alpha = 1.0, beta = 0.0, tsafe = 3.0e38;
+    for (int l = 0; l < nl; ++l) {
+        double nmax = 0.0, cmax = 0.0;
+        for (int r = threadIdx.x; r < rows[l]; r += 256) {
+            double sum = 0.0;
+            for (int c = 0; c < cols[l]; ++c) sum += fabs((double)mlp_weight(net, l, cols[l], r, c));
+            nmax = (sum > nmax || sum != sum) ? sum : nmax;
+            const double b = fabs((double)mlp_bias(net, l, r));
+            cmax = (b > cmax || b != b) ? b : cmax;
+        }
+        for (int k = 0; k < 2; ++k) {
+            red[threadIdx.x] = k == 0 ? nmax : cmax;
+            __syncthreads();
+            for (int w = 128; w > 0; w >>= 1) {
+                if (threadIdx.x < w) {
+                    const double a = red[threadIdx.x], b = red[threadIdx.x + w];
+                    red[threadIdx.x] = (b > a || b != b) ? b : a;
+                }
+                __syncthreads();
+            }
+            if (k == 0) nmax = red[0]; else cmax = red[0];
+            __syncthreads();
+        }
+        alpha = nmax * alpha;
+        beta = nmax * beta + cmax;
+        if (!(beta < lim) || !(alpha < 1e300)) tsafe = 0.0;
+        else if (alpha > 0.0) tsafe = fmin(tsafe, (lim - beta) / alpha);
+    }
+    return tsafe;
+}
+
 }  // namespace nfx
