@@ -18,7 +18,7 @@ import statistics
 import sys
 
 HOT = ("affine_coupling_kernel", "spline_coupling_kernel", "made_parallel_kernel", "made_tile_kernel", "made_seq_kernel",
-       "gauss_logprob_kernel", "rqs_unit_kernel")
+       "made_wide_kernel", "made_seqg_kernel", "gauss_logprob_kernel", "rqs_unit_kernel")
 
 
 def rows(path_glob):
@@ -92,7 +92,8 @@ def main():
                 json.dump(res, f, indent=1)
             for p in glob.glob(os.path.join(d, cfg, "trace", "*", "*_kernel_stats.csv")):
                 shutil.copy(p, f"{dest}_{cfg}_kernel_stats.csv")
-            dom = {"affine_coupling_kernel": "cfg2", "spline_coupling_kernel": "cfg3", "made_tile_kernel": "cfg4"}
+            dom = {"affine_coupling_kernel": "cfg2", "spline_coupling_kernel": "cfg3", "made_tile_kernel": "cfg4",
+                   "made_wide_kernel": "cfg5f", "made_seqg_kernel": "cfg5i"}
             for tag, c in dom.items():
                 # every template instance of the dominant kernel (the last layer runs the fused
                 # log_prob variant), weighted by dispatch count = the per-launch mean bench.py times
