@@ -217,10 +217,10 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
                 const float xa = cur.xr[j] * m;
                 float t;
                 if constexpr (DIR < 0) {
-                    t = (cur.xr[j] - bv[j]) * expf(-sv[j]);
+                    t = (cur.xr[j] - bv[j]) * exp_fast(-sv[j]);
                     ld = ld + om * (-sv[j]);
                 } else {
-                    t = cur.xr[j] * expf(sv[j]) + bv[j];
+                    t = cur.xr[j] * exp_fast(sv[j]) + bv[j];
                     ld = ld + om * sv[j];
                 }
                 const float v = xa + om * t;

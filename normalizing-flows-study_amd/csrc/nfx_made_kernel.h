@@ -95,7 +95,7 @@ __device__ __forceinline__ float made_affine(float xv, float mu, float al, float
         // z = (x - mu) * exp(clamp(-alpha, -5, 5)); guard z -> 0 (:35)
         const float a = tclamp(al, -3.f, 3.f);
         acc = acc + a;
-        const float z = (xv - mu) * expf(tclamp(-a, -5.f, 5.f));
+        const float z = (xv - mu) * exp_fast(tclamp(-a, -5.f, 5.f));
         return nonfinite(z) ? 0.f : z;
     } else {
         // inverse_autoregressive_flow.py:40-53: alpha = clamp(alpha,-2,2); mu = clamp(mu,-10,10);
@@ -103,7 +103,7 @@ __device__ __forceinline__ float made_affine(float xv, float mu, float al, float
         const float a = tclamp(al, -2.f, 2.f);
         const float m = tclamp(mu, -10.f, 10.f);
         acc = acc + a;
-        const float y = xv * expf(tclamp(a, -3.f, 3.f)) + m;
+        const float y = xv * exp_fast(tclamp(a, -3.f, 3.f)) + m;
         return nonfinite(y) ? xv : y;
     }
 }
@@ -357,14 +357,14 @@ __global__ __launch_bounds__(64) void made_seq_kernel(
         if constexpr (VAR == NFX_MAF_FORWARD) {
             // masked_autoregressive_flow.py:57-65
             const float a = tclamp(al, -3.f, 3.f);
-            xi = xin * expf(tclamp(a, -5.f, 5.f)) + mu;
+            xi = xin * exp_fast(tclamp(a, -5.f, 5.f)) + mu;
             ld = ld + a;
             if (valid) out[s * d + i] = nonfinite(xi) ? 0.f : xi;
         } else {
             // inverse_autoregressive_flow.py:79-88
             const float a = tclamp(al, -2.f, 2.f);
             const float m = tclamp(mu, -10.f, 10.f);
-            xi = (xin - m) * expf(tclamp(-a, -3.f, 3.f));
+            xi = (xin - m) * exp_fast(tclamp(-a, -3.f, 3.f));
             ld = ld - a;
             if (valid) out[s * d + i] = nonfinite(xi) ? xin : xi;
         }

@@ -63,28 +63,13 @@ struct SplineConsts {
     float rs_from_scale;        // (hi-lo)/(2B)
 };
 
-// exp(x) for x <= 20 (softmax numerators are <= 0, softplus arguments <= 20): x*log2(e) carried as a compensated pair (t, e) so the
-// hardware exp2 sees the exactly-rounded t and the product's rounding error is folded back as
-// exp2(t) * (1 + e*ln2). A few ulp like expf, at 6 instructions instead of 13 (no overflow
-// path needed; results below 2^-126 are irrelevant next to the softmax sum >= 1).
-__device__ __forceinline__ float exp_nonpos(float x) {
-    const float t = x * 1.44269502f;
-    const float e = __builtin_fmaf(x, 1.44269502f, -t) + x * 1.9259629e-8f;
-    const float r = __builtin_amdgcn_exp2f(t);
-    return __builtin_fmaf(r, e * 0.693147182f, r);
-}
-
-// Same for x <= 20 (softplus below its threshold; no overflow possible). Large negative x
-// underflows to 0 like expf.
-__device__ __forceinline__ float exp_small(float x) { return exp_nonpos(x); }
-
 // torch softplus (beta=1, threshold=20): x > 20 ? x : log1p(exp(x)).
 // log1p(u) = log(w) * u / (w - 1) with w = fl(1 + u) (exact u when w == 1): the rounding error
 // of 1 + u cancels in the ratio, giving log1p to a few ulp for every u > 0 at ~1/6 the cost of
 // the double-float log1pf (which dominated the spline's vector time).
 __device__ __forceinline__ float tsoftplus(float x) {
 #pragma clang fp contract(off)
-    const float u = exp_small(x);
+    const float u = exp_fast(x);
     const float w = 1.f + u;
     const float wm1 = w - 1.f;
     const float l = wm1 == 0.f ? u : logf(w) * (u * __builtin_amdgcn_rcpf(wm1));
@@ -111,7 +96,7 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
             for (int k = 1; k < K; ++k) m = tmax(m, p[k]);
             float s = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) { w[k] = exp_nonpos(p[k] - m); s = s + w[k]; }
+            for (int k = 0; k < K; ++k) { w[k] = exp_fast(p[k] - m); s = s + w[k]; }
             const float inv = 1.f / s;
 #pragma unroll
             for (int k = 0; k < K; ++k) w[k] = tclamp_min(C.min_w + C.cw * (w[k] * inv), eps);
@@ -122,7 +107,7 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
             for (int k = 1; k < K; ++k) m = tmax(m, p[K + k]);
             float s = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) { h[k] = exp_nonpos(p[K + k] - m); s = s + h[k]; }
+            for (int k = 0; k < K; ++k) { h[k] = exp_fast(p[K + k] - m); s = s + h[k]; }
             const float inv = 1.f / s;
 #pragma unroll
             for (int k = 0; k < K; ++k) h[k] = tclamp_min(C.min_h + C.ch * (h[k] * inv), eps);
