@@ -86,7 +86,9 @@ constexpr int kStageStride = 33;              // wave-private x tile [64][33] (c
 constexpr int kTileStride = 65;               // made_tile_kernel x tile [32][65] (d <= 64)
 constexpr int kStageFloats = 64 * kStageStride;
 
-// Affine epilogues (exact reference op order and clamps).
+// Affine epilogues (exact reference op order and clamps). The reference's second clamp of the
+// scale exponent (clamp(-alpha, -5, 5) after alpha in [-3, 3]; clamp(alpha, -3, 3) after alpha in
+// [-2, 2]) is the identity on that range, NaN included, and is not repeated here.
 template <int VAR>
 __device__ __forceinline__ float made_affine(float xv, float mu, float al, float& acc) {
 #pragma clang fp contract(off)  // separate mul/add roundings, as the reference's torch ops
@@ -95,7 +97,7 @@ __device__ __forceinline__ float made_affine(float xv, float mu, float al, float
         // z = (x - mu) * exp(clamp(-alpha, -5, 5)); guard z -> 0 (:35)
         const float a = tclamp(al, -3.f, 3.f);
         acc = acc + a;
-        const float z = (xv - mu) * exp_fast(tclamp(-a, -5.f, 5.f));
+        const float z = (xv - mu) * exp_fast(-a);
         return nonfinite(z) ? 0.f : z;
     } else {
         // inverse_autoregressive_flow.py:40-53: alpha = clamp(alpha,-2,2); mu = clamp(mu,-10,10);
@@ -103,7 +105,7 @@ __device__ __forceinline__ float made_affine(float xv, float mu, float al, float
         const float a = tclamp(al, -2.f, 2.f);
         const float m = tclamp(mu, -10.f, 10.f);
         acc = acc + a;
-        const float y = xv * exp_fast(tclamp(a, -3.f, 3.f)) + m;
+        const float y = xv * exp_fast(a) + m;
         return nonfinite(y) ? xv : y;
     }
 }
@@ -357,14 +359,14 @@ __global__ __launch_bounds__(64) void made_seq_kernel(
         if constexpr (VAR == NFX_MAF_FORWARD) {
             // masked_autoregressive_flow.py:57-65
             const float a = tclamp(al, -3.f, 3.f);
-            xi = xin * exp_fast(tclamp(a, -5.f, 5.f)) + mu;
+            xi = xin * exp_fast(a) + mu;
             ld = ld + a;
             if (valid) out[s * d + i] = nonfinite(xi) ? 0.f : xi;
         } else {
             // inverse_autoregressive_flow.py:79-88
             const float a = tclamp(al, -2.f, 2.f);
             const float m = tclamp(mu, -10.f, 10.f);
-            xi = (xin - m) * exp_fast(tclamp(-a, -3.f, 3.f));
+            xi = (xin - m) * exp_fast(-a);
             ld = ld - a;
             if (valid) out[s * d + i] = nonfinite(xi) ? xin : xi;
         }

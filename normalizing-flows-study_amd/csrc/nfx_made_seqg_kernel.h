@@ -163,14 +163,14 @@ __global__ __launch_bounds__(512) void made_seqg_kernel(
                 if constexpr (VAR == NFX_MAF_FORWARD) {
                     // masked_autoregressive_flow.py:57-65
                     const float a = tclamp(al, -3.f, 3.f);
-                    vi = xin * exp_fast(tclamp(a, -5.f, 5.f)) + mu;
+                    vi = xin * exp_fast(a) + mu;
                     ld = ld + a;
                     vo = nonfinite(vi) ? 0.f : vi;
                 } else {
                     // inverse_autoregressive_flow.py:79-88
                     const float a = tclamp(al, -2.f, 2.f);
                     const float m = tclamp(mu, -10.f, 10.f);
-                    vi = (xin - m) * exp_fast(tclamp(-a, -3.f, 3.f));
+                    vi = (xin - m) * exp_fast(-a);
                     ld = ld - a;
                     vo = nonfinite(vi) ? xin : vi;
                 }

@@ -357,15 +357,15 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
             out_pair2_n<HT, HT>(dense ? HT : nkp[L.nk4 + j], wbj, B4, j, h1, mu0, mu1, al0, al1);
             put_x(false);
             wave_lds_sync();
+            // rows past d: zero weights and bias (alpha = 0 adds nothing to the log-det) and a
+            // zero x column; their z lands in the tile padding and is never stored
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = crow(r, h);
-                if (32 * j + row < d) {
-                    float* p0 = xt + col * kStageStride + row;
-                    float* p1 = xt + (32 + col) * kStageStride + row;
-                    *p0 = made_affine<VAR>(*p0, mu0[r], al0[r], acc0);
-                    *p1 = made_affine<VAR>(*p1, mu1[r], al1[r], acc1);
-                }
+                float* p0 = xt + col * kStageStride + row;
+                float* p1 = xt + (32 + col) * kStageStride + row;
+                *p0 = made_affine<VAR>(*p0, mu0[r], al0[r], acc0);
+                *p1 = made_affine<VAR>(*p1, mu1[r], al1[r], acc1);
             }
             wave_lds_sync();
             {
