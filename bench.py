@@ -143,6 +143,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the captured HIP graph of the pass (nfs_amd.GraphedFlow) instead of eager launches")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: split ONE global batch (default 1M) over the ranks")
     a = ap.parse_args()
@@ -170,10 +172,20 @@ def main():
     x = torch.randn(B, d, device=dev, generator=g)
     flow = model.flow if hasattr(model, "flow") else model
 
+    graphed = None
+    if a.graph:
+        graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
+
     def step():
-        if sampling:  # sampling pass: x = forward(z), no exchange
+        if graphed is not None:
+            out = graphed()
+            if sampling:
+                return out
+            sums = out[1]
+        elif sampling:  # sampling pass: x = forward(z), no exchange
             return flow.forward(x)
-        logp, sums = flow.log_prob(x, return_sums=True)
+        else:
+            logp, sums = flow.log_prob(x, return_sums=True)
         if world > 1:
             dist.all_reduce(sums)  # RCCL over xGMI: 16 bytes
         return sums
@@ -197,11 +209,14 @@ def main():
         # ~5 us of GPU idle between kernels (measured, profiles/).
         flow.layer_events = []
         for _ in range(a.steps):
-            step()
+            if sampling:
+                flow.forward(x)
+            else:
+                flow.log_prob(x, return_sums=True)
         torch.cuda.synchronize()
         events = flow.layer_events
         flow.layer_events = None
-    if nfs_amd.STATS["torch"] != 0 or nfs_amd.STATS["hip"] == 0:
+    if nfs_amd.STATS["torch"] != 0 or (nfs_amd.STATS["hip"] == 0 and graphed is None):
         raise RuntimeError(f"hot path did not run on the HIP kernels: {nfs_amd.STATS}")
     t_all = torch.tensor([t], device=dev, dtype=torch.float64)
     if world > 1:
@@ -237,7 +252,8 @@ def main():
             "data": "synthetic: x ~ N(0,1) generated on device (seed 1234+rank); seeded random-init "
                     "weights perturbed N(0, 0.1^2) with non-trivial BatchNorm running stats",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B_global,
-                       "parallelism": f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"},
+                       "parallelism": f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)",
+                       "launch": "hip-graph replay" if a.graph else "eager"},
             "nll_f64": nll,
             "roofline": {"bound": "mfma", "pipe": "valu" if a.config == "cfg5i" else "mfma",
                          "kernel": kname, "achieved": achieved,

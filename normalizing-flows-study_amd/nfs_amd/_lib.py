@@ -112,7 +112,8 @@ def load(path=LIB_PATH):
 
 
 def lib():
-    return load()
+    l = _lib
+    return l if l is not None else load()
 
 
 def available():
@@ -130,12 +131,21 @@ def check(rc, what):
 
 
 def ptr(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """Device address of a tensor as a plain int (ctypes c_void_p arguments accept ints)."""
+    return None if t is None else t.data_ptr()
+
+
+try:
+    _raw_stream = torch._C._cuda_getCurrentRawStream
+except AttributeError:  # pragma: no cover - older torch
+    _raw_stream = None
 
 
 def stream_of(t):
     """hipStream_t of torch's current stream on t's device (the stream kernels are enqueued on)."""
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    if _raw_stream is not None and t.device.type == "cuda":
+        return _raw_stream(t.device.index if t.device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(t.device).cuda_stream
 
 
 def mlp_raw(linears, batchnorms=(), masks=None):

@@ -123,7 +123,7 @@ class _MadeAffineFlow(HipFlow):
         self.conditioner = MADE(dim, hidden_dim, 2, use_batch_norm=use_batch_norm)
 
     def _torch_only(self):
-        return any(bn.training or bn.running_mean is None for bn in self.conditioner.batchnorms())
+        return any(bn.training or bn.running_mean is None for bn in self._batchnorms())
 
     def _hip_supported(self, x):
         d, H = self.dim, self.conditioner.hidden_dim

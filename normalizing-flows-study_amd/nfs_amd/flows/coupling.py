@@ -68,8 +68,7 @@ class CouplingLayer(HipFlow):
     def _torch_only(self):
         # Train-mode BatchNorm normalises with batch statistics (batch-global), which a
         # per-sample fused kernel cannot reproduce; the eval hot path folds running stats.
-        bns = [m for m in list(self.s_net) + list(self.b_net) if isinstance(m, nn.BatchNorm1d)]
-        return any(bn.training or bn.running_mean is None for bn in bns)
+        return any(bn.training or bn.running_mean is None for bn in self._batchnorms())
 
     def _hip_supported(self, x):
         d, H = self.data_dim, self._hidden()

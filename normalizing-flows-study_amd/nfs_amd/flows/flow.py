@@ -150,17 +150,48 @@ class HipFlow(Flow):
         return False
 
     # -- packed-weight cache -------------------------------------------------------------
+    # The cache key must notice every change of a parameter/buffer (in-place optimizer steps
+    # and load_state_dict bump `_version`, `.to()` moves `data_ptr`, assigning a new Parameter
+    # or submodule replaces the object). Walking `parameters()` per call costs ~15 us per layer
+    # (named_modules traversal), more than a small-batch kernel, so the module tree is resolved
+    # once into direct references to each module's `_parameters`/`_buffers` dicts plus the
+    # parent->child links, and re-resolved only when one of those links changed.
+    def _nfx_binding(self):
+        b = self.__dict__.get("_nfx_bind")
+        if b is not None:
+            for parent, name, child in b[0]:
+                if parent.get(name) is not child:
+                    b = None
+                    break
+        if b is None:
+            links, slots = [], []
+            for mod in self.modules():
+                for name, child in mod._modules.items():
+                    links.append((mod._modules, name, child))
+                for name in mod._parameters:
+                    slots.append((mod._parameters, name))
+                for name in mod._buffers:
+                    slots.append((mod._buffers, name))
+            bns = [m for m in self.modules() if isinstance(m, nn.BatchNorm1d)]
+            b = (links, slots, bns)
+            object.__setattr__(self, "_nfx_bind", b)
+        return b
+
+    def _batchnorms(self):
+        return self._nfx_binding()[2]
+
     def _state_key(self, device):
-        key = [str(device)]
-        for t in list(self.parameters()) + list(self.buffers()):
-            key.append((t.data_ptr(), t._version))
+        key = [device]
+        for d, name in self._nfx_binding()[1]:
+            t = d[name]
+            key.append(None if t is None else (t.data_ptr(), t._version))
         return tuple(key)
 
     def _packed(self, device, build):
         """Return the cached device weight image, rebuilding it when any parameter/buffer
         changed (in-place optimizer steps and load_state_dict bump tensor versions)."""
         key = self._state_key(device)
-        cache = getattr(self, "_nfx_pack_cache", None)
+        cache = self.__dict__.get("_nfx_pack_cache")
         if cache is not None and cache[0] == key:
             return cache[1]
         packed = build(device)
