@@ -142,6 +142,26 @@ int nfx_made_affine_logprob(const float* packed, const float* in, float* out, fl
                             int variant, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Training: backward of MaskedAutoregressiveFlow.inverse
+ * (masked_autoregressive_flow.py:18-44) under autograd — the reference's density-training
+ * direction — for d <= 64, H <= 64 and no BatchNorm (NFX_EUNSUPPORTED otherwise).
+ * nfx_made_pack_backward adds the transposed weight tiles to a packed image built by
+ * nfx_made_pack (same buffer). nfx_made_affine_backward recomputes the layer and writes
+ *   grad_in [B, d]  = dL/dx
+ *   factors [3d + 6H + 4][B], feature-major rows:
+ *     [δμ | δα] (2d) | δ3 | δ2 | δ1 (H each) | h3, 1 | h2, 1 | h1, 1 (H + 1 each) | x, 1 (d + 1)
+ * from grad_out = dL/dz [B, d] and grad_log_det = dL/dlog_det [B]. The parameter gradients
+ * are plain GEMMs over the sample dimension: [dW4 | db4] = [δμ;δα]·[h3;1]ᵀ, [dW3 | db3] =
+ * δ3·[h2;1]ᵀ, [dW2 | db2] = δ2·[h1;1]ᵀ, [dW1 | db1] = δ1·[x;1]ᵀ (each dW ⊙ its MADE mask).
+ * `factors` holds nfx_made_backward_factor_floats(B, d, H) floats.
+ * ------------------------------------------------------------------------------------- */
+int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
+size_t nfx_made_backward_factor_floats(int64_t B, int d, int H);
+int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,
+                             const float* grad_log_det, float* grad_in, float* factors, int64_t B,
+                             int d, int H, int variant, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Gaussian base log-density + NLL partial sums — the log_prob glue of the callers
  * (Flow.log_prob src/flows/flow/flow.py:56-73; README.md:113-114; src/utils.py:39-55):
  *   logp[i] = -0.5 * (fp32(d*log(2*pi)) + sum_j z[i,j]^2) + log_det[i]

@@ -20,7 +20,7 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     const MadeLayout L = made_layout(d, HT);
     const int Hp = L.Hp, G1 = 4 * L.NKC;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
-        if (i >= L.s_deg + Hp) continue;  // completion-order tables are scattered below
+        if (i >= L.s_deg) continue;  // degree tables: made_live_kernel
         float v = 0.f;
         if (i < L.b1) {
             int t = i - L.w1, rr = t & 3, lane = (t >> 2) & 63, g = (t >> 8) % G1, ht = (t >> 8) / G1;
@@ -69,18 +69,6 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
         } else if (i < L.s_deg) {
             int row = i - L.s_b4;
             v = row < 2 * d ? mlp_bias(net, 3, row) : 0.f;
-        } else {
-            // unit a: degree, and its position in the stable by-degree completion order
-            const int a = i - L.s_deg;
-            const int da = a < H ? made_unit_degree(net, d, a) : 1000000000;
-            int rank = 0;
-            for (int b = 0; b < Hp; ++b) {
-                const int db = b < H ? made_unit_degree(net, d, b) : 1000000000;
-                rank += (db < da || (db == da && b < a)) ? 1 : 0;
-            }
-            packed[L.s_deg + Hp + rank] = (float)da;
-            packed[L.s_deg + 2 * Hp + rank] = (float)a;
-            v = (float)da;
         }
         packed[i] = v;
     }
@@ -99,6 +87,22 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
 __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
+    // hidden-unit degrees (row sums of the input mask) and the stable by-degree completion
+    // order of the sequential kernels: s_deg [unit degree | degrees in order | units in order]
+    {
+        __shared__ int deg[128];
+        const int Hp = L.Hp;
+        for (int a = threadIdx.x; a < Hp; a += 256) deg[a] = a < H ? made_unit_degree(net, d, a) : 1000000000;
+        __syncthreads();
+        for (int a = threadIdx.x; a < Hp; a += 256) {
+            const int da = deg[a];
+            int rank = 0;
+            for (int b = 0; b < Hp; ++b) rank += (deg[b] < da || (deg[b] == da && b < a)) ? 1 : 0;
+            packed[L.s_deg + a] = (float)da;
+            packed[L.s_deg + Hp + rank] = (float)da;
+            packed[L.s_deg + 2 * Hp + rank] = (float)a;
+        }
+    }
     int* nk = reinterpret_cast<int*>(packed);
     const int n1 = HT * 4 * L.NKC, n23 = HT * HT * 4, n4 = L.NJ * 2 * HT * 4;
     for (int i = threadIdx.x; i < 3 * HT + L.NJ; i += 256) nk[L.nk1 + i] = 0;

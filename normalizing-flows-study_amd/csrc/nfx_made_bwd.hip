@@ -1,0 +1,356 @@
+// Backward (training) pass of the MAF density direction — MaskedAutoregressiveFlow.inverse
+// (masked_autoregressive_flow.py:18-44) under autograd, d <= 64, H <= 64, no BatchNorm.
+// SURVEY.md §8(f) item 1.
+//
+// One fused kernel per layer recomputes the forward on fp32 MFMA (same tile kernel structure
+// as made_tile_kernel: a wave owns 32 samples, hidden activations stay in accumulator registers)
+// and runs the data-gradient chain back through the net on MFMA with the TRANSPOSED weights:
+// the (mu, alpha) gradients δ4 come out of the affine epilogue's backward in accumulator layout,
+// which is exactly the B operand of gh3 = W4mᵀ δ4; each ReLU backward masks with the kept
+// activations; gx = the epilogue's direct term + W1mᵀ δ1. The weight gradients are reductions
+// over the SAMPLE dimension (K = B), which the per-sample tile layout cannot contract without a
+// transpose per tile, so the kernel writes the per-sample factors feature-major (δ4ᵀ, δ3ᵀ, δ2ᵀ,
+// δ1ᵀ, h3ᵀ, h2ᵀ, h1ᵀ: coalesced 128-byte rows, one half-wave per feature row) and the weight
+// gradients are plain GEMMs over them (gW4 = δ4ᵀ·h3, …, gW1 = δ1ᵀ·x; hipBLASLt through torch),
+// masked like the reference's weight*mask.
+//
+// Epilogue backward, per element (torch semantics of the reference ops):
+//   a = clamp(alpha, -3, 3); e = exp(-a); zr = (x - mu) * e; z = finite(zr) ? zr : 0
+//   ld_raw = -sum a; ld1 = finite(ld_raw) ? ld_raw : 0; ld = clamp(ld1, -100, 100)
+//   gzr = finite(zr) ? gz : 0;  gld1 = gld * [-100 <= ld1 <= 100] * finite(ld_raw)
+//   gx += gzr * e;  gmu = -gzr * e;  galpha = [-3 <= alpha <= 3] * (-(gzr * (x - mu) * e) - gld1)
+#include "nfx_made_kernel.h"
+#include "nfx_pack.h"
+
+namespace nfx {
+
+__global__ void made_bwd_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
+    for (int i = L.t4 + blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
+        float v = 0.f;
+        int base, nk;
+        if (i < L.t3) { base = L.t4; nk = 2 * L.NJ; }
+        else if (i < L.t2) { base = L.t3; nk = HT; }
+        else if (i < L.t1) { base = L.t2; nk = HT; }
+        else { base = L.t1; nk = HT; }
+        const int t = i - base, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+        const int kt = (t >> 10) % nk, ot = (t >> 10) / nk;
+        const int row = 32 * ot + (lane & 31);                     // out index (rows of the transposed)
+        const int kk = crow(4 * rq + rr, lane >> 5);               // k index inside the k tile
+        if (i < L.t3) {
+            const int j = kt >> 1, which = kt & 1, o = 32 * j + kk;  // output block (mu | alpha)
+            v = (row < H && o < d) ? mlp_weight(net, 3, H, which * d + o, row) : 0.f;
+        } else if (i < L.t1) {
+            const int layer = i < L.t2 ? 2 : 1, k = 32 * kt + kk;
+            v = (row < H && k < H) ? mlp_weight(net, layer, H, k, row) : 0.f;
+        } else {
+            const int k = 32 * kt + kk;                              // hidden unit
+            v = (row < d && k < H) ? mlp_weight(net, 0, d, k, row) : 0.f;
+        }
+        packed[i] = v;
+    }
+}
+
+// Feature-major store of one accumulator tile: rows `row0 + crow(r, h)` (< nrows) of a
+// [nrows x B] matrix, columns = the tile's 32 samples (base + col < B).
+__device__ __forceinline__ void store_fm(float* __restrict__ dst, const f32x16& t, int row0, int nrows, int64_t B,
+                                         int64_t base) {
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int64_t s = base + col;
+    if (s >= B) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = row0 + crow(r, h);
+        if (row < nrows) dst[(int64_t)row * B + s] = t[r];
+    }
+}
+
+// A-operand (weights) x B-operand (accumulator-layout tiles) chain over NK k tiles, A from
+// global/L2 in [out tile][k tile][r/4][lane][r%4] order.
+template <int NK>
+__device__ __forceinline__ f32x16 chain_gmem(const float* __restrict__ A, int ot, int nk_total,
+                                             const f32x16* bt, f32x16 acc) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(A + (((ot * nk_total + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) acc = mfma32(w[rr], bt[kt][4 * rq + rr], acc);
+        }
+    }
+    return acc;
+}
+
+template <int HT>
+__global__ __launch_bounds__(256) void made_bwd_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, const float* __restrict__ gout,
+    const float* __restrict__ gld_in, float* __restrict__ gin, float* __restrict__ acts, int64_t B, int d,
+    int H, int64_t ntiles) {
+    const MadeLayout L = made_layout(d, HT);
+    constexpr int S = kTileStride;
+    extern __shared__ f32x4 lds4[];
+    float* lds = reinterpret_cast<float*>(lds4);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int i = threadIdx.x; i < L.par_total / 4; i += 256) lds4[i] = reinterpret_cast<const f32x4*>(packed)[i];
+    float* xt = lds + L.par_total + wave * 2 * 32 * S;  // x tile, then gz tile
+    float* gt = xt + 32 * S;
+    __syncthreads();
+    const float* W = lds;
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int voff = lane < d ? lane * 4 : (1 << 30);
+    const int rowb = d * 4;
+    const int NJ = L.NJ, NKC = L.NKC;
+    // feature-major factors: [d4 (2d) | d3 | d2 | d1 (H each) | h3, 1 | h2, 1 | h1, 1 (H+1 each) |
+    // x, 1 (d+1)] rows x B — the trailing ones rows turn each weight-gradient GEMM into the
+    // bias gradient as well (its last column)
+    float* D4 = acts;
+    float* D3 = D4 + (int64_t)2 * d * B;
+    float* D2 = D3 + (int64_t)H * B;
+    float* D1 = D2 + (int64_t)H * B;
+    float* H3 = D1 + (int64_t)H * B;
+    float* H2 = H3 + (int64_t)(H + 1) * B;
+    float* H1 = H2 + (int64_t)(H + 1) * B;
+    float* X1 = H1 + (int64_t)(H + 1) * B;
+
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+        const int64_t base = t * 32;
+        const int rows = (int)(B - base < 32 ? B - base : 32);
+        {
+            const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + base * d, 0, rows * rowb, 0x00020000);
+            const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gout) + base * d, 0, rows * rowb, 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                xt[r * S + lane] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff, r * rowb, 0));
+                gt[r * S + lane] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, voff, r * rowb, 0));
+            }
+        }
+        wave_lds_sync();
+        const float* Wf = W + opaque_zero();
+        {
+            // x and the ones rows, feature-major: half-wave h writes dim row 2i+h of 32 samples
+            const int64_t s = base + col;
+            if (s < B) {
+                for (int i = 0; i < 32; ++i) {
+                    const int dim = 2 * i + h;
+                    if (dim < d) X1[(int64_t)dim * B + s] = xt[col * S + dim];
+                }
+                if (h == 0) {
+                    X1[(int64_t)d * B + s] = 1.f;
+                    H3[(int64_t)H * B + s] = 1.f;
+                    H2[(int64_t)H * B + s] = 1.f;
+                    H1[(int64_t)H * B + s] = 1.f;
+                }
+            }
+        }
+
+        // ---- forward (dense) ----
+        f32x16 h1[HT], h2[HT], h3[HT];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(Wf + L.b1 + ht * 32, h);
+        for (int kc = 0; kc < NKC; ++kc) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(Wf + L.w1 + ((ht * 4 * NKC + kc * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) h1[ht] = mfma32(w[rr], xt[col * S + 32 * kc + 8 * g + 2 * rr + h], h1[ht]);
+                }
+            }
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
+        made_hidden1<HT>(Wf, L.w2, L.b2, h1, h2);
+        made_hidden1<HT>(Wf, L.w3, L.b3, h2, h3);
+
+        // layer 4 for every output block (kept for the log-det sum), then the epilogue backward.
+        // d4[j*2 + 0] = mu / δmu rows of block j, d4[j*2 + 1] = alpha / δalpha rows (t4 k order).
+        f32x16 d4[4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j < NJ) {
+                f32x16 mu = load_bias16(Wf + L.b4 + (j * 2 + 0) * 32, h);
+                f32x16 al = load_bias16(Wf + L.b4 + (j * 2 + 1) * 32, h);
+#pragma unroll
+                for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+                    for (int rq = 0; rq < 4; ++rq) {
+                        const f32x4 wm = *reinterpret_cast<const f32x4*>(
+                            Wf + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                        const f32x4 wa = *reinterpret_cast<const f32x4*>(
+                            Wf + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) {
+                            mu = mfma32(wm[rr], h3[kt][4 * rq + rr], mu);
+                            al = mfma32(wa[rr], h3[kt][4 * rq + rr], al);
+                        }
+                    }
+                }
+                d4[2 * j] = mu;
+                d4[2 * j + 1] = al;
+            } else {
+                d4[2 * j] = d4[2 * j + 1] = f32x16{};
+            }
+        }
+        // ld_raw = -sum_i clamp(alpha_i, -3, 3) of the lane's sample, summed in the forward
+        // kernel's order (rows past d: alpha = 0)
+        float asum0 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) asum0 = asum0 + tclamp(d4[2 * j + 1][r], -3.f, 3.f);
+        const float ldraw = -halves_sum(asum0, asum0);
+        const float gld = (lane < 32 && col < rows) ? gld_in[base + col] : 0.f;
+        float gld1 = nonfinite(ldraw) ? 0.f : gld;
+        const float ld1 = nonfinite(ldraw) ? 0.f : ldraw;
+        if (!(ld1 >= -100.f && ld1 <= 100.f)) gld1 = 0.f;
+        const float gld1s = __shfl(gld1, col, 64);  // both lane halves of sample col
+
+        // epilogue backward; the direct dz/dx term replaces x in the tile (same lane, same slot)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int dim = 32 * j + crow(r, h);
+                float* px = xt + col * S + dim;
+                const float xv = *px;
+                const float gz = gt[col * S + dim];
+                const float alpha = d4[2 * j + 1][r];
+                const float a = tclamp(alpha, -3.f, 3.f);
+                const float e = exp_fast(-a);
+                const float xm = xv - d4[2 * j][r];
+                const float zr = xm * e;
+                const float gzr = nonfinite(zr) ? 0.f : gz;
+                const float ge = gzr * e;
+                *px = ge;
+                d4[2 * j][r] = -ge;                                          // δmu
+                const float ga = -(gzr * xm * e) - gld1s;
+                d4[2 * j + 1][r] = (alpha >= -3.f && alpha <= 3.f) ? ga : 0.f;  // δalpha
+            }
+        }
+
+        // ---- data-gradient chain on MFMA with the transposed weights (L2); every factor is
+        // written feature-major as soon as it is final so it can die ----
+        f32x16 g[HT];
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) {
+            f32x16 acc = NJ == 2 ? chain_gmem<4>(packed + L.t4, ot, 4, d4, f32x16{})
+                                 : chain_gmem<2>(packed + L.t4, ot, 2, d4, f32x16{});
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = h3[ot][r] > 0.f ? acc[r] : 0.f;
+            g[ot] = acc;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j < NJ) {
+                store_fm(D4, d4[2 * j], 32 * j, d, B, base);                        // mu rows
+                store_fm(D4 + (int64_t)d * B, d4[2 * j + 1], 32 * j, d, B, base);   // alpha rows
+            }
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            store_fm(D3, g[ht], 32 * ht, H, B, base);
+            store_fm(H3, h3[ht], 32 * ht, H, B, base);
+        }
+        f32x16 g2[HT];
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) {
+            f32x16 acc = chain_gmem<HT>(packed + L.t3, ot, HT, g, f32x16{});
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = h2[ot][r] > 0.f ? acc[r] : 0.f;
+            g2[ot] = acc;
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            store_fm(D2, g2[ht], 32 * ht, H, B, base);
+            store_fm(H2, h2[ht], 32 * ht, H, B, base);
+        }
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) {
+            f32x16 acc = chain_gmem<HT>(packed + L.t2, ot, HT, g2, f32x16{});
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = h1[ot][r] > 0.f ? acc[r] : 0.f;
+            g[ot] = acc;
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            store_fm(D1, g[ht], 32 * ht, H, B, base);
+            store_fm(H1, h1[ht], 32 * ht, H, B, base);
+        }
+        // gx = direct term (in the tile) + W1mᵀ δ1, accumulator layout rows = dims
+        wave_lds_sync();
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+            if (ot < NKC) {
+                const f32x16 gx = chain_gmem<HT>(packed + L.t1, ot, HT, g, f32x16{});
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float* px = xt + col * S + 32 * ot + crow(r, h);
+                    *px = *px + gx[r];
+                }
+            }
+        }
+
+        // ---- gx rows out of the tile, coalesced ----
+        wave_lds_sync();
+        {
+            const auto ro = __builtin_amdgcn_make_buffer_rsrc(gin + base * d, 0, rows * rowb, 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 32; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xt[r * S + lane]), ro, voff, r * rowb, 0);
+        }
+        wave_lds_sync();
+    }
+}
+
+}  // namespace nfx
+
+using namespace nfx;
+
+extern "C" int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
+    if (!net || !packed) return set_error(NFX_EINVAL, "made_pack_backward: null pointer");
+    if (d <= 0 || d > 4096 || H <= 0 || H > 128)
+        return set_error(NFX_EUNSUPPORTED, "made_pack_backward: d=%d H=%d outside d<=4096, H<=128", d, H);
+    const MadeLayout L = made_layout(d, (H + 31) / 32);
+    int blocks = (L.total - L.t4 + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    made_bwd_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
+    return check_launch("made_bwd_pack_kernel");
+}
+
+extern "C" size_t nfx_made_backward_factor_floats(int64_t B, int d, int H) {
+    if (B < 0 || d <= 0 || H <= 0) return 0;
+    return (size_t)B * (size_t)(3 * d + 6 * H + 4);
+}
+
+extern "C" int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,
+                                        const float* grad_log_det, float* grad_in, float* factors,
+                                        int64_t B, int d, int H, int variant, void* stream) {
+    if (variant != NFX_MAF_INVERSE)
+        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: only NFX_MAF_INVERSE (density training)");
+    if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine_backward: bad shape");
+    if (d > 64 || H > 64)
+        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: d=%d H=%d outside d<=64, H<=64", d, H);
+    if (B == 0) return NFX_OK;
+    if (!packed || !in || !grad_out || !grad_log_det || !grad_in || !factors)
+        return set_error(NFX_EINVAL, "made_affine_backward: null pointer");
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
+    const size_t lds = ((size_t)L.par_total + 4 * 2 * 32 * kTileStride) * sizeof(float);
+    const void* k = HT == 1 ? (const void*)made_bwd_kernel<1> : (const void*)made_bwd_kernel<2>;
+    int rc = prepare_lds(k, lds);
+    if (rc) return rc;
+    const int64_t ntiles = (B + 31) / 32;
+    const int grid = resident_grid(k, 256, lds, (ntiles + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+    if (HT == 1)
+        made_bwd_kernel<1><<<grid, 256, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
+    else
+        made_bwd_kernel<2><<<grid, 256, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
+    return check_launch("made_bwd_kernel");
+}

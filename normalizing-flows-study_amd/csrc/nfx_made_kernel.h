@@ -37,12 +37,18 @@ namespace nfx {
 //   nk1 [HT]  in 32-input chunks (layer 1)      nk2 [HT], nk3 [HT]  in 32-unit tiles
 //   nk4 [NJ]  in 32-unit tiles (mu and alpha rows of output tile pair j)
 //   tsafe (float): inputs with max|x| <= tsafe cannot overflow any layer (made_live_kernel)
+// then the transposed A-operand images of the backward data path (made_bwd_pack_kernel,
+// same [out tile][k tile][r/4][lane][r%4] order; row = out index, col = k index):
+//   t4 [HT][2*NJ][4][64][4]   W4mᵀ: hidden rows x (mu|alpha block) k tiles
+//   t3 [HT][HT]..., t2 [HT][HT]...  W3mᵀ, W2mᵀ
+//   t1 [NKC][HT]...           W1mᵀ: input rows x hidden k tiles
 struct MadeLayout {
     int d, HT, Hp, NKC, NJ;
     int w1, b1, w2, b2, w3, b3, w4, b4;  // parallel image
     int par_total;                       // floats of the parallel image (LDS-resident prefix)
     int s_w1t, s_b1, s_w2, s_b2, s_w3, s_b3, s_w4, s_b4, s_deg;
-    int nk1, nk2, nk3, nk4, tsafe, total;
+    int nk1, nk2, nk3, nk4, tsafe;
+    int t4, t3, t2, t1, total;
 };
 
 __host__ __device__ constexpr int made_up4(int v) { return (v + 3) & ~3; }
@@ -78,7 +84,12 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     L.nk3 = o; o += HT;
     L.nk4 = o; o += L.NJ;
     L.tsafe = o; o += 1;
-    L.total = made_up4(o);
+    o = made_up4(o);
+    L.t4 = o; o += HT * 2 * L.NJ * 1024;
+    L.t3 = o; o += HT * HT * 1024;
+    L.t2 = o; o += HT * HT * 1024;
+    L.t1 = o; o += L.NKC * HT * 1024;
+    L.total = o;
     return L;
 }
 

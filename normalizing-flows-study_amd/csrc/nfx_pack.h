@@ -36,12 +36,21 @@ __device__ inline double block_mlp_tsafe(const NfxMlpRaw& net, int nl, const int
     double alpha = 1.0, beta = 0.0, tsafe = 3.0e38;
     for (int l = 0; l < nl; ++l) {
         double nmax = 0.0, cmax = 0.0;
-        for (int r = threadIdx.x; r < rows[l]; r += 256) {
+        // 8 threads per row, each over a strided slice of the columns: independent loads in
+        // flight instead of one serial row walk per thread
+        for (int r0 = 0; r0 < rows[l]; r0 += 32) {
+            const int r = r0 + (threadIdx.x >> 3), q = threadIdx.x & 7;
             double sum = 0.0;
-            for (int c = 0; c < cols[l]; ++c) sum += fabs((double)mlp_weight(net, l, cols[l], r, c));
-            nmax = (sum > nmax || sum != sum) ? sum : nmax;
-            const double b = fabs((double)mlp_bias(net, l, r));
-            cmax = (b > cmax || b != b) ? b : cmax;
+            if (r < rows[l])
+                for (int c = q; c < cols[l]; c += 8) sum += fabs((double)mlp_weight(net, l, cols[l], r, c));
+            sum += __shfl_xor(sum, 1);
+            sum += __shfl_xor(sum, 2);
+            sum += __shfl_xor(sum, 4);
+            if (r < rows[l]) {
+                nmax = (sum > nmax || sum != sum) ? sum : nmax;
+                const double b = fabs((double)mlp_bias(net, l, r));
+                cmax = (b > cmax || b != b) ? b : cmax;
+            }
         }
         for (int k = 0; k < 2; ++k) {
             red[threadIdx.x] = k == 0 ? nmax : cmax;

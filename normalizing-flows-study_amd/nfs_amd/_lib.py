@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
     "nfx_rqs_unit",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
+    "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_affine_backward",
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob",
 )
 
@@ -81,6 +82,9 @@ _SIGNATURES = {
     "nfx_made_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
     "nfx_made_affine": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_made_affine_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
+    "nfx_made_pack_backward": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
+    "nfx_made_backward_factor_floats": (_sz, [_i64, _int, _int]),
+    "nfx_made_affine_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_gauss_workspace_bytes": (_sz, [_i64]),
     "nfx_gauss_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _vp]),
 }

@@ -113,6 +113,25 @@ class MADE(nn.Module):
         return [m for m in self.net if isinstance(m, nn.BatchNorm1d)]
 
 
+def _sample_gemm(a, b, chunk=8192):
+    """a [M, B] · b [N, B]ᵀ for a long sample dimension B: split-K as one strided-batched GEMM
+    over B // chunk contiguous sample chunks (a library GEMM picks one tile column for such
+    shapes and leaves most CUs idle), plus the remainder, reduced over the chunks."""
+    M, Bn = a.shape
+    S = Bn // chunk
+    out = None
+    if S >= 2:
+        n = S * chunk
+        pa = a[:, :n].reshape(M, S, chunk).transpose(0, 1)               # [S, M, chunk]
+        pb = b[:, :n].reshape(b.shape[0], S, chunk).permute(1, 2, 0)     # [S, chunk, N]
+        out = torch.bmm(pa, pb).sum(dim=0)
+        a, b = a[:, n:], b[:, n:]
+    if a.shape[1] > 0:
+        r = a @ b.t()
+        out = r if out is None else out + r
+    return out
+
+
 class _MadeAffineFlow(HipFlow):
     """Shared HIP plumbing of MAF / IAF (conditioner = MADE(dim, H, 2))."""
 
@@ -141,8 +160,49 @@ class _MadeAffineFlow(HipFlow):
         bns = self.conditioner.batchnorms() or ()
         raw, keep = _lib.mlp_raw(lins, bns, masks=[lin.mask for lin in lins])
         _lib.check(L.nfx_made_pack(raw, d, H, _lib.ptr(packed), _lib.stream_of(packed)), "nfx_made_pack")
+        _lib.check(L.nfx_made_pack_backward(raw, d, H, _lib.ptr(packed), _lib.stream_of(packed)),
+                   "nfx_made_pack_backward")
         packed._nfx_keep = keep
         return packed
+
+    # -- training: fused backward of the parallel density direction (§8(f) item 1) --------
+    def _hip_backward_ok(self, x, direction):
+        d, H = self.dim, self.conditioner.hidden_dim
+        return (self._variant(direction) == _lib.NFX_MAF_INVERSE and d <= 64 and H <= 64
+                and not self.conditioner.batchnorms() and x.dtype == torch.float32)
+
+    def _hip_backward(self, x, gz, gld):
+        """dL/dx and the parameter gradients (in self.parameters() order) of the inverse pass."""
+        x = x.contiguous()
+        B, d = x.shape
+        H = self.conditioner.hidden_dim
+        gz = torch.zeros_like(x) if gz is None else gz.contiguous().float()
+        gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
+        packed = self._packed(x.device, self._build_pack)
+        L = _lib.lib()
+        gx = torch.empty_like(x)
+        fac = torch.empty(L.nfx_made_backward_factor_floats(B, d, H), device=x.device, dtype=torch.float32)
+        _lib.check(L.nfx_made_affine_backward(_lib.ptr(packed), _lib.ptr(x), _lib.ptr(gz), _lib.ptr(gld),
+                                              _lib.ptr(gx), _lib.ptr(fac), B, d, H, _lib.NFX_MAF_INVERSE,
+                                              _lib.stream_of(x)), "nfx_made_affine_backward")
+        o = 0
+
+        def take(rows):
+            nonlocal o
+            t = fac[o:o + rows * B].view(rows, B)
+            o += rows * B
+            return t
+
+        d4, d3, d2, d1 = take(2 * d), take(H), take(H), take(H)
+        h3, h2, h1, x1 = take(H + 1), take(H + 1), take(H + 1), take(d + 1)
+        lins = self.conditioner.linears()
+        grads = {}
+        for lin, dl, act in zip(lins, (d1, d2, d3, d4), (x1, h1, h2, h3)):
+            g = _sample_gemm(dl, act)  # [out, in + 1]: weight gradient | bias gradient
+            grads[lin.weight] = g[:, :-1] * lin.mask.to(g.dtype)
+            if lin.bias is not None:
+                grads[lin.bias] = g[:, -1]
+        return gx, [grads.get(p) for p in self.parameters()]
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
         packed = self._packed(x.device, self._build_pack)

@@ -75,6 +75,12 @@ class HipFlowFunction(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         layer = ctx.layer
         params = [p for p in layer.parameters()]
+        if getattr(layer, "_hip_backward_ok", None) is not None and layer._hip_backward_ok(x, ctx.direction):
+            # fused gfx950 backward (MAF density direction); parameter grads as plain GEMMs
+            STATS["hip"] += 1
+            gx, gparams = layer._hip_backward(x.detach(), gy, gld)
+            gparams = [g if p.requires_grad else None for p, g in zip(params, gparams)]
+            return (None, None, gx, *gparams)
         with torch.enable_grad():
             xr = x.detach().requires_grad_(True)
             y, ld = layer._torch_call(xr, ctx.direction)
