@@ -84,6 +84,11 @@ def build(config):
         f = 2 * (d * H + 2 * H * H + 2 * d * H)
         import oracle
         return m, d, f, oracle.maf_spec(5), "cfg4 5x MaskedAutoregressiveFlow(63, 64) log_prob, eval"
+    if config == "cfg4t":
+        m, d, f, spec, _ = build("cfg4")
+        # training step: forward recompute + data-gradient chain in the fused backward kernel
+        return m, d, 2 * f, spec, "cfg4t 5x MaskedAutoregressiveFlow(63, 64) training step " \
+                                  "(-log_prob mean, fused backward, Adam), train mode"
     if config in ("cfg5f", "cfg5i"):
         torch.manual_seed(40)
         m = nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)])
@@ -100,7 +105,8 @@ def build(config):
     raise ValueError(config)
 
 # per-GPU batch of each config (weak scaling unit)
-DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 500_000, "cfg5f": 524_288, "cfg5i": 8_192}
+DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 500_000, "cfg4t": 500_000, "cfg5f": 524_288,
+                 "cfg5i": 8_192}
 
 
 def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=262144):
@@ -134,12 +140,41 @@ def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=2621
         (None if forward else oracle.nll_f64(lp)), x
 
 
+def cpu_training_baseline(model, spec, x_gpu, budget_s=12.0, max_rows=32768):
+    """One training step of the oracle on this host: autograd through oracle/flows_ref.py."""
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    n = min(x_gpu.shape[0], max_rows)
+    x = x_gpu[:n].detach().float().cpu()
+    sd = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point()) for k, v in model.state_dict().items()}
+    times = []
+
+    def run():
+        for v in sd.values():
+            v.grad = None
+        z, ld = oracle.flow_model(sd, spec, x, -1)
+        (-oracle.gauss_log_prob(z, ld).mean()).backward()
+
+    with torch.enable_grad():
+        run()
+        t_end = time.perf_counter() + budget_s
+        while len(times) < 5 and (time.perf_counter() < t_end or len(times) < 2):
+            t0 = time.perf_counter()
+            run()
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} rows, loss + backward via autograd through oracle/flows_ref.py "
+                      f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5f", "cfg5i"])
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i"])
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -158,7 +193,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     model, d, f_layer, spec, desc = build(a.config)
-    model = model.to(dev).eval()
+    training = a.config == "cfg4t"
+    model = model.to(dev).train(training)
     from nfs_amd.distributed import broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
     B_unit = a.batch or DEFAULT_BATCH[a.config]
@@ -173,10 +209,30 @@ def main():
     flow = model.flow if hasattr(model, "flow") else model
 
     graphed = None
-    if a.graph:
+    if a.graph and not training:
         graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-5) if training else None
+    params = [p for p in model.parameters()]
 
     def step():
+        if training:
+            # data-parallel training step: HIP forward, fused HIP backward, one bucketed RCCL
+            # all-reduce of the flat gradient (412 KB at cfg4), Adam
+            opt.zero_grad(set_to_none=True)
+            logp = flow.log_prob(x)
+            loss = -logp.mean()
+            loss.backward()
+            if world > 1:
+                flat = torch.cat([p.grad.reshape(-1) for p in params])
+                dist.all_reduce(flat)
+                flat /= world
+                o = 0
+                for p in params:
+                    n = p.numel()
+                    p.grad.copy_(flat[o:o + n].view_as(p))
+                    o += n
+            opt.step()
+            return torch.stack([-loss.detach().double() * B, torch.tensor(float(B), device=dev, dtype=torch.float64)])
         if graphed is not None:
             out = graphed()
             if sampling:
@@ -190,7 +246,8 @@ def main():
             dist.all_reduce(sums)  # RCCL over xGMI: 16 bytes
         return sums
 
-    with torch.no_grad():
+    from nfs_amd.flows import autoregressive as _ar
+    with torch.set_grad_enabled(training):
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
@@ -207,15 +264,23 @@ def main():
         # Kernel durations: the same K steps again with HIP events around every layer launch
         # on the launch stream. Kept out of the headline loop because each event record adds
         # ~5 us of GPU idle between kernels (measured, profiles/).
-        flow.layer_events = []
-        for _ in range(a.steps):
-            if sampling:
-                flow.forward(x)
-            else:
-                flow.log_prob(x, return_sums=True)
-        torch.cuda.synchronize()
-        events = flow.layer_events
-        flow.layer_events = None
+        if training:
+            _ar.BACKWARD_EVENTS = []
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+            events = _ar.BACKWARD_EVENTS
+            _ar.BACKWARD_EVENTS = None
+        else:
+            flow.layer_events = []
+            for _ in range(a.steps):
+                if sampling:
+                    flow.forward(x)
+                else:
+                    flow.log_prob(x, return_sums=True)
+            torch.cuda.synchronize()
+            events = flow.layer_events
+            flow.layer_events = None
     if nfs_amd.STATS["torch"] != 0 or (nfs_amd.STATS["hip"] == 0 and graphed is None):
         raise RuntimeError(f"hot path did not run on the HIP kernels: {nfs_amd.STATS}")
     t_all = torch.tensor([t], device=dev, dtype=torch.float64)
@@ -252,7 +317,8 @@ def main():
             "data": "synthetic: x ~ N(0,1) generated on device (seed 1234+rank); seeded random-init "
                     "weights perturbed N(0, 0.1^2) with non-trivial BatchNorm running stats",
             "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B_global,
-                       "parallelism": f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)",
+                       "parallelism": (f"dp{world} (sample shards, 1 bucketed RCCL all-reduce of the flat gradient per step)"
+                            if training else f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"),
                        "launch": "hip-graph replay" if a.graph else "eager"},
             "nll_f64": nll,
             "roofline": {"bound": "mfma", "pipe": "valu" if a.config == "cfg5i" else "mfma",
@@ -262,7 +328,15 @@ def main():
                          "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs)},
             "cpu_baseline": None,
         }
-        if world == 1 and not a.no_cpu:
+        if training:
+            result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
+            result["nll_f64"] = None
+            result["roofline"]["note"] = ("dominant kernel = the fused backward (forward recompute + "
+                                          "data-gradient chain, 2x the layer's forward flops); the "
+                                          "weight gradients run as batched library GEMMs")
+        if world == 1 and not a.no_cpu and training:
+            result["cpu_baseline"] = cpu_training_baseline(model, spec, x)
+        elif world == 1 and not a.no_cpu:
             rows = {"cfg5f": 16384, "cfg5i": 256}.get(a.config, 262144)
             cb, cpu_nll, xs = cpu_baseline(model, spec, x, forward=sampling, max_rows=rows)
             if not sampling:

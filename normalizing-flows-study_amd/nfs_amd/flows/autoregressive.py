@@ -25,6 +25,9 @@ from .flow import HipFlow
 
 MAX_H = 128
 MAX_D = 4096
+# Profiling hook (bench.py): when set to a list, every fused backward launch appends
+# (name, start, end) HIP events recorded on the launch stream around the kernel.
+BACKWARD_EVENTS = None
 
 
 def made_degrees(input_dim, hidden_dim):
@@ -182,9 +185,16 @@ class _MadeAffineFlow(HipFlow):
         L = _lib.lib()
         gx = torch.empty_like(x)
         fac = torch.empty(L.nfx_made_backward_factor_floats(B, d, H), device=x.device, dtype=torch.float32)
+        ev = BACKWARD_EVENTS
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         _lib.check(L.nfx_made_affine_backward(_lib.ptr(packed), _lib.ptr(x), _lib.ptr(gz), _lib.ptr(gld),
                                               _lib.ptr(gx), _lib.ptr(fac), B, d, H, _lib.NFX_MAF_INVERSE,
                                               _lib.stream_of(x)), "nfx_made_affine_backward")
+        if ev is not None:
+            e1.record()
+            ev.append(("made_bwd_kernel", e0, e1))
         o = 0
 
         def take(rows):
