@@ -195,7 +195,7 @@ def main():
     model, d, f_layer, spec, desc = build(a.config)
     training = a.config == "cfg4t"
     model = model.to(dev).train(training)
-    from nfs_amd.distributed import broadcast_parameters, shard_range
+    from nfs_amd.distributed import average_gradients, broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
     B_unit = a.batch or DEFAULT_BATCH[a.config]
     sampling = a.config == "cfg5f"
@@ -212,7 +212,6 @@ def main():
     if a.graph and not training:
         graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
     opt = torch.optim.Adam(model.parameters(), lr=1e-5) if training else None
-    params = [p for p in model.parameters()]
 
     def step():
         if training:
@@ -222,15 +221,7 @@ def main():
             logp = flow.log_prob(x)
             loss = -logp.mean()
             loss.backward()
-            if world > 1:
-                flat = torch.cat([p.grad.reshape(-1) for p in params])
-                dist.all_reduce(flat)
-                flat /= world
-                o = 0
-                for p in params:
-                    n = p.numel()
-                    p.grad.copy_(flat[o:o + n].view_as(p))
-                    o += n
+            average_gradients(model)
             opt.step()
             return torch.stack([-loss.detach().double() * B, torch.tensor(float(B), device=dev, dtype=torch.float64)])
         if graphed is not None:

@@ -39,3 +39,27 @@ def sharded_nll(model, x_local, group=None, return_log_prob=False):
     s = sums.detach().cpu()
     nll = -(s[0] / s[1]).item() if float(s[1]) > 0 else float("nan")
     return (nll, logp) if return_log_prob else nll
+
+
+def average_gradients(module, group=None):
+    """Data-parallel training exchange: average every parameter gradient over the ranks with
+    ONE bucketed all-reduce of the flattened gradients (412 KB for 5 x MAF(63, 64); a single
+    message is latency-optimal on xGMI at that size). With equal shards and a mean loss per
+    rank this equals the full-batch gradient. Parameters without a gradient are skipped."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    params = [p for p in module.parameters() if p.grad is not None]
+    if not params:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    dist.all_reduce(flat, group=group)
+    flat /= world
+    o = 0
+    for p in params:
+        n = p.numel()
+        p.grad.copy_(flat[o:o + n].view_as(p))
+        o += n
+

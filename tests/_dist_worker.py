@@ -11,7 +11,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import nfs_amd  # noqa: E402
-from nfs_amd.distributed import broadcast_parameters, shard_range, sharded_nll  # noqa: E402
+from nfs_amd.distributed import average_gradients, broadcast_parameters, shard_range, sharded_nll  # noqa: E402
 
 
 def _model(seed, kind):
@@ -44,4 +44,21 @@ def _worker(rank, world, port, kind, n, q):
     finally:
         dist.destroy_process_group()
 
+
+def _train_worker(rank, world, port, kind, n, q):
+    """One data-parallel training step: mean loss on this rank's shard, averaged gradients."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = _model(1000 + rank, kind).train()
+        broadcast_parameters(m, src=0)
+        d = 2 if kind != "maf" else 5
+        x = torch.randn(n, d, generator=torch.Generator().manual_seed(9))
+        a, b = shard_range(n, rank, world)
+        loss = -m.log_prob(x[a:b]).mean()
+        loss.backward()
+        average_gradients(m)
+        q.put((rank, {k: p.grad.numpy().copy() for k, p in m.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
 

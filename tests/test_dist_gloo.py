@@ -10,7 +10,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from nfs_amd.distributed import shard_range
-from _dist_worker import _model, _worker
+from _dist_worker import _model, _train_worker, _worker
 
 
 def _free_port():
@@ -56,3 +56,30 @@ def test_shard_range_balanced_and_contiguous():
                 assert b == c
             sizes = [b - a for a, b in rs]
             assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("kind", ["maf", "spline"])
+def test_data_parallel_gradients_match_full_batch(kind):
+    """Equal shards + mean loss per rank + one averaged-gradient all-reduce == the full-batch
+    gradient of the single-process model (the training exchange of bench.py cfg4t). Models
+    without train-mode BatchNorm only: RealNVP's conditioner BatchNorm normalises with batch
+    statistics, which would need a SyncBN all-reduce per layer."""
+    world, n = 2, 800
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, kind, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m = _model(1000, kind).train()
+    d = 2 if kind != "maf" else 5
+    x = torch.randn(n, d, generator=torch.Generator().manual_seed(9))
+    (-m.log_prob(x).mean()).backward()
+    for k, p in m.named_parameters():
+        for r in range(world):
+            assert torch.allclose(torch.from_numpy(res[r][1][k]), p.grad, rtol=1e-4, atol=1e-6), k
+
