@@ -53,16 +53,20 @@ __global__ void made_bwd_pack_kernel(NfxMlpRaw net, int d, int H, float* packed)
 }
 
 // Feature-major store of one accumulator tile: rows `row0 + crow(r, h)` (< nrows) of a
-// [nrows x B] matrix, columns = the tile's 32 samples (base + col < B).
+// [nrows x B] matrix, columns = the tile's 32 samples (base + col < B). Raw buffer stores: the
+// lane offset carries the sample and the lane half's +4 rows, the row of each register rides in
+// the scalar offset, and the descriptor's range check drops rows >= nrows; lanes past B get an
+// offset outside every range. No per-element branches or 64-bit address math.
 __device__ __forceinline__ void store_fm(float* __restrict__ dst, const f32x16& t, int row0, int nrows, int64_t B,
                                          int64_t base) {
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
-    const int64_t s = base + col;
-    if (s >= B) return;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, (int)(((int64_t)nrows * B - base) * 4),
+                                                      0x00020000);
+    const int vo = base + col < B ? (int)((col + 4 * h * B) * 4) : (int)0xFFFFFFF0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int row = row0 + crow(r, h);
-        if (row < nrows) dst[(int64_t)row * B + s] = t[r];
+        const int rowu = row0 + (r & 3) + 8 * (r >> 2);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * B * 4), 0);
     }
 }
 
@@ -128,21 +132,25 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
             }
         }
         wave_lds_sync();
+        // opaque offsets keep the compiler from hoisting every (loop-invariant) weight read out
+        // of the tile loop into registers
         const float* Wf = W + opaque_zero();
+        const float* Pt = packed + opaque_zero();
         {
             // x and the ones rows, feature-major: half-wave h writes dim row 2i+h of 32 samples
-            const int64_t s = base + col;
-            if (s < B) {
-                for (int i = 0; i < 32; ++i) {
-                    const int dim = 2 * i + h;
-                    if (dim < d) X1[(int64_t)dim * B + s] = xt[col * S + dim];
-                }
-                if (h == 0) {
-                    X1[(int64_t)d * B + s] = 1.f;
-                    H3[(int64_t)H * B + s] = 1.f;
-                    H2[(int64_t)H * B + s] = 1.f;
-                    H1[(int64_t)H * B + s] = 1.f;
-                }
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(X1 + base, 0, (int)(((int64_t)(d + 1) * B - base) * 4),
+                                                              0x00020000);
+            const int vo = base + col < B ? (int)((col + h * B) * 4) : (int)0xFFFFFFF0;
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+                if (2 * i < d)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(2 * i + h < d ? xt[col * S + 2 * i + h] : 1.f), rs,
+                                                          vo, (int)(2 * i * B * 4), 0);
+            if (h == 0 && base + col < B) {
+                if ((d & 1) == 0) X1[(int64_t)d * B + base + col] = 1.f;  // odd d: written above (row 2i+1 = d)
+                H3[(int64_t)H * B + base + col] = 1.f;
+                H2[(int64_t)H * B + base + col] = 1.f;
+                H1[(int64_t)H * B + base + col] = 1.f;
             }
         }
 
@@ -239,8 +247,8 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
         f32x16 g[HT];
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = NJ == 2 ? chain_gmem<4>(packed + L.t4, ot, 4, d4, f32x16{})
-                                 : chain_gmem<2>(packed + L.t4, ot, 2, d4, f32x16{});
+            f32x16 acc = NJ == 2 ? chain_gmem<4>(Pt + L.t4, ot, 4, d4, f32x16{})
+                                 : chain_gmem<2>(Pt + L.t4, ot, 2, d4, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = h3[ot][r] > 0.f ? acc[r] : 0.f;
             g[ot] = acc;
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
         f32x16 g2[HT];
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = chain_gmem<HT>(packed + L.t3, ot, HT, g, f32x16{});
+            f32x16 acc = chain_gmem<HT>(Pt + L.t3, ot, HT, g, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = h2[ot][r] > 0.f ? acc[r] : 0.f;
             g2[ot] = acc;
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
         }
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = chain_gmem<HT>(packed + L.t2, ot, HT, g2, f32x16{});
+            f32x16 acc = chain_gmem<HT>(Pt + L.t2, ot, HT, g2, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = h1[ot][r] > 0.f ? acc[r] : 0.f;
             g[ot] = acc;
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
             if (ot < NKC) {
-                const f32x16 gx = chain_gmem<HT>(packed + L.t1, ot, HT, g, f32x16{});
+                const f32x16 gx = chain_gmem<HT>(Pt + L.t1, ot, HT, g, f32x16{});
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     float* px = xt + col * S + 32 * ot + crow(r, h);
