@@ -70,6 +70,18 @@ __device__ __forceinline__ void store_fm(float* __restrict__ dst, const f32x16& 
     }
 }
 
+// ReLU-backward masks of HT accumulator tiles as bits (tile ot, register r -> bit ot*16 + r):
+// the backward needs only (h > 0), so the activations can be written out and die early.
+template <int HT>
+__device__ __forceinline__ uint32_t relu_bits(const f32x16 (&t)[HT]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int ot = 0; ot < HT; ++ot)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m |= (t[ot][r] > 0.f ? 1u : 0u) << (ot * 16 + r);
+    return m;
+}
+
 // A-operand (weights) x B-operand (accumulator-layout tiles) chain over NK k tiles, A from
 // global/L2 in [out tile][k tile][r/4][lane][r%4] order.
 template <int NK>
@@ -88,8 +100,10 @@ __device__ __forceinline__ f32x16 chain_gmem(const float* __restrict__ A, int ot
     return acc;
 }
 
+constexpr int kBwdWaves = 8;  // 2 per SIMD; weights are read from L2, LDS holds the tiles
+
 template <int HT>
-__global__ __launch_bounds__(256) void made_bwd_kernel(
+__global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, const float* __restrict__ gout,
     const float* __restrict__ gld_in, float* __restrict__ gin, float* __restrict__ acts, int64_t B, int d,
     int H, int64_t ntiles) {
@@ -98,11 +112,9 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int i = threadIdx.x; i < L.par_total / 4; i += 256) lds4[i] = reinterpret_cast<const f32x4*>(packed)[i];
-    float* xt = lds + L.par_total + wave * 2 * 32 * S;  // x tile, then gz tile
+    float* xt = lds + wave * 2 * 32 * S;  // x tile, then gz tile
     float* gt = xt + 32 * S;
-    __syncthreads();
-    const float* W = lds;
+    const float* W = packed;
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
     const int voff = lane < d ? lane * 4 : (1 << 30);
     const int rowb = d * 4;
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
     float* H1 = H2 + (int64_t)(H + 1) * B;
     float* X1 = H1 + (int64_t)(H + 1) * B;
 
-    for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    for (int64_t t = (int64_t)blockIdx.x * kBwdWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kBwdWaves) {
         const int64_t base = t * 32;
         const int rows = (int)(B - base < 32 ? B - base : 32);
         {
@@ -174,7 +186,13 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
         made_hidden1<HT>(Wf, L.w2, L.b2, h1, h2);
+        const uint32_t m1 = relu_bits<HT>(h1);
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) store_fm(H1, h1[ht], 32 * ht, H, B, base);
         made_hidden1<HT>(Wf, L.w3, L.b3, h2, h3);
+        const uint32_t m2 = relu_bits<HT>(h2);
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) store_fm(H2, h2[ht], 32 * ht, H, B, base);
 
         // layer 4 for every output block (kept for the log-det sum), then the epilogue backward.
         // d4[j*2 + 0] = mu / δmu rows of block j, d4[j*2 + 1] = alpha / δalpha rows (t4 k order).
@@ -205,6 +223,10 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
                 d4[2 * j] = d4[2 * j + 1] = f32x16{};
             }
         }
+        const uint32_t m3 = relu_bits<HT>(h3);
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) store_fm(H3, h3[ht], 32 * ht, H, B, base);
+
         // ld_raw = -sum_i clamp(alpha_i, -3, 3) of the lane's sample, summed in the forward
         // kernel's order (rows past d: alpha = 0)
         float asum0 = 0.f;
@@ -250,7 +272,7 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
             f32x16 acc = NJ == 2 ? chain_gmem<4>(Pt + L.t4, ot, 4, d4, f32x16{})
                                  : chain_gmem<2>(Pt + L.t4, ot, 2, d4, f32x16{});
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = h3[ot][r] > 0.f ? acc[r] : 0.f;
+            for (int r = 0; r < 16; ++r) acc[r] = ((m3 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g[ot] = acc;
         }
 #pragma unroll
@@ -263,32 +285,29 @@ __global__ __launch_bounds__(256) void made_bwd_kernel(
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
             store_fm(D3, g[ht], 32 * ht, H, B, base);
-            store_fm(H3, h3[ht], 32 * ht, H, B, base);
         }
         f32x16 g2[HT];
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
             f32x16 acc = chain_gmem<HT>(Pt + L.t3, ot, HT, g, f32x16{});
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = h2[ot][r] > 0.f ? acc[r] : 0.f;
+            for (int r = 0; r < 16; ++r) acc[r] = ((m2 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g2[ot] = acc;
         }
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
             store_fm(D2, g2[ht], 32 * ht, H, B, base);
-            store_fm(H2, h2[ht], 32 * ht, H, B, base);
         }
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
             f32x16 acc = chain_gmem<HT>(Pt + L.t2, ot, HT, g2, f32x16{});
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = h1[ot][r] > 0.f ? acc[r] : 0.f;
+            for (int r = 0; r < 16; ++r) acc[r] = ((m1 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g[ot] = acc;
         }
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
             store_fm(D1, g[ht], 32 * ht, H, B, base);
-            store_fm(H1, h1[ht], 32 * ht, H, B, base);
         }
         // gx = direct term (in the tile) + W1mᵀ δ1, accumulator layout rows = dims
         wave_lds_sync();
@@ -349,16 +368,17 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
         return set_error(NFX_EINVAL, "made_affine_backward: null pointer");
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
-    const size_t lds = ((size_t)L.par_total + 4 * 2 * 32 * kTileStride) * sizeof(float);
+    const size_t lds = (size_t)kBwdWaves * 2 * 32 * kTileStride * sizeof(float);
     const void* k = HT == 1 ? (const void*)made_bwd_kernel<1> : (const void*)made_bwd_kernel<2>;
     int rc = prepare_lds(k, lds);
     if (rc) return rc;
     const int64_t ntiles = (B + 31) / 32;
-    const int grid = resident_grid(k, 256, lds, (ntiles + 3) / 4);
+    const int threads = 64 * kBwdWaves;
+    const int grid = resident_grid(k, threads, lds, (ntiles + kBwdWaves - 1) / kBwdWaves);
     hipStream_t s = (hipStream_t)stream;
     if (HT == 1)
-        made_bwd_kernel<1><<<grid, 256, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
+        made_bwd_kernel<1><<<grid, threads, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
     else
-        made_bwd_kernel<2><<<grid, 256, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
+        made_bwd_kernel<2><<<grid, threads, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
     return check_launch("made_bwd_kernel");
 }
