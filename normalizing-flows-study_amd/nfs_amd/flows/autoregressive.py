@@ -116,7 +116,7 @@ class MADE(nn.Module):
         return [m for m in self.net if isinstance(m, nn.BatchNorm1d)]
 
 
-def _sample_gemm(a, b, chunk=8192):
+def _sample_gemm(a, b, chunk=4096):
     """a [M, B] · b [N, B]ᵀ for a long sample dimension B: split-K as one strided-batched GEMM
     over B // chunk contiguous sample chunks (a library GEMM picks one tile column for such
     shapes and leaves most CUs idle), plus the remainder, reduced over the chunks."""
