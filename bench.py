@@ -84,6 +84,15 @@ def build(config):
         f = 2 * (d * H + 2 * H * H + 2 * d * H)
         import oracle
         return m, d, f, oracle.maf_spec(5), "cfg4 5x MaskedAutoregressiveFlow(63, 64) log_prob, eval"
+    if config == "sample4k":
+        torch.manual_seed(3)
+        m = nfs_amd.RealNVP(2, 10, 128)
+        perturb(m, 0.1, 4)
+        H = 128
+        f = 2 * 2 * (1 * H + H * H + H * 1)
+        import oracle
+        return m, 2, f, oracle.realnvp_spec(10), \
+            "sample4k RealNVP(2,10,128) sampling: model.forward(z), n=4000 per call (plots/_common.py:264-274)"
     if config == "cfg4t":
         m, d, f, spec, _ = build("cfg4")
         # training step: forward recompute + data-gradient chain in the fused backward kernel
@@ -106,7 +115,10 @@ def build(config):
 
 # per-GPU batch of each config (weak scaling unit)
 DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 500_000, "cfg4t": 500_000, "cfg5f": 524_288,
-                 "cfg5i": 8_192}
+                 "cfg5i": 8_192, "sample4k": 4_000}
+# The reference's only published throughput (assets/benchmark.png via
+# plots/_common.py:264-274): RealNVP(2,10,128) sampling, model.forward(z) on n = 4,000, CPU.
+PUBLISHED_SAMPLE4K = 186_000.0
 
 
 def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=262144):
@@ -174,7 +186,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i"])
+    ap.add_argument("--config", default="cfg2",
+                    choices=["cfg2", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k"])
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -198,7 +211,7 @@ def main():
     from nfs_amd.distributed import average_gradients, broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
     B_unit = a.batch or DEFAULT_BATCH[a.config]
-    sampling = a.config == "cfg5f"
+    sampling = a.config in ("cfg5f", "sample4k")
     if a.strong:
         lo, hi = shard_range(B_unit, rank, world)
         B, B_global = hi - lo, B_unit
@@ -319,6 +332,10 @@ def main():
                          "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs)},
             "cpu_baseline": None,
         }
+        if a.config == "sample4k":
+            result["metric"] = "sampling samples/sec (RealNVP(2,10,128), n=4000 per forward call)"
+            result["vs_baseline"] = result["value"] / PUBLISHED_SAMPLE4K
+            result["nll_f64"] = None
         if training:
             result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
             result["nll_f64"] = None
@@ -328,7 +345,7 @@ def main():
         if world == 1 and not a.no_cpu and training:
             result["cpu_baseline"] = cpu_training_baseline(model, spec, x)
         elif world == 1 and not a.no_cpu:
-            rows = {"cfg5f": 16384, "cfg5i": 256}.get(a.config, 262144)
+            rows = {"cfg5f": 16384, "cfg5i": 256, "sample4k": 4000}.get(a.config, 262144)
             cb, cpu_nll, xs = cpu_baseline(model, spec, x, forward=sampling, max_rows=rows)
             if not sampling:
                 gpu_nll = flow.nll(xs.to(dev))
