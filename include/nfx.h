@@ -89,6 +89,16 @@ int nfx_affine_coupling(const float* packed, const float* in, float* out, float*
 int nfx_affine_coupling_logprob(const float* packed, const float* in, float* out, float* log_det,
                                 float* logp, double* sums, void* workspace, int64_t B, int d,
                                 int H, int accumulate, void* stream);
+/* Which affine-coupling kernel runs: the streaming one (a wave per 64-sample chunk, weights
+ * in LDS) or the small-batch one (a workgroup per 32 samples, the conditioner split across
+ * 2*HT waves). Both compute the same function (output-layer sums associated differently,
+ * within fp32 rounding). NFX_AFFINE_AUTO (default, or $NFX_AFFINE_POLICY) picks by an
+ * occupancy cost model. policy >= 0 sets it and returns the previous policy; a negative value
+ * only reads it. Process-wide; host-only (no GPU call). */
+#define NFX_AFFINE_AUTO 0
+#define NFX_AFFINE_STREAMING 1
+#define NFX_AFFINE_SMALL 2
+int nfx_affine_kernel_policy(int policy);
 
 /* ---------------------------------------------------------------------------------------
  * Rational-quadratic spline coupling — SplineCouplingLayer

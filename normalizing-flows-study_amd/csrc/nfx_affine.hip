@@ -16,11 +16,18 @@
 // Work decomposition: a wave owns 64-sample chunks (two 32-sample MFMA column tiles);
 // after the output layer lane l holds sample (chunk*64 + l) for the epilogue, so x/y/log_det
 // accesses are fully coalesced. Waves grid-stride over chunks so the LDS weight image is
-// loaded once per workgroup.
+// loaded once per workgroup. Small batches go to the latency-oriented variant in
+// nfx_affine_small_kernel.h instead (see affine_policy).
+#include <atomic>
+#include <climits>
+#include <cstdlib>
+
 #include "nfx_affine_kernel.h"
+#include "nfx_affine_small_kernel.h"
 #include "nfx_pack.h"
 
 namespace nfx {
+
 
 __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float* mask, int d,
                                    int H, float* packed) {
@@ -75,6 +82,29 @@ static affine_kernel_t pick_affine(int HT, int d, int dir, bool logp) {
     }
 }
 
+static affine_kernel_t pick_affine_small(int HT, int d, int dir, bool logp) {
+    switch (HT) {
+        case 1: return affine_small_pick_ht<1>(d, dir, logp);
+        case 2: return affine_small_pick_ht<2>(d, dir, logp);
+        case 3: return affine_small_pick_ht<3>(d, dir, logp);
+        case 4: return affine_small_pick_ht<4>(d, dir, logp);
+        default: return nullptr;
+    }
+}
+
+// Kernel choice (nfx_affine_kernel_policy). AUTO compares MFMA "rounds": the streaming kernel
+// runs ceil(chunks / resident waves) 64-sample chunks per wave, each a chain of ~2*HT times the
+// MFMAs of one small-kernel 32-sample tile, of which the small kernel runs ceil(tiles /
+// resident workgroups) per workgroup. (Measured at RealNVP H=128: small 8 us vs streaming 37 us
+// per layer up to 8k samples, break-even near 64k.) Initial policy: $NFX_AFFINE_POLICY or AUTO.
+static std::atomic<int>& affine_policy() {
+    static std::atomic<int> v{[] {
+        const char* e = getenv("NFX_AFFINE_POLICY");
+        return e ? atoi(e) : NFX_AFFINE_AUTO;
+    }()};
+    return v;
+}
+
 static int affine_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
                          int d, int H, int direction, int accumulate, float* logp, double* sums,
                          void* workspace, hipStream_t stream) {
@@ -92,10 +122,29 @@ static int affine_launch(const float* packed, const float* in, float* out, float
     const size_t lds = (size_t)affine_layout(d, HT).total * sizeof(float);
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
+    double* partials = reinterpret_cast<double*>(workspace);
     const int64_t nchunks = (B + 63) / 64;
+    const int64_t ntiles = (B + 31) / 32;
+    const int policy = affine_policy().load(std::memory_order_relaxed);
+    affine_kernel_t ks = pick_affine_small(HT, d, direction, fused);
+    int grid_small = resident_grid((const void*)ks, 128 * HT, 0, ntiles);
+    bool small = policy == NFX_AFFINE_SMALL;
+    if (policy == NFX_AFFINE_AUTO) {
+        const int64_t waves = 4 * (int64_t)resident_grid((const void*)k, 256, lds, INT64_MAX);
+        const int64_t rounds_stream = (nchunks + waves - 1) / waves;
+        const int64_t rounds_small = (ntiles + grid_small - 1) / grid_small;
+        small = rounds_small < 2 * HT * rounds_stream;
+    }
+    if (small) {
+        if (grid_small > kMaxPartials) grid_small = kMaxPartials;
+        ks<<<grid_small, 128 * HT, 0, stream>>>(packed, in, out, log_det, B, accumulate, ntiles, logp,
+                                                partials, gauss_const(d));
+        rc = check_launch("affine_small_kernel");
+        if (rc || !fused) return rc;
+        return gauss_finish(partials, grid_small, sums, B, stream);
+    }
     int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
     if (grid > kMaxPartials) grid = kMaxPartials;
-    double* partials = reinterpret_cast<double*>(workspace);
     k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, accumulate, nchunks, logp, partials, gauss_const(d));
     rc = check_launch("affine_coupling_kernel");
     if (rc || !fused) return rc;
@@ -152,6 +201,12 @@ extern "C" int nfx_affine_coupling(const float* packed, const float* in, float* 
                                    void* stream) {
     return affine_launch(packed, in, out, log_det, B, d, H, direction, accumulate, nullptr, nullptr,
                          nullptr, (hipStream_t)stream);
+}
+
+extern "C" int nfx_affine_kernel_policy(int policy) {
+    if (policy < 0) return affine_policy().load();
+    if (policy > NFX_AFFINE_SMALL) return set_error(NFX_EINVAL, "affine_kernel_policy: unknown policy %d", policy);
+    return affine_policy().exchange(policy);
 }
 
 extern "C" int nfx_affine_coupling_logprob(const float* packed, const float* in, float* out,

@@ -22,11 +22,15 @@ NFX_MAF_INVERSE = 0
 NFX_IAF_FORWARD = 1
 NFX_MAF_FORWARD = 2
 NFX_IAF_INVERSE = 3
+NFX_AFFINE_AUTO = 0
+NFX_AFFINE_STREAMING = 1
+NFX_AFFINE_SMALL = 2
 
 # Every symbol include/nfx.h declares (tests check the built library exports all of them).
 EXPORTED_SYMBOLS = (
     "nfx_abi_version", "nfx_last_error",
     "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
+    "nfx_affine_kernel_policy",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
     "nfx_rqs_unit",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
@@ -71,6 +75,7 @@ _SIGNATURES = {
     "nfx_affine_pack": (_int, [ctypes.POINTER(NfxMlpRaw), ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _vp, _vp]),
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_affine_kernel_policy": (_int, [_int]),
     "nfx_spline_packed_floats": (_sz, [_int, _int, _int]),
     "nfx_spline_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _int, _vp, _vp]),
     "nfx_spline_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _f,

@@ -61,3 +61,15 @@ def test_product_raises_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(_lib.NfxLibraryError):
         _lib.load(str(tmp_path / "missing.so"))
+
+
+def test_affine_kernel_policy_roundtrip():
+    """Host-only entry point: set/read the affine kernel policy (no GPU call)."""
+    f = _lib.load().nfx_affine_kernel_policy
+    prev = f(-1)
+    assert prev in (_lib.NFX_AFFINE_AUTO, _lib.NFX_AFFINE_STREAMING, _lib.NFX_AFFINE_SMALL)
+    assert f(_lib.NFX_AFFINE_SMALL) == prev
+    assert f(-1) == _lib.NFX_AFFINE_SMALL
+    assert f(7) == _lib.NFX_EINVAL
+    assert f(prev) == _lib.NFX_AFFINE_SMALL
+    assert f(-1) == prev

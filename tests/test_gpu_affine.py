@@ -2,6 +2,8 @@
 
 Checks against (a) the reference's own outputs (golden fixtures, tests/golden/) and (b) the CPU
 oracle on the same seeded inputs, including ragged batches, B=0 and non-finite inputs.
+Both kernels are exercised: the small-batch one (a workgroup per 32 samples) and the
+streaming one, forced through nfx_affine_kernel_policy by the `affine_kernel` fixture.
 Tolerances (SURVEY §8(c)): per-sample z/x |d| <= 1e-5 * (1 + |ref|); log-det <= 1e-4 (d=2);
 NLL <= 1e-5 absolute.
 """
@@ -34,6 +36,15 @@ def assert_lp(lp, ref):
     assert not bad.any(), f"log_prob mismatch at {np.flatnonzero(bad)[:5]}: {lp[bad][:5]} vs {ref[bad][:5]}"
 
 
+@pytest.fixture(params=["small", "streaming"])
+def affine_kernel(request):
+    """Route every affine-coupling launch of the test to one kernel, restore afterwards."""
+    L = nfs_amd._lib
+    prev = L.lib().nfx_affine_kernel_policy(L.NFX_AFFINE_SMALL if request.param == "small" else L.NFX_AFFINE_STREAMING)
+    yield request.param
+    L.lib().nfx_affine_kernel_policy(prev)
+
+
 N_REGULAR = 4048  # g2/g3 rows before the 45 edge rows (|x| up to 1e10)
 
 
@@ -44,7 +55,7 @@ def realnvp_from_golden(dev, name="g2_realnvp.npz"):
     return m.to(dev).eval(), g
 
 
-def test_layer0_inverse_forward(cuda_device):
+def test_layer0_inverse_forward(cuda_device, affine_kernel):
     m, g = realnvp_from_golden(cuda_device)
     layer = m.flow.flows[0]
     nfs_amd.reset_stats()
@@ -58,7 +69,7 @@ def test_layer0_inverse_forward(cuda_device):
     assert_ld(ldf.cpu(), g["l0_fwd_ld"])
 
 
-def test_realnvp_model_vs_reference(cuda_device):
+def test_realnvp_model_vs_reference(cuda_device, affine_kernel):
     m, g = realnvp_from_golden(cuda_device)
     x = torch.from_numpy(g["x"]).to(cuda_device)
     z = torch.from_numpy(g["z"]).to(cuda_device)
@@ -78,7 +89,7 @@ def test_realnvp_model_vs_reference(cuda_device):
     assert abs(nll - (-g["log_prob"][:N_REGULAR].astype(np.float64).mean())) <= 1e-5
 
 
-def test_moons_config1(cuda_device):
+def test_moons_config1(cuda_device, affine_kernel):
     """Config 1 (two-moons 5k, trained RealNVP) log_prob / NLL vs the reference."""
     m, g = realnvp_from_golden(cuda_device, "g7_moons.npz")
     with torch.no_grad():
@@ -88,7 +99,7 @@ def test_moons_config1(cuda_device):
 
 
 @pytest.mark.parametrize("name", ["cpl_alt", "cpl_half", "cpl_d3", "cpl_d1"])
-def test_small_coupling_layers(cuda_device, name):
+def test_small_coupling_layers(cuda_device, affine_kernel, name):
     """d in {1,3,4}, H=16 (padded to one 32-row MFMA tile) as in the reference's own tests."""
     g = load_golden("g9_small.npz")
     sd = oracle_sd(g, name + ".")
@@ -107,7 +118,7 @@ def test_small_coupling_layers(cuda_device, name):
 
 
 @pytest.mark.parametrize("B", [1, 31, 63, 64, 65, 1000, 4097])
-def test_ragged_batches_vs_oracle(cuda_device, B):
+def test_ragged_batches_vs_oracle(cuda_device, affine_kernel, B):
     m, _ = realnvp_from_golden(cuda_device)
     x = torch.randn(B, 2, generator=torch.Generator().manual_seed(B)) * 1.5
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
@@ -122,7 +133,7 @@ def test_ragged_batches_vs_oracle(cuda_device, B):
     assert_ld(ldf.cpu(), lfr)
 
 
-def test_empty_batch(cuda_device):
+def test_empty_batch(cuda_device, affine_kernel):
     m, _ = realnvp_from_golden(cuda_device)
     with torch.no_grad():
         z, ld = m.inverse(torch.empty(0, 2, device=cuda_device))
@@ -131,7 +142,7 @@ def test_empty_batch(cuda_device):
     assert float(sums[1]) == 0.0
 
 
-def test_nonfinite_inputs_follow_reference_guards(cuda_device):
+def test_nonfinite_inputs_follow_reference_guards(cuda_device, affine_kernel):
     """inf/NaN inputs: the reference's clamp (NaN-propagating), 0*inf=NaN masking and the
     NaN/Inf -> 0 guards must come out identical (single layer, so no float drift)."""
     m, _ = realnvp_from_golden(cuda_device)
@@ -191,3 +202,30 @@ def test_full_scale_nll_cfg2(cuda_device):
     m, _ = realnvp_from_golden(cuda_device)
     nll = m.nll(x.to(cuda_device))
     assert abs(nll - meta["nll_f64"]) <= 1e-5, (nll, meta["nll_f64"])
+
+
+@pytest.mark.parametrize("d,H,B", [(2, 64, 4000), (2, 128, 777), (3, 96, 1000), (8, 32, 513), (1, 16, 65)])
+def test_small_and_streaming_kernels_agree(cuda_device, d, H, B):
+    """Both kernels compute the same layer: equal up to the output-layer summation order."""
+    torch.manual_seed(d * 1000 + H)
+    mask = torch.zeros(d)
+    mask[::2] = 1
+    layer = nfs_amd.CouplingLayer(d, H, mask)
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(0.1 * torch.randn(p.shape))
+    layer = layer.to(cuda_device).eval()
+    x = torch.randn(B, d, device=cuda_device)
+    L = nfs_amd._lib
+    f = L.lib().nfx_affine_kernel_policy
+    prev = f(-1)
+    out = {}
+    try:
+        for name, pol in (("small", L.NFX_AFFINE_SMALL), ("streaming", L.NFX_AFFINE_STREAMING)):
+            f(pol)
+            with torch.no_grad():
+                out[name] = layer.forward(x) + layer.inverse(x)
+    finally:
+        f(prev)
+    for a, b in zip(out["small"], out["streaming"]):
+        assert ((a - b).abs() <= 2e-6 * (1 + b.abs())).all(), (a - b).abs().max().item()
