@@ -134,6 +134,22 @@ int nfx_rqs_unit(const float* in, const float* widths, const float* heights,
                  void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * ARQS — autoregressive unit-interval RQ spline flow (src/flows/spline/arqs.py:7-114):
+ * forward replaces arqs.py:44-80, inverse replaces arqs.py:82-114. One launch runs the
+ * reference's d sequential steps (MADE on the partial output vector, view(B, d, 3K-1) row i,
+ * rational_quadratic_spline of column i). made: the conditioner MADE(d, H, 3K-1) — its four
+ * MaskedLinear layers with masks (and eval BatchNorm when use_batch_norm). H <= 128,
+ * 2 <= K <= 11. rescale: 0 = data_min/data_max None; 1 = scalar rescale (x - data_min) /
+ * (data_max - data_min) in fp32 with fp32(data_max - data_min) from the double difference.
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_arqs_packed_floats(int d, int H, int K);
+int nfx_arqs_pack(const NfxMlpRaw* made, int d, int H, int K, float* packed, void* stream);
+int nfx_arqs(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d,
+             int H, int K, float min_bin_width, float min_bin_height, float min_derivative,
+             int rescale, double data_min, double data_max, int direction, int accumulate,
+             void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * MADE-masked autoregressive affine flows — MADE (src/flows/autoregressive/made.py:6-140),
  * MaskedLinear (masked_linear.py:4-18), MaskedAutoregressiveFlow
  * (masked_autoregressive_flow.py:18-78), InverseAutoregressiveFlow

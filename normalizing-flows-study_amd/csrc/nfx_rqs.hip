@@ -7,7 +7,7 @@
 //
 // One thread per input; the N x (3K-1) parameter rows are read once (HBM-bound:
 // (3K+2)*4 bytes per element at K bins).
-#include "nfx_common.h"
+#include "nfx_rqs_unit.h"
 
 namespace nfx {
 
@@ -16,90 +16,17 @@ __global__ __launch_bounds__(256) void rqs_unit_kernel(
     const float* __restrict__ in, const float* __restrict__ uw, const float* __restrict__ uh,
     const float* __restrict__ ud, float* __restrict__ out, float* __restrict__ logdet, int64_t N,
     float min_w, float cw, float min_h, float ch, float min_d) {
-#pragma clang fp contract(off)
-    const float eps = 1e-6f;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N; i += (int64_t)gridDim.x * 256) {
-        const float x = in[i];
-        float w[K], h[K], xk[K + 1], yk[K + 1], dv[K + 1];
-        float mw = uw[i * K], mh = uh[i * K];
+        float w[K], h[K], dv[K - 1];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             w[k] = uw[i * K + k];
             h[k] = uh[i * K + k];
-            mw = tmax(mw, w[k]);
-            mh = tmax(mh, h[k]);
         }
-        float sw = 0.f, sh = 0.f;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            w[k] = expf(w[k] - mw);
-            sw = sw + w[k];
-            h[k] = expf(h[k] - mh);
-            sh = sh + h[k];
-        }
-        const float iw = 1.f / sw, ih = 1.f / sh;
-        double aw = 0.0, ah = 0.0;
-        xk[0] = 0.f;
-        yk[0] = 0.f;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            w[k] = tclamp_min(min_w + cw * (w[k] * iw), eps);
-            h[k] = tclamp_min(min_h + ch * (h[k] * ih), eps);
-            aw += (double)w[k];  // ATen CPU cumsum: float accumulated in double (:36-37)
-            ah += (double)h[k];
-            xk[k + 1] = (float)aw;
-            yk[k + 1] = (float)ah;
-        }
-        dv[0] = 1.f;
-        dv[K] = 1.f;
-#pragma unroll
-        for (int k = 0; k < K - 1; ++k) {
-            const float u = ud[i * (K - 1) + k];
-            const float sp = u > 20.f ? u : log1pf(expf(u));
-            dv[k + 1] = tclamp_min(sp + min_d, eps);
-        }
-        int cnt = 0;
-#pragma unroll
-        for (int k = 0; k <= K; ++k) cnt += ((INV ? yk[k] : xk[k]) <= x) ? 1 : 0;
-        int bin = cnt - 1;
-        bin = bin < 0 ? 0 : (bin > K - 1 ? K - 1 : bin);
-        float w_k = w[0], x_k = xk[0], h_k = h[0], y_k = yk[0], d_k = dv[0], d_k1 = dv[1];
-#pragma unroll
-        for (int k = 1; k < K; ++k) {
-            const bool s = (k == bin);
-            w_k = s ? w[k] : w_k;
-            x_k = s ? xk[k] : x_k;
-            h_k = s ? h[k] : h_k;
-            y_k = s ? yk[k] : y_k;
-            d_k = s ? dv[k] : d_k;
-            d_k1 = s ? dv[k + 1] : d_k1;
-        }
-        const float s_k = h_k / tclamp_min(w_k, eps);
+        for (int k = 0; k < K - 1; ++k) dv[k] = ud[i * (K - 1) + k];
         float o, l;
-        if constexpr (INV) {
-            const float dy = x - y_k;
-            const float t1 = dy * (d_k + d_k1 - 2.f * s_k);
-            const float a = h_k * (s_k - d_k) + t1;
-            const float b = h_k * d_k - t1;
-            const float c = -s_k * dy;
-            const float disc = tclamp_min(b * b - 4.f * a * c, 0.f);
-            const float th = tclamp((2.f * c) / (-b - sqrtf(disc)), 0.f, 1.f);
-            o = th * w_k + x_k;
-            const float tt = th * (1.f - th);
-            const float om = 1.f - th;
-            const float nom = (s_k * s_k) * (d_k1 * (th * th) + 2.f * s_k * tt + d_k * (om * om));
-            const float dd = s_k + (d_k + d_k1 - 2.f * s_k) * tt;
-            l = -logf(tclamp_min(nom / tclamp_min(dd * dd, eps), eps));
-        } else {
-            const float th = tclamp((x - x_k) / tclamp_min(w_k, eps), 0.f, 1.f);
-            const float tt = th * (1.f - th);
-            const float om = 1.f - th;
-            const float nom = h_k * (s_k * (th * th) + d_k * tt);
-            const float den = s_k + (d_k + d_k1 - 2.f * s_k) * tt;
-            o = y_k + nom / tclamp_min(den, eps);
-            const float nd = (s_k * s_k) * (d_k1 * (th * th) + 2.f * s_k * tt + d_k * (om * om));
-            l = logf(tclamp_min(nd / tclamp_min(den * den, eps), eps));
-        }
+        rqs_unit_eval<K, INV>(in[i], w, h, dv, min_w, cw, min_h, ch, min_d, o, l);
         out[i] = o;
         logdet[i] = l;
     }

@@ -5,12 +5,12 @@ src/models/*), backed by hand-written HIP kernels in libnfx.so (C-ABI: include/n
 """
 from . import _lib
 from .flows import (Flow, SequentialFlow, CouplingLayer, SplineCouplingLayer,
-                    rational_quadratic_spline, MaskedLinear, MADE, MaskedAutoregressiveFlow,
+                    rational_quadratic_spline, ARQS, MaskedLinear, MADE, MaskedAutoregressiveFlow,
                     InverseAutoregressiveFlow, made_degrees, STATS, reset_stats)
 from .models import NormalizingFlowModel, RealNVP, RealNVPSpline, gauss_logprob
 from .graphs import GraphedFlow
 
 __all__ = ["Flow", "SequentialFlow", "CouplingLayer", "SplineCouplingLayer",
-           "rational_quadratic_spline", "MaskedLinear", "MADE", "MaskedAutoregressiveFlow",
+           "rational_quadratic_spline", "ARQS", "MaskedLinear", "MADE", "MaskedAutoregressiveFlow",
            "InverseAutoregressiveFlow", "NormalizingFlowModel", "RealNVP", "RealNVPSpline",
            "gauss_logprob", "made_degrees", "STATS", "reset_stats", "GraphedFlow"]

@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "nfx_affine_kernel_policy",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
     "nfx_rqs_unit",
+    "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
     "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_affine_backward",
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob",
@@ -76,6 +77,10 @@ _SIGNATURES = {
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_affine_kernel_policy": (_int, [_int]),
+    "nfx_arqs_packed_floats": (_sz, [_int, _int, _int]),
+    "nfx_arqs_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _int, _vp, _vp]),
+    "nfx_arqs": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _int, ctypes.c_double,
+                        ctypes.c_double, _int, _int, _vp]),
     "nfx_spline_packed_floats": (_sz, [_int, _int, _int]),
     "nfx_spline_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _int, _vp, _vp]),
     "nfx_spline_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _f,

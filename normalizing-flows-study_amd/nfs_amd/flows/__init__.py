@@ -2,9 +2,10 @@
 from .flow import Flow, SequentialFlow, HipFlow, STATS, reset_stats
 from .coupling import CouplingLayer
 from .spline import SplineCouplingLayer, rational_quadratic_spline
+from .arqs import ARQS
 from .autoregressive import (MaskedLinear, MADE, MaskedAutoregressiveFlow,
                              InverseAutoregressiveFlow, made_degrees)
 
 __all__ = ["Flow", "SequentialFlow", "HipFlow", "CouplingLayer", "SplineCouplingLayer",
-           "rational_quadratic_spline", "MaskedLinear", "MADE", "MaskedAutoregressiveFlow",
+           "rational_quadratic_spline", "ARQS", "MaskedLinear", "MADE", "MaskedAutoregressiveFlow",
            "InverseAutoregressiveFlow", "made_degrees", "STATS", "reset_stats"]

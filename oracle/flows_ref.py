@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 __all__ = [
-    "made_degrees", "made_masks", "coupling", "spline_coupling", "rqs_unit", "made", "maf", "iaf",
+    "made_degrees", "made_masks", "coupling", "spline_coupling", "rqs_unit", "made", "made_bn", "maf", "iaf", "arqs",
     "flow_model", "gauss_log_prob", "nll_f64", "realnvp_spec", "spline_model_spec", "maf_spec",
 ]
 
@@ -271,10 +271,50 @@ def iaf(sd, p, x, direction):
 
 
 # ---------------------------------------------------------------------------------------------
+# ARQS — src/flows/spline/arqs.py:7-114 (MADE(d, H, 3K-1) conditioner + unit RQS, sequential)
+# ---------------------------------------------------------------------------------------------
+def made_bn(sd, p, x):
+    """MADE with use_batch_norm=True in eval: MaskedLinear -> BatchNorm1d -> ReLU (made.py:87-114)."""
+    h = x
+    idx = 0
+    for i in range(4):
+        q = f"{p}net.{idx}."
+        h = F.linear(h, sd[q + "weight"] * sd[q + "mask"].to(sd[q + "weight"].dtype), sd[q + "bias"])
+        idx += 1
+        if i < 3:
+            b = f"{p}net.{idx}."
+            h = F.batch_norm(h, sd[b + "running_mean"], sd[b + "running_var"], sd[b + "weight"],
+                             sd[b + "bias"], False, 0.0, 1e-5)
+            h = F.relu(h)
+            idx += 2
+    return h
+
+
+def arqs(sd, p, x, direction, K=8, data_min=None, data_max=None, batch_norm=False):
+    B, d = x.shape
+    R = 3 * K - 1
+    net = made_bn if batch_norm else made
+    rescale = data_min is not None and data_max is not None
+    xr = (x - data_min) / (data_max - data_min) if rescale else x                   # :28-34
+    state = torch.zeros_like(xr)                                                    # :49 / :87
+    ld = torch.zeros(B)                                                             # :50 / :88
+    for i in range(d):                                                              # :52 / :90
+        prm = net(sd, p + "conditioner.", state).view(B, d, R)                      # :54-58
+        o, l = rqs_unit(xr[:, i], prm[:, i, :K], prm[:, i, K:2 * K], prm[:, i, 2 * K:],
+                        inverse=direction < 0)                                       # :64-70
+        sn = state.clone()                                                          # :72-74
+        sn[:, i] = o
+        state = sn
+        ld += l
+    out = state * (data_max - data_min) + data_min if rescale else state            # :36-42
+    return out, ld
+
+
+# ---------------------------------------------------------------------------------------------
 # Model chaining — src/models/normalizing_flow_model.py:25-65 (batch_norm_between_layers=False)
 # spec: list of (kind, prefix, kwargs); kind in {"coupling", "spline", "maf", "iaf"}
 # ---------------------------------------------------------------------------------------------
-_LAYER = {"coupling": coupling, "spline": spline_coupling, "maf": maf, "iaf": iaf}
+_LAYER = {"coupling": coupling, "spline": spline_coupling, "maf": maf, "iaf": iaf, "arqs": arqs}
 
 
 def flow_model(sd, spec, x, direction):

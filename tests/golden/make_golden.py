@@ -17,6 +17,8 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
   g6_iaf784.npz       IAF(784,64): forward 64 rows, inverse 16 rows
   g7_moons.npz        config 1: two-moons 5k, RealNVP(2,8,64) trained 45 steps, eval log_prob/NLL
   g9_small.npz        d=4/H=16 layers of the reference's own tests (+ MAF/IAF d=10)
+  g10_arqs.npz        ARQS (src/flows/spline/arqs.py) forward/inverse: d in {1,3,5,10}, H up to
+                      128, K in {2,5,8,11}, scalar data_min/data_max, eval BatchNorm in MADE
   g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes
 
 Each npz holds the module's state_dict arrays under their reference keys (prefixed per case),
@@ -300,6 +302,42 @@ def g9(flows, models):
     np.savez_compressed(os.path.join(HERE, "g9_small.npz"), **out)
 
 
+def g10(flows):
+    """ARQS: the sequential unit-interval spline flow with a MADE(d, H, 3K-1) conditioner."""
+    out = {}
+    cases = [  # name, dim, hidden, K, data range, use_batch_norm, rows
+        ("a1", 1, 16, 2, None, False, 64),
+        ("a3", 3, 16, 8, None, False, 512),
+        ("a5", 5, 128, 8, None, False, 256),
+        ("a4bn", 4, 32, 11, None, True, 256),
+        ("a10", 10, 64, 5, (-3.0, 3.0), False, 256),
+    ]
+    for i, (name, d, H, K, rng, bn, n) in enumerate(cases):
+        torch.manual_seed(100 + i)
+        kw = {"data_min": rng[0], "data_max": rng[1]} if rng else {}
+        m = flows.ARQS(d, hidden_dim=H, num_bins=K, use_batch_norm=bn, **kw)
+        perturb(m, 0.3, 200 + i)
+        m.eval()
+        g = torch.Generator().manual_seed(300 + i)
+        if rng:
+            x = torch.randn(n, d, generator=g) * 1.2
+        else:
+            x = torch.rand(n, d, generator=g)
+            x[:4] = torch.tensor([0.0, 1.0, 0.5, 1e-7])[:, None].expand(4, d)
+            x[4:6] = torch.tensor([-0.25, 1.25])[:, None].expand(2, d)  # clamped by the spline
+        with torch.no_grad():
+            xf, ldf = m.forward(x)
+            zi, ldi = m.inverse(x)
+            zr, ldr = m.inverse(xf)
+        out.update(sd_arrays(m, name + "."))
+        out.update({f"{name}.x": x.numpy(), f"{name}.fwd_y": xf.numpy(), f"{name}.fwd_ld": ldf.numpy(),
+                    f"{name}.inv_y": zi.numpy(), f"{name}.inv_ld": ldi.numpy(),
+                    f"{name}.rt_y": zr.numpy(), f"{name}.rt_ld": ldr.numpy(),
+                    f"{name}.meta": np.array([d, H, K, int(bn), rng[0] if rng else np.nan,
+                                              rng[1] if rng else np.nan], dtype=np.float64)})
+    np.savez_compressed(os.path.join(HERE, "g10_arqs.npz"), **out)
+
+
 def g8(m2, m3, m5):
     """Full-scale NLL scalars (float64 mean of the reference's fp32 log_prob)."""
     torch.set_num_threads(8)
@@ -331,8 +369,12 @@ def g8(m2, m3, m5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
+    ap.add_argument("--only", default=None, help="write one fixture only, e.g. g10")
     a = ap.parse_args()
     flows, models = import_reference()
+    if a.only == "g10":
+        g10(flows)
+        return
     import src.utils as src_utils
     g1(flows)
     m2 = g2(models)
@@ -342,6 +384,7 @@ def main():
     g6(flows)
     g7(models, src_utils)
     g9(flows, models)
+    g10(flows)
     if not a.skip_full:
         g8(m2, m3, m5)
     print("golden fixtures written to", HERE)

@@ -51,6 +51,7 @@ def _flows(dim, H=32):
         "spline_half": nfs_amd.SplineCouplingLayer(dim, H, _mask(dim, "half"), num_bins=8),
         "maf": nfs_amd.MaskedAutoregressiveFlow(dim, H),
         "iaf": nfs_amd.InverseAutoregressiveFlow(dim, H),
+        "arqs": nfs_amd.ARQS(dim, H, num_bins=8),
         "realnvp_bn": nfs_amd.RealNVP(dim, 4, H, batch_norm_between_layers=True),
         "realnvp_spline_bn": nfs_amd.RealNVPSpline(dim, 2, H, batch_norm_between_layers=True),
         "mixed": nfs_amd.NormalizingFlowModel([
@@ -63,7 +64,9 @@ def _flows(dim, H=32):
 AUTOREG = ("maf", "iaf")
 
 
-@pytest.mark.parametrize("name", list(_flows(4).keys()))
+# ARQS is left out: the reference's inverse conditions on z where its forward conditions on x
+# (arqs.py:54 vs :92), so ARQS.inverse is not the inverse of ARQS.forward (g10 fixtures).
+@pytest.mark.parametrize("name", [n for n in _flows(4).keys() if n != "arqs"])
 def test_invertibility_and_logdet_symmetry(cuda_device, name):
     torch.manual_seed(456)
     f = _perturb(_flows(4)[name], 0.05 if name in AUTOREG else 0.1, 7).to(cuda_device).eval()
@@ -97,7 +100,8 @@ def test_logdet_matches_autodiff_jacobian(cuda_device, name, dim):
         assert abs(ld[i].item() - ref.item()) <= 1e-4 + 1e-4 * abs(ref.item()), (i, ld[i].item(), ref.item())
 
 
-@pytest.mark.parametrize("cls,direction", [("maf", -1), ("maf", 1), ("iaf", 1), ("iaf", -1)])
+@pytest.mark.parametrize("cls,direction", [("maf", -1), ("maf", 1), ("iaf", 1), ("iaf", -1), ("arqs", 1),
+                                           ("arqs", -1)])
 @pytest.mark.parametrize("d", [3, 5, 10, 63, 100])
 def test_autoregressive_structure_bitwise(cuda_device, cls, direction, d):
     """Output i of the kernel depends only on inputs <= i (inputs < i for the conditioner):
@@ -105,6 +109,8 @@ def test_autoregressive_structure_bitwise(cuda_device, cls, direction, d):
     torch.manual_seed(d)
     f = _perturb(_flows(d, 32)[cls], 0.05, d).to(cuda_device).eval()
     x = torch.randn(64, d, device=cuda_device)
+    if cls == "arqs":
+        x = torch.rand(64, d, device=cuda_device) * 0.5  # inside the unit interval after +0.75
     run = f.inverse if direction < 0 else f.forward
     with torch.no_grad():
         y0, _ = run(x)

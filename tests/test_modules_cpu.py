@@ -131,3 +131,22 @@ def test_gradcheck_float64_coupling():
     x = torch.randn(4, 3, dtype=torch.float64, requires_grad=True)
     assert torch.autograd.gradcheck(lambda t: f.inverse(t)[0], (x,), eps=1e-6, atol=1e-4, rtol=1e-3)
     assert torch.autograd.gradcheck(lambda t: f.inverse(t)[1], (x,), eps=1e-6, atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("name", ["a1", "a3", "a5", "a4bn", "a10"])
+def test_arqs_composite_matches_reference(name):
+    """nfs_amd.ARQS (constructor, state_dict keys, composite path) vs the reference's outputs."""
+    g = load_golden("g10_arqs.npz")
+    d, H, K, bn, lo, hi = g[name + ".meta"]
+    kw = {} if np.isnan(lo) else {"data_min": float(lo), "data_max": float(hi)}
+    m = nfs_amd.ARQS(int(d), hidden_dim=int(H), num_bins=int(K), use_batch_norm=bool(bn), **kw)
+    ours = {k for k in m.state_dict() if not k.endswith("num_batches_tracked")}
+    assert ours == {k[len(name) + 1:] for k in g if k.startswith(name + ".conditioner.")}
+    m.load_state_dict(state_dict_from(g, name + ".", m))
+    m.eval()
+    x = torch.from_numpy(g[name + ".x"])
+    with torch.no_grad():
+        yf, lf = m.forward(x)
+        yi, li = m.inverse(x)
+    for got, key in ((yf, "fwd_y"), (lf, "fwd_ld"), (yi, "inv_y"), (li, "inv_ld")):
+        np.testing.assert_allclose(got.numpy(), g[f"{name}.{key}"], rtol=1e-5, atol=1e-5, err_msg=key)

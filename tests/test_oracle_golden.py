@@ -142,3 +142,26 @@ def test_small_layers_g9(name, kind):
     close(lf, g[name + ".fwd_ld"], rtol=1e-5, atol=1e-5)
     close(yi, g[name + ".inv_y"], rtol=1e-5, atol=1e-5)
     close(li, g[name + ".inv_ld"], rtol=1e-5, atol=1e-5)
+
+
+ARQS_CASES = ["a1", "a3", "a5", "a4bn", "a10"]
+
+
+def arqs_case(g, name):
+    d, H, K, bn, lo, hi = g[name + ".meta"]
+    rng = {} if np.isnan(lo) else {"data_min": float(lo), "data_max": float(hi)}
+    return int(d), int(H), int(K), bool(bn), rng
+
+
+@pytest.mark.parametrize("name", ARQS_CASES)
+def test_arqs_g10(name):
+    """ARQS (arqs.py:44-114): the oracle's sequential restatement vs the reference."""
+    g = load_golden("g10_arqs.npz")
+    d, H, K, bn, rng = arqs_case(g, name)
+    sd = oracle_sd(g, name + ".")
+    x = torch.from_numpy(g[name + ".x"])
+    for direction, key in ((1, "fwd"), (-1, "inv")):
+        with torch.no_grad():
+            y, ld = oracle.arqs(sd, "", x, direction, K=K, batch_norm=bn, **rng)
+        close(y, g[f"{name}.{key}_y"], rtol=1e-5, atol=1e-6)
+        close(ld, g[f"{name}.{key}_ld"], rtol=1e-5, atol=1e-5)
