@@ -8,6 +8,12 @@ small per-GPU shard (strong scaling, or the reference's 4,000-sample throughput 
 bound by. Inputs go through a static buffer; outputs are the graph's static tensors (valid
 until the next replay).
 
+mode="sample" is the fused sampling path (`Flow.sample`, flow.py:40-54,
+and the reference's sampling throughput loop, plots/_common.py:217-222,264-274): the graph
+draws z ~ N(0, I) on device with torch's graph-safe Philox generator (a fresh draw per replay)
+and runs forward(z) — one graph launch per batch of samples, no host round trip. The example
+tensor only gives the shape [n, d]; `static_in` holds the last z.
+
 The packed weight images are built before capture and baked into the graph. With
 `strict=True` (default) every call checks that no parameter or buffer changed since capture
 (in-place optimizer steps and load_state_dict bump tensor versions) and raises instead of
@@ -23,12 +29,13 @@ def _tensor_versions(model):
 
 
 class GraphedFlow:
-    """Capture `model.log_prob(x, return_sums=True)` (mode="log_prob") or `model.forward(x)`
-    (mode="forward") for inputs shaped like `example`."""
+    """Capture `model.log_prob(x, return_sums=True)` (mode="log_prob"), `model.forward(x)`
+    (mode="forward"), `model.inverse(x)` (mode="inverse") or z ~ N(0, I) + `model.forward(z)`
+    (mode="sample") for inputs shaped like `example`."""
 
     def __init__(self, model, example, mode="log_prob", strict=True, warmup=2):
-        if mode not in ("log_prob", "forward", "inverse"):
-            raise ValueError(f"mode must be log_prob/forward/inverse, got {mode}")
+        if mode not in ("log_prob", "forward", "inverse", "sample"):
+            raise ValueError(f"mode must be log_prob/forward/inverse/sample, got {mode}")
         if example.device.type != "cuda":
             raise ValueError("GraphedFlow needs a ROCm device tensor")
         self.model = model.flow if hasattr(model, "flow") and hasattr(model.flow, "log_prob") else model
@@ -53,6 +60,9 @@ class GraphedFlow:
         self.versions = _tensor_versions(self.model) if strict else None
 
     def _call(self):
+        if self.mode == "sample":
+            self.static_in.normal_()
+            return self.model.forward(self.static_in)
         if self.mode == "log_prob":
             return self.model.log_prob(self.static_in, return_sums=True)
         if self.mode == "forward":
@@ -63,6 +73,8 @@ class GraphedFlow:
         if self.strict and _tensor_versions(self.model) != self.versions:
             raise RuntimeError("GraphedFlow: parameters changed since capture; capture again")
         if x is not None:
+            if self.mode == "sample":
+                raise ValueError("GraphedFlow(mode='sample') draws its own z; call it without an input")
             if x.shape != self.static_in.shape:
                 raise ValueError(f"GraphedFlow captured shape {tuple(self.static_in.shape)}, got {tuple(x.shape)}")
             self.static_in.copy_(x)

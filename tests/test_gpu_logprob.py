@@ -148,3 +148,25 @@ def test_graphed_flow_matches_eager(cuda_device, kind):
         next(m.parameters()).add_(1e-3)
     with pytest.raises(RuntimeError):
         g()
+
+
+def test_graphed_sampling(cuda_device):
+    """GraphedFlow(mode="sample") — on-device z ~ N(0, I) + forward in one graph launch
+    (§8(f) item 3): every replay draws fresh z, the output equals the eager forward of that z
+    bit for bit, and the draws are standard normal."""
+    m, d, _ = _model("realnvp")
+    m = m.to(cuda_device).eval()
+    g = nfs_amd.GraphedFlow(m, torch.empty(4000, d, device=cuda_device), mode="sample")
+    x1, ld1 = g()
+    z1 = g.static_in.clone()
+    x1 = x1.clone()
+    x2, _ = g()
+    z2 = g.static_in.clone()
+    assert not torch.equal(z1, z2)
+    with torch.no_grad():
+        y, ld = m.forward(z2)
+    assert torch.equal(x2, y)
+    zs = torch.cat([z1, z2])
+    assert abs(zs.mean().item()) < 0.05 and abs(zs.std().item() - 1) < 0.05
+    with pytest.raises(ValueError):
+        g(z1)
