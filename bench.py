@@ -93,6 +93,31 @@ def build(config):
         import oracle
         return m, 2, f, oracle.realnvp_spec(10), \
             "sample4k RealNVP(2,10,128) sampling: model.forward(z), n=4000 per call (plots/_common.py:264-274)"
+    if config == "sample4k_spline":
+        torch.manual_seed(5)
+        m = nfs_amd.RealNVPSpline(2, 8, 64)
+        perturb(m, 0.1, 6)
+        H, K = 64, 10
+        # 2 flop x (n_c*H + H*H + H*n_t*(3K-1)), n_c = n_t = 1
+        f = 2 * (1 * H + H * H + H * (3 * K - 1))
+        import oracle
+        return m, 2, f, oracle.spline_model_spec(8), \
+            "sample4k_spline RealNVPSpline(2,8,64) (K=10) sampling: model.forward(z), n=4000 per call " \
+            "(plots/_common.py:163,264-274)"
+    if config in ("sample4k_maf", "sample4k_iaf"):
+        torch.manual_seed(7)
+        cls = nfs_amd.MaskedAutoregressiveFlow if config == "sample4k_maf" else nfs_amd.InverseAutoregressiveFlow
+        m = nfs_amd.NormalizingFlowModel([cls(2, 64) for _ in range(6)])
+        perturb(m, 0.02, 8)
+        d, H = 2, 64
+        f = 2 * (d * H + 2 * H * H + 2 * d * H)
+        import oracle
+        kind = "maf" if config == "sample4k_maf" else "iaf"
+        spec = [(kind, f"flows.{i}.", {}) for i in range(6)]
+        what = "MAF forward = sequential over d" if kind == "maf" else "IAF forward = parallel"
+        return m, d, f, spec, \
+            f"{config} 6x{kind.upper()}(2,64) sampling ({what}): model.forward(z), n=4000 per call " \
+            f"(plots/_common.py:165-167,264-274)"
     if config == "cfg4t":
         m, d, f, spec, _ = build("cfg4")
         # training step: forward recompute + data-gradient chain in the fused backward kernel
@@ -115,10 +140,16 @@ def build(config):
 
 # per-GPU batch of each config (weak scaling unit)
 DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 500_000, "cfg4t": 500_000, "cfg5f": 524_288,
-                 "cfg5i": 8_192, "sample4k": 4_000}
+                 "cfg5i": 8_192, "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000,
+                 "sample4k_iaf": 4_000}
 # The reference's only published throughput (assets/benchmark.png via
 # plots/_common.py:264-274): RealNVP(2,10,128) sampling, model.forward(z) on n = 4,000, CPU.
-PUBLISHED_SAMPLE4K = 186_000.0
+# The same figure's other sampling numbers: Spline = RealNVPSpline(2,8,64) K=10,
+# MAF = 6x MaskedAutoregressiveFlow(2,64), IAF = 6x InverseAutoregressiveFlow(2,64) (plots/_common.py:161-167).
+PUBLISHED_SAMPLING = {"sample4k": ("RealNVP(2,10,128)", 186_000.0),
+                      "sample4k_spline": ("RealNVPSpline(2,8,64), K=10", 334_000.0),
+                      "sample4k_maf": ("6x MAF(2,64)", 602_000.0),
+                      "sample4k_iaf": ("6x IAF(2,64)", 1_121_000.0)}
 
 
 def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=262144):
@@ -187,7 +218,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k"])
+                    choices=["cfg2", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
+                             "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -211,7 +243,7 @@ def main():
     from nfs_amd.distributed import average_gradients, broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
     B_unit = a.batch or DEFAULT_BATCH[a.config]
-    sampling = a.config in ("cfg5f", "sample4k")
+    sampling = a.config == "cfg5f" or a.config.startswith("sample4k")
     if a.strong:
         lo, hi = shard_range(B_unit, rank, world)
         B, B_global = hi - lo, B_unit
@@ -332,9 +364,12 @@ def main():
                          "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs)},
             "cpu_baseline": None,
         }
-        if a.config == "sample4k":
-            result["metric"] = "sampling samples/sec (RealNVP(2,10,128), n=4000 per forward call)"
-            result["vs_baseline"] = result["value"] / PUBLISHED_SAMPLE4K
+        if a.config in PUBLISHED_SAMPLING:
+            mname, pub = PUBLISHED_SAMPLING[a.config]
+            result["metric"] = f"sampling samples/sec ({mname}, n=4000 per forward call)"
+            result["vs_baseline"] = result["value"] / pub
+            result["published_baseline"] = {"value": pub, "unit": "samples/s", "hardware": "CPU (unspecified)",
+                                            "source": "assets/benchmark.png via plots/_common.py:264-274"}
             result["nll_f64"] = None
         if training:
             result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
@@ -345,7 +380,7 @@ def main():
         if world == 1 and not a.no_cpu and training:
             result["cpu_baseline"] = cpu_training_baseline(model, spec, x)
         elif world == 1 and not a.no_cpu:
-            rows = {"cfg5f": 16384, "cfg5i": 256, "sample4k": 4000}.get(a.config, 262144)
+            rows = {"cfg5f": 16384, "cfg5i": 256}.get(a.config, 4000 if a.config.startswith("sample4k") else 262144)
             cb, cpu_nll, xs = cpu_baseline(model, spec, x, forward=sampling, max_rows=rows)
             if not sampling:
                 gpu_nll = flow.nll(xs.to(dev))

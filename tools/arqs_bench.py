@@ -2,11 +2,13 @@
 
     python tools/arqs_bench.py [d] [B]
 """
+import os
 import sys
 import time
 
-sys.path.insert(0, "normalizing-flows-study_amd")
-sys.path.insert(0, ".")
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(_ROOT, "normalizing-flows-study_amd"))
+sys.path.insert(0, _ROOT)
 import torch
 import nfs_amd
 import oracle
