@@ -118,6 +118,21 @@ def build(config):
         return m, d, f, spec, \
             f"{config} 6x{kind.upper()}(2,64) sampling ({what}): model.forward(z), n=4000 per call " \
             f"(plots/_common.py:165-167,264-274)"
+    if config in ("cfg2t", "train5k"):
+        torch.manual_seed(0)
+        m = nfs_amd.RealNVP(2, 8, 64)
+        perturb(m, 0.03, 1)
+        H = 64
+        # dominant kernel = BWD2 of the train-mode backward: per net layer-2 forward recompute,
+        # (diag(r2) W2)^T e2 and dW2 = sum e2 a1^T (3 x 2H^2) + layer 1 (2H) + output layer and
+        # W3^T delta3 (2 x 2H), n_c = n_t = 1
+        f = 2 * (3 * 2 * H * H + 2 * H + 2 * 2 * H)
+        import oracle
+        what = ("cfg2t RealNVP(2,8,64) training step (train-mode BatchNorm: batch statistics + "
+                "running-stat update, -log_prob mean, fused backward, Adam)") if config == "cfg2t" else \
+            ("train5k RealNVP(2,8,64) full-batch training step on 5,000 samples (README.md:107-117: "
+             "two-moons-sized batch, train-mode BatchNorm, Adam)")
+        return m, 2, f, oracle.realnvp_spec(8, training=True), what
     if config == "cfg4t":
         m, d, f, spec, _ = build("cfg4")
         # training step: forward recompute + data-gradient chain in the fused backward kernel
@@ -139,7 +154,8 @@ def build(config):
     raise ValueError(config)
 
 # per-GPU batch of each config (weak scaling unit)
-DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 500_000, "cfg4t": 500_000, "cfg5f": 524_288,
+DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "cfg3": 1_000_000, "cfg4": 500_000,
+                 "cfg4t": 500_000, "cfg5f": 524_288,
                  "cfg5i": 8_192, "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000,
                  "sample4k_iaf": 4_000}
 # The reference's only published throughput (assets/benchmark.png via
@@ -190,7 +206,8 @@ def cpu_training_baseline(model, spec, x_gpu, budget_s=12.0, max_rows=32768):
     torch.set_num_threads(threads)
     n = min(x_gpu.shape[0], max_rows)
     x = x_gpu[:n].detach().float().cpu()
-    sd = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point()) for k, v in model.state_dict().items()}
+    sd = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point() and not k.endswith(
+        ("running_mean", "running_var", "mask"))) for k, v in model.state_dict().items()}
     times = []
 
     def run():
@@ -218,7 +235,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
+                    choices=["cfg2", "cfg2t", "train5k", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
                              "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
@@ -238,7 +255,11 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     model, d, f_layer, spec, desc = build(a.config)
-    training = a.config == "cfg4t"
+    training = a.config in ("cfg4t", "cfg2t", "train5k")
+    coupling_train = a.config in ("cfg2t", "train5k")
+    if coupling_train and world > 1:
+        from nfs_amd.distributed import enable_sync_batchnorm
+        enable_sync_batchnorm(True)  # batch statistics over all ranks = the full-batch step
     model = model.to(dev).train(training)
     from nfs_amd.distributed import average_gradients, broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
@@ -300,7 +321,15 @@ def main():
         # Kernel durations: the same K steps again with HIP events around every layer launch
         # on the launch stream. Kept out of the headline loop because each event record adds
         # ~5 us of GPU idle between kernels (measured, profiles/).
-        if training:
+        if coupling_train:
+            from nfs_amd.flows import coupling as _cp
+            _cp.TRAIN_EVENTS = []
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+            events = [e for e in _cp.TRAIN_EVENTS if e[0].endswith("<BWD2>")]
+            _cp.TRAIN_EVENTS = None
+        elif training:
             _ar.BACKWARD_EVENTS = []
             for _ in range(a.steps):
                 step()
@@ -371,7 +400,16 @@ def main():
             result["published_baseline"] = {"value": pub, "unit": "samples/s", "hardware": "CPU (unspecified)",
                                             "source": "assets/benchmark.png via plots/_common.py:264-274"}
             result["nll_f64"] = None
-        if training:
+        if coupling_train:
+            result["metric"] = "training samples/sec/GPU (RealNVP d=2 train-mode step)"
+            result["nll_f64"] = None
+            result["roofline"]["note"] = ("dominant kernel = BWD2 of the train-mode coupling backward "
+                                          "(layer-2 recompute, W2^T e2 and the sample-contraction dW2 on "
+                                          "MFMA); a layer runs STATS1, STATS2, the fused forward, BWD1-3")
+            if world > 1:
+                result["config"]["parallelism"] = (f"dp{world} (sample shards, SyncBN: 4 all-gathers/all-reduces "
+                                                   f"of <= 3 KB per layer + 1 bucketed gradient all-reduce)")
+        elif training:
             result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
             result["nll_f64"] = None
             result["roofline"]["note"] = ("dominant kernel = the fused backward (forward recompute + "

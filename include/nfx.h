@@ -188,6 +188,53 @@ int nfx_made_affine_backward(const float* packed, const float* in, const float* 
                              int d, int H, int variant, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Training (SURVEY.md §8(f) items 1 + 2): CouplingLayer in TRAIN mode — BatchNorm1d with
+ * batch statistics (coupling_layer.py:18-35 under model.train(); the reference's training
+ * loops README.md:107-117, plots/_common.py:194-211) — and its backward, for d <= 8, H <= 64
+ * (NFX_EUNSUPPORTED otherwise). Replaces the autograd graph of coupling_layer.py:40-96.
+ * Statistics are float64 triples stats[2 nets][Hp][3] = (n, mean, M2), Hp = 32*ceil(H/32),
+ * so data-parallel ranks can merge them exactly (SyncBN); BatchNorm normalises with
+ * var = M2/n and updates running_var with M2/(n-1) (momentum as given).
+ * One layer's step (the caller orders them on one stream):
+ *   nfx_affine_train_pack(stats1 = stats2 = NULL)  -> tpack (identity BatchNorm)
+ *   nfx_affine_train_stats(layer 1)                -> stats1      [SyncBN: merge over ranks]
+ *   nfx_affine_train_pack(stats1, NULL)            -> tpack
+ *   nfx_affine_train_stats(layer 2)                -> stats2      [SyncBN: merge over ranks]
+ *   nfx_affine_train_pack(stats1, stats2, epack)   -> tpack + eval-layout pack epack
+ *   nfx_affine_coupling(epack, ...)                -> (y, log_det) of the train-mode layer
+ *   nfx_affine_train_update_running                -> BatchNorm running statistics [4 BNs:
+ *                                                     s_net.1, s_net.4, b_net.1, b_net.4]
+ * backward, from grad_out = dL/dy [B,d] and grad_log_det [B]:
+ *   nfx_affine_train_backward(stage 1, 2, 3)       -> G (float64 sums; stage-1/-2 BatchNorm
+ *                                                     sums G[0:4Hp] and the stage-2 block are
+ *                                                     all-reduced between stages under SyncBN)
+ *                                                     and grad_in [B,d]
+ *   nfx_affine_train_assemble                      -> fp32 parameter gradients in the layer's
+ *                                                     parameters() order (s_net then b_net)
+ * `workspace` holds nfx_affine_train_workspace_bytes(B, d, H) bytes and must be the same buffer
+ * for stages 2 and 3 of one backward.
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_affine_train_pack_floats(int d, int H);
+size_t nfx_affine_train_stats_doubles(int H);
+size_t nfx_affine_train_grad_doubles(int d, int H);
+size_t nfx_affine_train_param_floats(int d, int H);
+size_t nfx_affine_train_workspace_bytes(int64_t B, int d, int H);
+int nfx_affine_train_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, const float* mask,
+                          const double* stats1, const double* stats2, int d, int H, float* tpack,
+                          float* epack, void* stream);
+int nfx_affine_train_stats(const float* tpack, const float* in, int64_t B, int d, int H, int layer,
+                           double* stats, void* workspace, void* stream);
+int nfx_affine_train_update_running(const double* stats1, const double* stats2,
+                                    float* const* running_mean, float* const* running_var, int H,
+                                    double momentum, void* stream);
+int nfx_affine_train_backward(const float* tpack, const float* in, const float* grad_out,
+                              const float* grad_log_det, float* grad_in, int64_t B, int d, int H,
+                              int direction, int stage, const double* stats2, double* G,
+                              void* workspace, void* stream);
+int nfx_affine_train_assemble(const double* G, const double* stats1, const double* stats2, int d,
+                              int H, float eps, float* grads, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Gaussian base log-density + NLL partial sums — the log_prob glue of the callers
  * (Flow.log_prob src/flows/flow/flow.py:56-73; README.md:113-114; src/utils.py:39-55):
  *   logp[i] = -0.5 * (fp32(d*log(2*pi)) + sum_j z[i,j]^2) + log_det[i]

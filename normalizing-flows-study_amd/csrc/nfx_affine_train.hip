@@ -1,0 +1,435 @@
+// Train-mode affine coupling layer (RealNVP CouplingLayer, BatchNorm with batch statistics)
+// and its backward, for gfx950. SURVEY.md §8(f) items 1 and 2.
+//
+// Reference: src/flows/coupling/coupling_layer.py
+//   nets :18-35  Linear(d,H) BatchNorm1d(H) ReLU Linear(H,H) BatchNorm1d(H) ReLU Linear(H,d)
+//   forward :40-68 / inverse :70-96, clamps :50-51/:79-80, guards :61-66/:89-94
+// In train mode (model.train(), the reference's training loops: README.md:107-117,
+// plots/_common.py:194-211) each BatchNorm1d normalises with the statistics of the whole batch
+// and updates its running statistics (momentum 0.1, unbiased variance).
+//
+// Pass structure of one layer (all on the caller's stream, no host synchronisation):
+//   forward   STATS1  per-feature (n, mean, M2) of h1 = W1 xa + b1 (both nets)
+//             STATS2  h2 = W2 relu(BN1(h1)) + b2 statistics           (layer 1 folded with STATS1)
+//             fold    eval-layout pack with the batch statistics -> the streaming eval kernel
+//                     produces (y, log_det); running statistics updated
+//   backward  BWD1    recompute, epilogue backward, g_y2 = relu'(.) W3^T delta3:
+//                     sums for BN2 backward (sum g, sum g x^), dW3, db3; gx (direct term)
+//             BWD2    recompute + e2 = gamma2 (g_y2 - k1 - x^2 k2): dW2 = r2 sum e2 a1^T (MFMA
+//                     over the sample dimension), db2, g_y1 = relu'(.) W2^T dh2 (MFMA) -> HBM,
+//                     sums for BN1 backward
+//             BWD3    e1 = gamma1 (g_y1 - k1 - x^1 k2): dW1, db1, gx += m * W1^T dh1
+//             assemble the parameter gradients (fp32, the module's parameters() order)
+// Under SyncBN (data-parallel training) the host all-reduces the statistics after STATS1/STATS2
+// and the BN-backward sums after BWD1/BWD2 (nfs_amd.distributed), which makes the sharded step
+// equal to the full-batch step.
+#include <cmath>
+
+#include "nfx_affine_kernel.h"
+#include "nfx_affine_train_kernel.h"
+#include "nfx_pack.h"
+
+namespace nfx {
+
+// BatchNorm fold of layer `layer` (0 or 1) of net P from float64 statistics triples
+// [Hp][3] = (n, mean, M2): r = 1/sqrt(var + eps), var = M2 / n (biased, as BatchNorm1d
+// normalises). stats == nullptr -> identity (mean 0, r 1).
+struct BnFold {
+    double mean, r;
+};
+__device__ inline BnFold bn_fold(const double* stats, int Hp, int net, int row, double eps) {
+    if (!stats) return {0.0, 1.0};
+    const double* q = stats + ((size_t)net * Hp + row) * 3;
+    const double var = q[0] > 0.0 ? q[2] / q[0] : 0.0;
+    return {q[1], 1.0 / sqrt(var + eps)};
+}
+
+__device__ inline float raw_w(const NfxMlpRaw& P, int layer, int in_dim, int row, int col) {
+    return P.w[layer][(size_t)row * in_dim + col];
+}
+__device__ inline float raw_b(const NfxMlpRaw& P, int layer, int row) { return P.b[layer] ? P.b[layer][row] : 0.f; }
+__device__ inline float raw_g(const NfxMlpRaw& P, int layer, int row) { return P.bn_w[layer] ? P.bn_w[layer][row] : 1.f; }
+__device__ inline float raw_be(const NfxMlpRaw& P, int layer, int row) { return P.bn_b[layer] ? P.bn_b[layer][row] : 0.f; }
+
+__global__ void affine_train_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float* mask,
+                                         const double* stats1, const double* stats2, int d, int D, int H,
+                                         float* tpack, float* epack) {
+    const int HT = (H + 31) / 32, Hp = 32 * HT;
+    const TrainLayout L = train_layout(D, HT);
+    const double eps = s_net.bn_eps;
+    const int gstride = gridDim.x * blockDim.x;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gstride) {
+        float v = 0.f;
+        if (i >= L.mask) {
+            const int j = i - L.mask;
+            v = j < d ? mask[j] : 1.f;
+        } else {
+            const int net = i / L.net;
+            const NfxMlpRaw& P = net ? b_net : s_net;
+            const int o = i - net * L.net;
+            if (o < L.c1) {  // w1 [HT][KS1][64]
+                const int t = o - L.w1, lane = t & 63, ks = (t >> 6) % L.KS1, ht = (t >> 6) / L.KS1;
+                const int row = 32 * ht + (lane & 31), c = 2 * ks + (lane >> 5);
+                if (row < H && c < d) v = (float)(bn_fold(stats1, Hp, net, row, eps).r * (double)raw_w(P, 0, d, row, c));
+            } else if (o < L.w2) {  // c1, g1, e1 [HT][32] accumulator order
+                const int which = (o - L.c1) / (HT * 32), t = (o - L.c1) % (HT * 32);
+                const int row = 32 * (t >> 5) + crow(t & 15, (t >> 4) & 1);
+                if (row < H) {
+                    if (which == 0) {
+                        const BnFold f = bn_fold(stats1, Hp, net, row, eps);
+                        v = (float)(f.r * ((double)raw_b(P, 0, row) - f.mean));
+                    } else {
+                        v = which == 1 ? raw_g(P, 0, row) : raw_be(P, 0, row);
+                    }
+                }
+            } else if (o < L.c2) {  // w2 [o][kt][rq][lane][rr]
+                const int t = o - L.w2, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+                const int kt = (t >> 10) % HT, ot = (t >> 10) / HT;
+                const int row = 32 * ot + (lane & 31), c = 32 * kt + crow(4 * rq + rr, lane >> 5);
+                if (row < H && c < H) v = (float)(bn_fold(stats2, Hp, net, row, eps).r * (double)raw_w(P, 1, H, row, c));
+            } else if (o < L.w3) {  // c2, g2, e2
+                const int which = (o - L.c2) / (HT * 32), t = (o - L.c2) % (HT * 32);
+                const int row = 32 * (t >> 5) + crow(t & 15, (t >> 4) & 1);
+                if (row < H) {
+                    if (which == 0) {
+                        const BnFold f = bn_fold(stats2, Hp, net, row, eps);
+                        v = (float)(f.r * ((double)raw_b(P, 1, row) - f.mean));
+                    } else {
+                        v = which == 1 ? raw_g(P, 1, row) : raw_be(P, 1, row);
+                    }
+                }
+            } else if (o < L.b3) {  // w3 [D][HT][32]
+                const int t = o - L.w3, j = t / (HT * 32), a = t % (HT * 32);
+                const int c = 32 * (a >> 5) + crow(a & 15, (a >> 4) & 1);
+                if (j < d && c < H) v = raw_w(P, 2, H, j, c);
+            } else if (o < L.w2t) {
+                const int j = o - L.b3;
+                if (j < d) v = raw_b(P, 2, j);
+            } else if (o < L.w1c) {  // w2t [kt][o][rq][lane][rr]: A[i][k] = W2r[32 o + k][32 kt + i]
+                const int t = o - L.w2t, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+                const int ot = (t >> 10) % HT, kt = (t >> 10) / HT;
+                const int row = 32 * ot + crow(4 * rq + rr, lane >> 5), c = 32 * kt + (lane & 31);
+                if (row < H && c < H) v = (float)(bn_fold(stats2, Hp, net, row, eps).r * (double)raw_w(P, 1, H, row, c));
+            } else {  // w1c [D][HT][32]: (diag(r1) W1)[row][j]
+                const int t = o - L.w1c, j = t / (HT * 32), a = t % (HT * 32);
+                const int row = 32 * (a >> 5) + crow(a & 15, (a >> 4) & 1);
+                if (j < d && row < H) v = (float)(bn_fold(stats1, Hp, net, row, eps).r * (double)raw_w(P, 0, d, row, j));
+            }
+        }
+        tpack[i] = v;
+    }
+    if (!epack) return;
+    // eval-layout pack of the streaming kernel, BatchNorm folded with the batch statistics
+    const AffineLayout E = affine_layout(d, HT);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < E.total; i += gstride) {
+        float v = 0.f;
+        if (i >= E.mask) {
+            const int j = i - E.mask;
+            v = j < d ? mask[j] : 0.f;
+        } else {
+            const int net = i / E.net;
+            const NfxMlpRaw& P = net ? b_net : s_net;
+            const int o = i - net * E.net;
+            auto wfold = [&](int layer, int in_dim, const double* st, int row, int c) {
+                const BnFold f = bn_fold(st, Hp, net, row, eps);
+                const double a = (double)raw_g(P, layer, row) * f.r;
+                return (float)(a * (double)raw_w(P, layer, in_dim, row, c));
+            };
+            auto bfold = [&](int layer, const double* st, int row) {
+                const BnFold f = bn_fold(st, Hp, net, row, eps);
+                const double a = (double)raw_g(P, layer, row) * f.r;
+                return (float)(a * ((double)raw_b(P, layer, row) - f.mean) + (double)raw_be(P, layer, row));
+            };
+            if (o < E.b1) {
+                const int t = o - E.w1, lane = t & 63, ks = (t >> 6) % E.KS1, ht = (t >> 6) / E.KS1;
+                const int row = 32 * ht + (lane & 31), c = 2 * ks + (lane >> 5);
+                if (row < H && c < d) v = wfold(0, d, stats1, row, c);
+            } else if (o < E.w2) {
+                const int t = o - E.b1, r = t & 15, hh = (t >> 4) & 1, ht = t >> 5;
+                const int row = 32 * ht + crow(r, hh);
+                if (row < H) v = bfold(0, stats1, row);
+            } else if (o < E.b2) {
+                const int t = o - E.w2, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+                const int kt = (t >> 10) % HT, hto = (t >> 10) / HT;
+                const int row = 32 * hto + (lane & 31), c = 32 * kt + crow(4 * rq + rr, lane >> 5);
+                if (row < H && c < H) v = wfold(1, H, stats2, row, c);
+            } else if (o < E.w3) {
+                const int t = o - E.b2, r = t & 15, hh = (t >> 4) & 1, ht = t >> 5;
+                const int row = 32 * ht + crow(r, hh);
+                if (row < H) v = bfold(1, stats2, row);
+            } else if (o < E.b3) {
+                const int t = o - E.w3, r = t & 15, hh = (t >> 4) & 1, ht = (t >> 5) % HT, j = (t >> 5) / HT;
+                const int c = 32 * ht + crow(r, hh);
+                if (c < H) v = raw_w(P, 2, H, j, c);
+            } else {
+                const int j = o - E.b3;
+                if (j < d) v = raw_b(P, 2, j);
+            }
+        }
+        epack[i] = v;
+    }
+}
+
+// stats[net][row][3] = Chan merge, in wave order, of the per-wave triples.
+__global__ void affine_train_stats_finish(const double* part, int64_t nw, int Hp, double* stats) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // net * Hp + row
+    if (i >= 2 * Hp) return;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    for (int64_t w = 0; w < nw; ++w) {
+        const double* q = part + (w * 2 * Hp + i) * 3;
+        if (n == 0.0) {
+            n = q[0]; mean = q[1]; m2 = q[2];
+        } else {
+            chan_merge(n, mean, m2, q[0], q[1], q[2]);
+        }
+    }
+    stats[i * 3 + 0] = n;
+    stats[i * 3 + 1] = mean;
+    stats[i * 3 + 2] = m2;
+}
+
+// out[i] = sum_w part[w * len + i] in float64, wave order (deterministic).
+__global__ void affine_train_sum_finish(const float* part, int64_t nw, int len, double* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    double a = 0.0;
+    for (int64_t w = 0; w < nw; ++w) a += (double)part[w * len + i];
+    out[i] = a;
+}
+
+// Parameter gradients in CouplingLayer.parameters() order, per net (s_net then b_net):
+//   0.weight [H,d] 0.bias [H] 1.weight [H] 1.bias [H] 3.weight [H,H] 3.bias [H]
+//   4.weight [H] 4.bias [H] 6.weight [d,H] 6.bias [d]
+__global__ void affine_train_assemble_kernel(const double* G, const double* stats1, const double* stats2,
+                                             int d, int D, int H, double eps, float* grads) {
+    const int HT = (H + 31) / 32, Hp = 32 * HT;
+    const TrainGrad GL = train_grad_layout(D, HT);
+    const int per_net = H * d + H + 2 * H + H * H + H + 2 * H + d * H + d;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * per_net; i += gridDim.x * blockDim.x) {
+        const int net = i / per_net;
+        int o = i % per_net;
+        double v;
+        if (o < H * d) {  // 0.weight: r1 * sum e1 xa^T
+            const int row = o / d, j = o % d;
+            v = bn_fold(stats1, Hp, net, row, eps).r * G[GL.g3w + net * (D * Hp + Hp) + j * Hp + row];
+        } else if ((o -= H * d) < H) {  // 0.bias
+            v = bn_fold(stats1, Hp, net, o, eps).r * G[GL.g3w + net * (D * Hp + Hp) + D * Hp + o];
+        } else if ((o -= H) < H) {  // 1.weight (gamma1) = sum g_y1 x^1
+            v = G[GL.g2s + (net * 2 + 1) * Hp + o];
+        } else if ((o -= H) < H) {  // 1.bias (beta1) = sum g_y1
+            v = G[GL.g2s + (net * 2 + 0) * Hp + o];
+        } else if ((o -= H) < H * H) {  // 3.weight: r2 * sum e2 a1^T
+            const int row = o / H, c = o % H;
+            v = bn_fold(stats2, Hp, net, row, eps).r * G[GL.g2w + net * (Hp * Hp + Hp) + row * Hp + c];
+        } else if ((o -= H * H) < H) {  // 3.bias
+            v = bn_fold(stats2, Hp, net, o, eps).r * G[GL.g2w + net * (Hp * Hp + Hp) + Hp * Hp + o];
+        } else if ((o -= H) < H) {  // 4.weight (gamma2)
+            v = G[GL.g1s + (net * 2 + 1) * Hp + o];
+        } else if ((o -= H) < H) {  // 4.bias (beta2)
+            v = G[GL.g1s + (net * 2 + 0) * Hp + o];
+        } else if ((o -= H) < d * H) {  // 6.weight [d, H]
+            const int j = o / H, c = o % H;
+            v = G[GL.g1w + net * (D * Hp + D) + j * Hp + c];
+        } else {  // 6.bias
+            o -= d * H;
+            v = G[GL.g1w + net * (D * Hp + D) + D * Hp + o];
+        }
+        grads[i] = (float)v;
+    }
+}
+
+// BatchNorm1d running statistics (train mode, momentum m): running_mean = m mean + (1-m) rm,
+// running_var = m var_unbiased + (1-m) rv, in double then rounded (ATen's CPU kernel order).
+struct NfxBnPtrs {
+    float* rm[4];
+    float* rv[4];
+};
+__global__ void affine_train_running_kernel(const double* stats1, const double* stats2, NfxBnPtrs p, int H,
+                                            int Hp, double momentum) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (net * 2 + layer) * H + row
+    if (i >= 4 * H) return;
+    const int k = i / H, row = i % H, net = k >> 1, layer = k & 1;
+    const double* q = (layer ? stats2 : stats1) + ((size_t)net * Hp + row) * 3;
+    const double n = q[0];
+    const double var_u = n > 1.0 ? q[2] / (n - 1.0) : NAN;
+    if (p.rm[k]) p.rm[k][row] = (float)(momentum * q[1] + (1.0 - momentum) * (double)p.rm[k][row]);
+    if (p.rv[k]) p.rv[k][row] = (float)(momentum * var_u + (1.0 - momentum) * (double)p.rv[k][row]);
+}
+
+static int pad_d(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 8 ? 8 : 0)); }
+
+static affine_train_kernel_t pick_train(int HT, int D, int stage) {
+    switch (HT) {
+        case 1: return affine_train_pick_ht<1>(D, stage);
+        case 2: return affine_train_pick_ht<2>(D, stage);
+        default: return nullptr;
+    }
+}
+
+static int train_check(int d, int H, const char* what) {
+    if (d <= 0 || H <= 0) return set_error(NFX_EINVAL, "%s: bad shape d=%d H=%d", what, d, H);
+    if (!pad_d(d) || H > 64)
+        return set_error(NFX_EUNSUPPORTED, "%s: d=%d H=%d outside the compiled train-mode family (d<=8, H<=64)",
+                         what, d, H);
+    return NFX_OK;
+}
+
+struct TrainGrid {
+    int grid;
+    int64_t nwaves, ntiles;
+};
+
+static TrainGrid train_grid(affine_train_kernel_t k, size_t lds, int64_t B) {
+    TrainGrid g;
+    g.ntiles = (B + 31) / 32;
+    g.grid = resident_grid((const void*)k, 256, lds, (g.ntiles + 3) / 4);
+    if (g.grid > 2 * num_cus()) g.grid = 2 * num_cus();  // the workspace is sized for <= 2 WGs per CU
+    g.nwaves = (int64_t)g.grid * 4;
+    return g;
+}
+
+}  // namespace nfx
+
+using namespace nfx;
+
+extern "C" size_t nfx_affine_train_pack_floats(int d, int H) {
+    const int D = pad_d(d);
+    if (!D || H <= 0 || H > 64) return 0;
+    return (size_t)((train_layout(D, (H + 31) / 32).total + 3) & ~3);
+}
+
+extern "C" size_t nfx_affine_train_stats_doubles(int H) {
+    if (H <= 0) return 0;
+    return (size_t)2 * 32 * ((H + 31) / 32) * 3;
+}
+
+extern "C" size_t nfx_affine_train_grad_doubles(int d, int H) {
+    const int D = pad_d(d);
+    if (!D || H <= 0 || H > 64) return 0;
+    return (size_t)train_grad_layout(D, (H + 31) / 32).total;
+}
+
+extern "C" size_t nfx_affine_train_param_floats(int d, int H) {
+    if (d <= 0 || H <= 0) return 0;
+    return (size_t)2 * (H * d + H + 2 * H + H * H + H + 2 * H + d * H + d);
+}
+
+// Workspace: per-wave partials (max over passes) + the g_y1 tiles BWD2 hands to BWD3.
+extern "C" size_t nfx_affine_train_workspace_bytes(int64_t B, int d, int H) {
+    const int D = pad_d(d);
+    if (!D || H <= 0 || H > 64 || B < 0) return 0;
+    const int HT = (H + 31) / 32, Hp = 32 * HT;
+    const TrainGrad GL = train_grad_layout(D, HT);
+    const int64_t ntiles = (B + 31) / 32;
+    int64_t nw = 4 * (int64_t)num_cus() * 2;  // upper bound on resident waves (<= 2 WGs/CU)
+    const int64_t cap = 4 * ((ntiles + 3) / 4);
+    if (nw > cap) nw = cap < 4 ? 4 : cap;
+    size_t per_wave = (size_t)GL.len2 * sizeof(float);
+    const size_t st = (size_t)2 * Hp * 3 * sizeof(double);
+    if ((size_t)GL.len1 * sizeof(float) > per_wave) per_wave = (size_t)GL.len1 * sizeof(float);
+    if ((size_t)GL.len3 * sizeof(float) > per_wave) per_wave = (size_t)GL.len3 * sizeof(float);
+    if (st > per_wave) per_wave = st;
+    const size_t partials = ((size_t)nw * per_wave + 255) & ~(size_t)255;
+    return partials + (size_t)ntiles * 2 * HT * 1024 * sizeof(float);
+}
+
+extern "C" int nfx_affine_train_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, const float* mask,
+                                     const double* stats1, const double* stats2, int d, int H, float* tpack,
+                                     float* epack, void* stream) {
+    int rc = train_check(d, H, "affine_train_pack");
+    if (rc) return rc;
+    if (!s_net || !b_net || !mask || !tpack) return set_error(NFX_EINVAL, "affine_train_pack: null pointer");
+    if (epack && (!stats1 || !stats2)) return set_error(NFX_EINVAL, "affine_train_pack: eval pack needs both statistics");
+    const NfxMlpRaw* nets[2] = {s_net, b_net};
+    for (int n = 0; n < 2; ++n)
+        for (int l = 0; l < 3; ++l)
+            if (!nets[n]->w[l]) return set_error(NFX_EINVAL, "affine_train_pack: net %d layer %d weight is null", n, l);
+    const int D = pad_d(d);
+    const int total = (int)nfx_affine_train_pack_floats(d, H);
+    int blocks = (total + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    affine_train_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*s_net, *b_net, mask, stats1, stats2, d, D, H,
+                                                                      tpack, epack);
+    return check_launch("affine_train_pack_kernel");
+}
+
+extern "C" int nfx_affine_train_stats(const float* tpack, const float* x, int64_t B, int d, int H, int layer,
+                                      double* stats, void* workspace, void* stream) {
+    int rc = train_check(d, H, "affine_train_stats");
+    if (rc) return rc;
+    if (layer != 1 && layer != 2) return set_error(NFX_EINVAL, "affine_train_stats: layer must be 1 or 2");
+    if (B < 1) return set_error(NFX_EINVAL, "affine_train_stats: batch statistics need B >= 1 (B=%lld)", (long long)B);
+    if (!tpack || !x || !stats || !workspace) return set_error(NFX_EINVAL, "affine_train_stats: null pointer");
+    const int D = pad_d(d), HT = (H + 31) / 32, Hp = 32 * HT;
+    affine_train_kernel_t k = pick_train(HT, D, layer == 1 ? TS_STATS1 : TS_STATS2);
+    const size_t lds = affine_train_lds(D, HT);
+    if ((rc = prepare_lds((const void*)k, lds))) return rc;
+    const TrainGrid g = train_grid(k, lds, B);
+    hipStream_t s = (hipStream_t)stream;
+    k<<<g.grid, 256, lds, s>>>(tpack, x, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, workspace, B, d, 1,
+                               g.ntiles);
+    if ((rc = check_launch("affine_train_kernel(stats)"))) return rc;
+    affine_train_stats_finish<<<(2 * Hp + 127) / 128, 128, 0, s>>>(reinterpret_cast<const double*>(workspace),
+                                                                   g.nwaves, Hp, stats);
+    return check_launch("affine_train_stats_finish");
+}
+
+extern "C" int nfx_affine_train_update_running(const double* stats1, const double* stats2, float* const* running_mean,
+                                               float* const* running_var, int H, double momentum, void* stream) {
+    if (!stats1 || !stats2 || !running_mean || !running_var || H <= 0)
+        return set_error(NFX_EINVAL, "affine_train_update_running: bad arguments");
+    NfxBnPtrs p;
+    for (int k = 0; k < 4; ++k) {
+        p.rm[k] = running_mean[k];
+        p.rv[k] = running_var[k];
+    }
+    const int Hp = 32 * ((H + 31) / 32);
+    affine_train_running_kernel<<<(4 * H + 255) / 256, 256, 0, (hipStream_t)stream>>>(stats1, stats2, p, H, Hp, momentum);
+    return check_launch("affine_train_running_kernel");
+}
+
+extern "C" int nfx_affine_train_backward(const float* tpack, const float* x, const float* gy, const float* gld,
+                                         float* gx, int64_t B, int d, int H, int direction, int stage,
+                                         const double* stats2, double* G, void* workspace, void* stream) {
+    int rc = train_check(d, H, "affine_train_backward");
+    if (rc) return rc;
+    if (stage < 1 || stage > 3) return set_error(NFX_EINVAL, "affine_train_backward: stage must be 1, 2 or 3");
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE)
+        return set_error(NFX_EINVAL, "affine_train_backward: direction must be +1 or -1");
+    if (B < 1) return set_error(NFX_EINVAL, "affine_train_backward: B >= 1 required");
+    if (!tpack || !x || !gx || !G || !workspace || !stats2 || (stage < 3 && (!gy || !gld)))
+        return set_error(NFX_EINVAL, "affine_train_backward: null pointer");
+    const int D = pad_d(d), HT = (H + 31) / 32;
+    const TrainGrad GL = train_grad_layout(D, HT);
+    const int ts = stage == 1 ? TS_BWD1 : (stage == 2 ? TS_BWD2 : TS_BWD3);
+    affine_train_kernel_t k = pick_train(HT, D, ts);
+    const size_t lds = affine_train_lds(D, HT);
+    if ((rc = prepare_lds((const void*)k, lds))) return rc;
+    const TrainGrid g = train_grid(k, lds, B);
+    // partials first, then the g_y1 tiles (same offsets as nfx_affine_train_workspace_bytes)
+    const size_t full = nfx_affine_train_workspace_bytes(B, d, H);
+    const size_t gbytes = (size_t)g.ntiles * 2 * HT * 1024 * sizeof(float);
+    char* ws = reinterpret_cast<char*>(workspace);
+    float* gbuf = reinterpret_cast<float*>(ws + (full - gbytes));
+    hipStream_t s = (hipStream_t)stream;
+    k<<<g.grid, 256, lds, s>>>(tpack, x, gy, gld, gx, gbuf, G, stats2, workspace, B, d, direction, g.ntiles);
+    if ((rc = check_launch("affine_train_kernel(backward)"))) return rc;
+    const int off = stage == 1 ? GL.g1s : (stage == 2 ? GL.g2s : GL.g3w);
+    const int len = stage == 1 ? GL.len1 : (stage == 2 ? GL.len2 : GL.len3);
+    affine_train_sum_finish<<<(len + 255) / 256, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), g.nwaves,
+                                                              len, G + off);
+    return check_launch("affine_train_sum_finish");
+}
+
+extern "C" int nfx_affine_train_assemble(const double* G, const double* stats1, const double* stats2, int d, int H,
+                                         float eps, float* grads, void* stream) {
+    int rc = train_check(d, H, "affine_train_assemble");
+    if (rc) return rc;
+    if (!G || !stats1 || !stats2 || !grads) return set_error(NFX_EINVAL, "affine_train_assemble: null pointer");
+    const int n = (int)nfx_affine_train_param_floats(d, H);
+    int blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    affine_train_assemble_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(G, stats1, stats2, d, pad_d(d), H,
+                                                                          (double)eps, grads);
+    return check_launch("affine_train_assemble_kernel");
+}

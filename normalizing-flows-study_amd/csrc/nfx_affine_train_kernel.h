@@ -1,0 +1,658 @@
+// Train-mode affine coupling (RealNVP CouplingLayer with batch-statistics BatchNorm) and its
+// backward, for gfx950. See nfx_affine_train.hip for the pass structure and the math.
+//
+// Every kernel here walks the batch in 32-sample tiles, one tile per wave per iteration
+// (grid-stride), with the conditioner MLPs on fp32 MFMA exactly like the eval kernel: hidden
+// activations in accumulator layout, "hidden-unit rows x sample columns" (nfx_common.h).
+// Reductions over the SAMPLE dimension (BatchNorm statistics, weight and BN-parameter
+// gradients) need the sample index off the lane: a per-wave LDS transpose turns an
+// accumulator tile into lane l <-> feature (l & 31), samples 16*(l >> 5) + t (t = 0..15).
+// In that layout the per-feature sums are lane-local adds, and a weight gradient
+// dW = sum_s P[:, s] Q[:, s]^T is an MFMA whose k dimension runs over samples
+// (A = P^T-tile, B = Q^T-tile, both in the transposed layout).
+#pragma once
+#include "nfx_common.h"
+
+namespace nfx {
+
+enum TrainStage { TS_STATS1 = 0, TS_STATS2 = 1, TS_BWD1 = 2, TS_BWD2 = 3, TS_BWD3 = 4 };
+
+constexpr int kTS = 36;  // row stride (floats) of a per-wave 32 x 32 transpose buffer
+
+// Train pack, per net (floats). BatchNorm enters as x^ = (h - mu) * r, r = 1/sqrt(var + eps)
+// folded into the linear layer ("identity fold": mu = 0, r = 1 when the statistics of that layer
+// are not known yet), then y = gamma * x^ + beta on the VALU:
+//   w1  [HT][KS1][64]       A operand of diag(r1) W1          (columns = inputs)
+//   c1  [HT][32]            r1 (b1 - mu1)                       accumulator order [tile][half][16]
+//   g1  [HT][32], e1 [HT][32]   gamma1, beta1                   accumulator order
+//   w2  [HT][HT][4][64][4]  A operand of diag(r2) W2            [out tile][k tile][r/4][lane][r%4]
+//   c2, g2, e2 [HT][32]
+//   w3  [D][HT][32]         W3[j][row]                          accumulator order
+//   b3  [D]
+//   w2t [HT][HT][4][64][4]  A operand of (diag(r2) W2)^T         [in tile][out tile][..]
+//   w1c [D][HT][32]         (diag(r1) W1)[row][j]              accumulator order
+// then mask [D] (padding columns j >= d: mask 1, zero weights).
+struct TrainLayout {
+    int D, HT, KS1;
+    int w1, c1, g1, e1, w2, c2, g2, e2, w3, b3, w2t, w1c, net, mask, total;
+};
+
+__host__ __device__ constexpr TrainLayout train_layout(int D, int HT) {
+    TrainLayout L{};
+    L.D = D;
+    L.HT = HT;
+    L.KS1 = (D + 1) / 2;
+    int o = 0;
+    L.w1 = o; o += HT * L.KS1 * 64;
+    L.c1 = o; o += HT * 32;
+    L.g1 = o; o += HT * 32;
+    L.e1 = o; o += HT * 32;
+    L.w2 = o; o += HT * HT * 1024;
+    L.c2 = o; o += HT * 32;
+    L.g2 = o; o += HT * 32;
+    L.e2 = o; o += HT * 32;
+    L.w3 = o; o += D * HT * 32;
+    L.b3 = o; o += (D + 3) & ~3;
+    L.w2t = o; o += HT * HT * 1024;
+    L.w1c = o; o += D * HT * 32;
+    L.net = o;
+    L.mask = 2 * o;
+    L.total = 2 * o + ((D + 3) & ~3);
+    return L;
+}
+
+// Per-wave partial lengths (floats, doubles for the statistics) and the layout of the float64
+// gradient-sum vector G (one per layer; a stage's partials have exactly its G block's layout):
+//   g1s [2 nets][2][Hp]        BWD1: sum g_y2, sum g_y2 * x^2     (BN2 backward sums)
+//   g1w [2 nets][D*Hp + D]     BWD1: dW3 [D][Hp], db3 [D]
+//   g2s [2 nets][2][Hp]        BWD2: sum g_y1, sum g_y1 * x^1     (BN1 backward sums)
+//   g2w [2 nets][Hp*Hp + Hp]   BWD2: sum e2 a1^T [Hp][Hp], sum e2 [Hp]   (dW2 = diag(r2) .)
+//   g3w [2 nets][D*Hp + Hp]    BWD3: sum e1 xa^T stored [D][Hp], sum e1 [Hp]  (dW1 = diag(r1) .)
+struct TrainGrad {
+    int Hp, D;
+    int g1s, g1w, g2s, g2w, g3w, total;
+    int len1, len2, len3;  // per-stage block lengths (contiguous from g1s, g2s, g3w)
+};
+
+__host__ __device__ constexpr TrainGrad train_grad_layout(int D, int HT) {
+    TrainGrad g{};
+    const int Hp = 32 * HT;
+    g.Hp = Hp;
+    g.D = D;
+    int o = 0;
+    g.g1s = o; o += 4 * Hp;
+    g.g1w = o; o += 2 * (D * Hp + D);
+    g.g2s = o; o += 4 * Hp;
+    g.g2w = o; o += 2 * (Hp * Hp + Hp);
+    g.g3w = o; o += 2 * (D * Hp + Hp);
+    g.total = o;
+    g.len1 = g.g2s - g.g1s;
+    g.len2 = g.g3w - g.g2s;
+    g.len3 = g.total - g.g3w;
+    return g;
+}
+
+// Accumulator tile X (lane l, reg r = X[crow(r, h)][l & 31]) -> T[t] = X[l & 31][16h + t].
+// buf: this wave's 32 x kTS LDS region. A wave's LDS instructions execute in order, so the
+// write -> read (other lanes) and read -> next write sequences need no barrier.
+__device__ __forceinline__ void transpose_tile(float* buf, const f32x16& X, float (&T)[16]) {
+    const int l = lane_id(), h = l >> 5, c = l & 31;
+    f32x4* wp = reinterpret_cast<f32x4*>(buf + c * kTS + 4 * h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wp[2 * q] = f32x4{X[4 * q], X[4 * q + 1], X[4 * q + 2], X[4 * q + 3]};
+    __builtin_amdgcn_wave_barrier();
+    const float* rp = buf + (16 * h) * kTS + c;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) T[t] = rp[t * kTS];
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Chan et al. pairwise combination of (count, mean, M2) — the stable parallel variance.
+__device__ __forceinline__ void chan_merge(double& n, double& mean, double& m2, double nb, double meanb,
+                                           double m2b) {
+    const double nt = n + nb;
+    if (nb == 0.0) return;
+    const double dl = meanb - mean;
+    mean = mean + dl * (nb / nt);
+    m2 = m2 + m2b + dl * dl * (n * nb / nt);
+    n = nt;
+}
+
+template <int D>
+struct TrainRow {
+    float v[D];
+};
+
+template <int HT, int D, int STAGE>
+__global__ __launch_bounds__(256) void affine_train_kernel(
+    const float* __restrict__ pack, const float* __restrict__ x, const float* __restrict__ gy,
+    const float* __restrict__ gld, float* __restrict__ gx, float* __restrict__ gbuf,
+    const double* __restrict__ G, const double* __restrict__ stats2, void* __restrict__ part,
+    int64_t B, int d, int dir, int64_t ntiles) {
+    constexpr TrainLayout L = train_layout(D, HT);
+    constexpr TrainGrad GL = train_grad_layout(D, HT);
+    constexpr int KS1 = L.KS1;
+    constexpr int Hp = 32 * HT;
+    constexpr int PACKF = (L.total + 3) & ~3;
+    extern __shared__ f32x4 lds4[];
+    float* sm = reinterpret_cast<float*>(lds4);
+    float* tbuf_all = sm + PACKF;                        // 4 x 32 x kTS
+    float* sbuf_all = tbuf_all + 4 * 32 * kTS;           // 4 x 32 x (2D)  per-sample scratch
+    float* kc = sbuf_all + 4 * 32 * 2 * D;               // [2 nets][2][Hp] BN-backward constants
+    {
+        const f32x4* src = reinterpret_cast<const f32x4*>(pack);
+        for (int i = threadIdx.x; i < PACKF / 4; i += 256) lds4[i] = src[i];
+    }
+    if constexpr (STAGE == TS_BWD2 || STAGE == TS_BWD3) {
+        // k1 = sum g / N, k2 = sum g x^ / N in accumulator order, N = the batch the statistics
+        // were taken over (all ranks under SyncBN)
+        const double N = stats2[0];
+        const double* S = G + (STAGE == TS_BWD2 ? GL.g1s : GL.g2s);
+        for (int i = threadIdx.x; i < 4 * Hp; i += 256) {
+            const int n = i / (2 * Hp), q = (i / Hp) & 1, a = i % Hp;  // a: accumulator index
+            const int ht = a >> 5, hh = (a >> 4) & 1, r = a & 15;
+            const int row = 32 * ht + crow(r, hh);
+            kc[i] = (float)(S[(n * 2 + q) * Hp + row] / N);
+        }
+    }
+    __syncthreads();
+
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31, wave = threadIdx.x >> 6;
+    float* tbuf = tbuf_all + wave * 32 * kTS;
+    float* sbuf = sbuf_all + wave * 32 * 2 * D;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + wave;
+
+    float mk[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) mk[j] = sm[L.mask + j];
+
+    // ---- per-lane accumulators ------------------------------------------------------------
+    // statistics: shift, sum, sum of squares per (net, tile) in the transposed layout
+    float st_c[2][HT];
+    double st_s1[2][HT], st_s2[2][HT];
+    double st_n = 0.0;
+    // backward sums (transposed layout unless noted)
+    float ac_s1[2][HT], ac_s2[2][HT];   // BWD1/BWD2: sum g, sum g x^;  BWD3: sum e1 (ac_s1)
+    float ac_w[2][HT][D];               // BWD1: dW3 (per j);  BWD3: dW1 (per j)
+    float ac_b[2][D];                   // BWD1: db3 (epilogue layout, half 0)
+    float ac_db[2][HT];                 // BWD2: sum e2
+    f32x16 ac_dw[2][HT][HT];            // BWD2: sum e2 a1^T (accumulator layout)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            st_c[n][ht] = 0.f;
+            st_s1[n][ht] = st_s2[n][ht] = 0.0;
+            ac_s1[n][ht] = ac_s2[n][ht] = ac_db[n][ht] = 0.f;
+#pragma unroll
+            for (int j = 0; j < D; ++j) ac_w[n][ht][j] = 0.f;
+            if constexpr (STAGE == TS_BWD2) {
+#pragma unroll
+                for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) ac_dw[n][ht][kt][r] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) ac_b[n][j] = 0.f;
+    }
+
+    bool first = true;
+    for (int64_t tile = wid; tile < ntiles; tile += nwaves) {
+        const int64_t base = tile * 32;
+        const int64_t s = base + col;
+        const bool valid = s < B;
+        const float* smi = sm + opaque_zero();
+        // the lane's sample row (both lane halves hold the same sample)
+        float xr[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) xr[j] = (valid && j < d) ? x[s * d + j] : 0.f;
+        float xb[KS1];  // layer-1 B operand: xa[sample col][2ks + h]
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) {
+            const float v0 = xr[2 * ks] * mk[2 * ks];
+            const float v1 = (2 * ks + 1 < D) ? xr[2 * ks + 1] * mk[2 * ks + 1] : 0.f;
+            xb[ks] = h ? v1 : v0;
+        }
+        // samples of this tile in the lane's transposed half: 16h + t valid for t < nvh
+        const int64_t rem = B - base - 16 * h;
+        const int nvh = rem <= 0 ? 0 : (rem >= 16 ? 16 : (int)rem);
+
+        auto layer1 = [&](const float* P, f32x16 (&acc)[HT]) {
+#pragma unroll
+            for (int ht = 0; ht < HT; ++ht) {
+                f32x16 a = load_bias16(P + L.c1 + ht * 32, h);
+#pragma unroll
+                for (int ks = 0; ks < KS1; ++ks) a = mfma32(P[L.w1 + (ht * KS1 + ks) * 64 + lane], xb[ks], a);
+                acc[ht] = a;
+            }
+        };
+        // a1 = relu(gamma1 x^1 + beta1) in place (keeps x^1 in xh, writes a1 into act)
+        auto bn_relu = [&](const float* gp, const float* ep, const f32x16 (&xh)[HT], f32x16 (&act)[HT]) {
+#pragma unroll
+            for (int ht = 0; ht < HT; ++ht) {
+                const f32x16 g = load_bias16(gp + ht * 32, h), e = load_bias16(ep + ht * 32, h);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) act[ht][r] = trelu(fmaf(g[r], xh[ht][r], e[r]));
+            }
+        };
+        auto layer2 = [&](const float* P, const f32x16 (&act)[HT], f32x16 (&acc)[HT]) {
+            const f32x4* wg = reinterpret_cast<const f32x4*>(P + L.w2) + lane;
+#pragma unroll
+            for (int o = 0; o < HT; ++o) {
+                f32x16 a = load_bias16(P + L.c2 + o * 32, h);
+#pragma unroll
+                for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                    for (int rq = 0; rq < 4; ++rq) {
+                        const f32x4 w = wg[((o * HT + kt) * 4 + rq) * 64];
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], act[kt][4 * rq + rr], a);
+                    }
+                acc[o] = a;
+            }
+        };
+        // statistics of an accumulator tile (transposed; invalid samples excluded)
+        auto stats_tile = [&](int n, int ht, const f32x16& X) {
+            float T[16];
+            transpose_tile(tbuf, X, T);
+            if (first) st_c[n][ht] = T[0];
+            const float c = st_c[n][ht];
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const float v = t < nvh ? T[t] - c : 0.f;
+                s1 += v;
+                s2 = fmaf(v, v, s2);
+            }
+            st_s1[n][ht] += (double)s1;
+            st_s2[n][ht] += (double)s2;
+        };
+
+        if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const float* P = smi + n * L.net;
+                f32x16 xh1[HT];
+                layer1(P, xh1);
+                if constexpr (STAGE == TS_STATS1) {
+#pragma unroll
+                    for (int ht = 0; ht < HT; ++ht) stats_tile(n, ht, xh1[ht]);
+                } else {
+                    f32x16 a1[HT], h2[HT];
+                    bn_relu(P + L.g1, P + L.e1, xh1, a1);
+                    layer2(P, a1, h2);
+#pragma unroll
+                    for (int ht = 0; ht < HT; ++ht) stats_tile(n, ht, h2[ht]);
+                }
+            }
+            st_n += (double)nvh;
+        } else if constexpr (STAGE == TS_BWD1 || STAGE == TS_BWD2) {
+            // ---- recompute the forward of both nets (layer-2 x^2 kept for both) ----------
+            f32x16 xh2[2][HT];
+            float outv[2][D];
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const float* P = smi + n * L.net;
+                f32x16 xh1[HT], a1[HT];
+                layer1(P, xh1);
+                bn_relu(P + L.g1, P + L.e1, xh1, a1);
+                layer2(P, a1, xh2[n]);
+                float pj[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) pj[j] = 0.f;
+#pragma unroll
+                for (int o = 0; o < HT; ++o) {
+                    const f32x16 g = load_bias16(P + L.g2 + o * 32, h), e = load_bias16(P + L.e2 + o * 32, h);
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + o) * 32, h);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            pj[j] = fmaf(w3[r], trelu(fmaf(g[r], xh2[n][o][r], e[r])), pj[j]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j) outv[n][j] = halves_sum(pj[j], pj[j]) + P[L.b3 + j];
+            }
+            // ---- epilogue backward (coupling_layer.py:40-96 under autograd) ---------------
+            const float gl_in = valid ? gld[s] : 0.f;
+            float gyr[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) gyr[j] = (valid && j < d) ? gy[s * d + j] : 0.f;
+            float dl[2][D], gxd[D];
+            {
+#pragma clang fp contract(off)
+                float ld = 0.f;
+                float ev[D], sv[D], bv[D];
+                bool fy[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    sv[j] = tclamp(outv[0][j], -10.f, 10.f);
+                    bv[j] = tclamp(outv[1][j], -10.f, 10.f);
+                    const float m = mk[j], om = 1.f - m;
+                    float t;
+                    if (dir < 0) {
+                        ev[j] = exp_fast(-sv[j]);
+                        t = (xr[j] - bv[j]) * ev[j];
+                        ld = ld + om * (-sv[j]);
+                    } else {
+                        ev[j] = exp_fast(sv[j]);
+                        t = xr[j] * ev[j] + bv[j];
+                        ld = ld + om * sv[j];
+                    }
+                    fy[j] = !nonfinite(xr[j] * m + om * t);
+                }
+                const float gl = nonfinite(ld) ? 0.f : gl_in;
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const float m = mk[j], om = 1.f - m;
+                    const float gv = (fy[j] && j < d) ? gyr[j] : 0.f;
+                    const float gt = gv * om;  // d v / d t = (1 - m)
+                    float gs, gb;
+                    if (dir < 0) {  // t = (x - b) * exp(-s); ld = sum (1-m)(-s)
+                        gs = (gt * (xr[j] - bv[j])) * (-ev[j]) + gl * (-om);
+                        gb = -(gt * ev[j]);
+                    } else {        // t = x * exp(s) + b;  ld = sum (1-m) s
+                        gs = (gt * xr[j]) * ev[j] + gl * om;
+                        gb = gt;
+                    }
+                    gxd[j] = gv * m + gt * ev[j];
+                    if (j >= d) gs = gb = 0.f;
+                    // torch.clamp backward: gradient where min <= input <= max
+                    dl[0][j] = (outv[0][j] >= -10.f && outv[0][j] <= 10.f) ? gs : 0.f;
+                    dl[1][j] = (outv[1][j] >= -10.f && outv[1][j] <= 10.f) ? gb : 0.f;
+                }
+            }
+            if constexpr (STAGE == TS_BWD1) {
+                if (h == 0 && valid) {
+#pragma unroll
+                    for (int j = 0; j < D; ++j)
+                        if (j < d) gx[s * d + j] = gxd[j];
+                }
+                // per-sample delta3 of both nets for the transposed dW3 sums
+                if (h == 0) {
+#pragma unroll
+                    for (int n = 0; n < 2; ++n)
+#pragma unroll
+                        for (int j = 0; j < D; ++j) sbuf[col * 2 * D + n * D + j] = dl[n][j];
+                }
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+#pragma unroll
+                    for (int j = 0; j < D; ++j) ac_b[n][j] += h == 0 ? dl[n][j] : 0.f;
+            }
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const float* P = smi + n * L.net;
+                f32x16 e2t[HT];  // BWD2: e2 of net n (accumulator layout)
+#pragma unroll
+                for (int o = 0; o < HT; ++o) {
+                    const f32x16 g = load_bias16(P + L.g2 + o * 32, h), e = load_bias16(P + L.e2 + o * 32, h);
+                    f32x16 gy2, a2;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float y2 = fmaf(g[r], xh2[n][o][r], e[r]);
+                        a2[r] = trelu(y2);
+                        gy2[r] = 0.f;
+                    }
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + o) * 32, h);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) gy2[r] = fmaf(w3[r], dl[n][j], gy2[r]);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) gy2[r] = a2[r] > 0.f ? gy2[r] : 0.f;  // relu backward
+                    if constexpr (STAGE == TS_BWD1) {
+                        float Tg[16], Tx[16], Ta[16];
+                        transpose_tile(tbuf, gy2, Tg);
+                        transpose_tile(tbuf, xh2[n][o], Tx);
+                        transpose_tile(tbuf, a2, Ta);
+                        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) {
+                            s1 += Tg[t];
+                            s2 = fmaf(Tg[t], Tx[t], s2);
+                        }
+                        ac_s1[n][o] += s1;
+                        ac_s2[n][o] += s2;
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            float w = 0.f;
+#pragma unroll
+                            for (int t = 0; t < 16; ++t) w = fmaf(sbuf[(16 * h + t) * 2 * D + n * D + j], Ta[t], w);
+                            ac_w[n][o][j] += w;
+                        }
+                    } else {
+                        // e2 = gamma2 (g_y2 - k1 - x^2 k2)  (BatchNorm backward with batch statistics)
+                        const f32x16 k1 = load_bias16(kc + (n * 2 + 0) * Hp + o * 32, h);
+                        const f32x16 k2 = load_bias16(kc + (n * 2 + 1) * Hp + o * 32, h);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const float v = g[r] * ((gy2[r] - k1[r]) - xh2[n][o][r] * k2[r]);
+                            e2t[o][r] = valid ? v : 0.f;
+                        }
+                    }
+                }
+                if constexpr (STAGE == TS_BWD2) {
+                    // a1 of net n again (layer 1 is K = d: cheap), its pre-activation y1 for the ReLU
+                    f32x16 xh1[HT], a1[HT];
+                    layer1(P, xh1);
+                    bn_relu(P + L.g1, P + L.e1, xh1, a1);
+                    float Te[HT][16];
+#pragma unroll
+                    for (int o = 0; o < HT; ++o) {
+                        transpose_tile(tbuf, e2t[o], Te[o]);
+                        float sb = 0.f;
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) sb += Te[o][t];
+                        ac_db[n][o] += sb;
+                    }
+#pragma unroll
+                    for (int kt = 0; kt < HT; ++kt) {
+                        float Ta[16];
+                        transpose_tile(tbuf, a1[kt], Ta);
+#pragma unroll
+                        for (int o = 0; o < HT; ++o)
+#pragma unroll
+                            for (int t = 0; t < 16; ++t) ac_dw[n][o][kt] = mfma32(Te[o][t], Ta[t], ac_dw[n][o][kt]);
+                    }
+                    // g_a1 = (diag(r2) W2)^T e2, relu backward, BN1 sums, g_y1 to HBM
+                    const f32x4* wt = reinterpret_cast<const f32x4*>(P + L.w2t) + lane;
+#pragma unroll
+                    for (int kt = 0; kt < HT; ++kt) {
+                        f32x16 ga;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) ga[r] = 0.f;
+#pragma unroll
+                        for (int o = 0; o < HT; ++o)
+#pragma unroll
+                            for (int rq = 0; rq < 4; ++rq) {
+                                const f32x4 w = wt[((kt * HT + o) * 4 + rq) * 64];
+#pragma unroll
+                                for (int rr = 0; rr < 4; ++rr) ga = mfma32(w[rr], e2t[o][4 * rq + rr], ga);
+                            }
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) ga[r] = a1[kt][r] > 0.f ? ga[r] : 0.f;
+                        float* gp = gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64 + lane;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) gp[r * 64] = ga[r];
+                        float Tg[16], Tx[16];
+                        transpose_tile(tbuf, ga, Tg);
+                        transpose_tile(tbuf, xh1[kt], Tx);
+                        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) {
+                            s1 += Tg[t];
+                            s2 = fmaf(Tg[t], Tx[t], s2);
+                        }
+                        ac_s1[n][kt] += s1;
+                        ac_s2[n][kt] += s2;
+                    }
+                }
+            }
+        } else {  // TS_BWD3: layer 1 only
+            if (h == 0) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) sbuf[col * 2 * D + j] = xr[j] * mk[j];
+            }
+            float gp[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) gp[j] = 0.f;
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const float* P = smi + n * L.net;
+                f32x16 xh1[HT];
+                layer1(P, xh1);
+#pragma unroll
+                for (int kt = 0; kt < HT; ++kt) {
+                    const float* gq = gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64 + lane;
+                    const f32x16 g = load_bias16(P + L.g1 + kt * 32, h);
+                    const f32x16 k1 = load_bias16(kc + (n * 2 + 0) * Hp + kt * 32, h);
+                    const f32x16 k2 = load_bias16(kc + (n * 2 + 1) * Hp + kt * 32, h);
+                    f32x16 e1;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float v = g[r] * ((gq[r * 64] - k1[r]) - xh1[kt][r] * k2[r]);
+                        e1[r] = valid ? v : 0.f;
+                    }
+                    float Te[16];
+                    transpose_tile(tbuf, e1, Te);
+                    float sb = 0.f;
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) sb += Te[t];
+                    ac_s1[n][kt] += sb;
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        float w = 0.f;
+#pragma unroll
+                        for (int t = 0; t < 16; ++t) w = fmaf(sbuf[(16 * h + t) * 2 * D + j], Te[t], w);
+                        ac_w[n][kt][j] += w;
+                        const f32x16 wc = load_bias16(P + L.w1c + (j * HT + kt) * 32, h);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) gp[j] = fmaf(wc[r], e1[r], gp[j]);
+                    }
+                }
+            }
+            float gxa[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) gxa[j] = halves_sum(gp[j], gp[j]);
+            if (h == 0 && valid) {
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    if (j < d) gx[s * d + j] = gx[s * d + j] + mk[j] * gxa[j];
+            }
+        }
+        first = false;
+    }
+
+    // ---- per-wave partials ------------------------------------------------------------------
+    if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
+        // per lane (n, mean, M2) of its half's samples; merge the two halves (same features)
+        double* pw = reinterpret_cast<double*>(part) + wid * (2 * Hp * 3);
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int ht = 0; ht < HT; ++ht) {
+                double cnt = st_n, mean = 0.0, m2 = 0.0;
+                if (cnt > 0.0) {
+                    mean = (double)st_c[n][ht] + st_s1[n][ht] / cnt;
+                    m2 = st_s2[n][ht] - st_s1[n][ht] * st_s1[n][ht] / cnt;
+                    if (m2 < 0.0) m2 = 0.0;
+                }
+                const double nb = __shfl_xor(cnt, 32, 64), mb = __shfl_xor(mean, 32, 64), qb = __shfl_xor(m2, 32, 64);
+                if (h == 0) {
+                    if (cnt == 0.0) { cnt = nb; mean = mb; m2 = qb; }
+                    else chan_merge(cnt, mean, m2, nb, mb, qb);
+                    double* q = pw + (n * Hp + 32 * ht + col) * 3;
+                    q[0] = cnt;
+                    q[1] = mean;
+                    q[2] = m2;
+                }
+            }
+    } else {
+        float* pw = reinterpret_cast<float*>(part);
+        if constexpr (STAGE == TS_BWD1) {
+            pw += wid * GL.len1;
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht) {
+                    const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
+                    const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
+                    if (h == 0) {
+                        pw[(n * 2 + 0) * Hp + 32 * ht + col] = a;
+                        pw[(n * 2 + 1) * Hp + 32 * ht + col] = b;
+                    }
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const float w = halves_sum(ac_w[n][ht][j], ac_w[n][ht][j]);
+                        if (h == 0) pw[4 * Hp + n * (D * Hp + D) + j * Hp + 32 * ht + col] = w;
+                    }
+                }
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    float v = ac_b[n][j];
+#pragma unroll
+                    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                    if (lane == 0) pw[4 * Hp + n * (D * Hp + D) + D * Hp + j] = v;
+                }
+        } else if constexpr (STAGE == TS_BWD2) {
+            pw += wid * GL.len2;
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht) {
+                    const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
+                    const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
+                    const float c = halves_sum(ac_db[n][ht], ac_db[n][ht]);
+                    if (h == 0) {
+                        pw[(n * 2 + 0) * Hp + 32 * ht + col] = a;
+                        pw[(n * 2 + 1) * Hp + 32 * ht + col] = b;
+                        pw[4 * Hp + n * (Hp * Hp + Hp) + Hp * Hp + 32 * ht + col] = c;
+                    }
+                }
+                float* pdw = pw + 4 * Hp + n * (Hp * Hp + Hp);
+#pragma unroll
+                for (int o = 0; o < HT; ++o)
+#pragma unroll
+                    for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            pdw[(32 * o + crow(r, h)) * Hp + 32 * kt + col] = ac_dw[n][o][kt][r];
+            }
+        } else {
+            pw += wid * GL.len3;
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht) {
+                    const float c = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
+                    if (h == 0) pw[n * (D * Hp + Hp) + D * Hp + 32 * ht + col] = c;
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const float w = halves_sum(ac_w[n][ht][j], ac_w[n][ht][j]);
+                        if (h == 0) pw[n * (D * Hp + Hp) + j * Hp + 32 * ht + col] = w;
+                    }
+                }
+        }
+    }
+}
+
+typedef void (*affine_train_kernel_t)(const float*, const float*, const float*, const float*, float*, float*,
+                                      const double*, const double*, void*, int64_t, int, int, int64_t);
+
+template <int HT>
+affine_train_kernel_t affine_train_pick_ht(int D, int stage);
+
+// LDS bytes of affine_train_kernel<HT, D, *>
+__host__ __device__ constexpr size_t affine_train_lds(int D, int HT) {
+    return (size_t)(((train_layout(D, HT).total + 3) & ~3) + 4 * 32 * kTS + 4 * 32 * 2 * D + 4 * 32 * HT) *
+           sizeof(float);
+}
+
+}  // namespace nfx

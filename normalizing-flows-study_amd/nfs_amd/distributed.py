@@ -63,3 +63,56 @@ def average_gradients(module, group=None):
         p.grad.copy_(flat[o:o + n].view_as(p))
         o += n
 
+
+
+# ---------------------------------------------------------------------------------------------
+# SyncBN for data-parallel TRAINING of coupling layers (SURVEY.md §8(e) "when it breaks", §8(f)
+# item 2). In train mode CouplingLayer's BatchNorm1d normalises with batch statistics
+# (coupling_layer.py:18-35), so a sample-sharded step only equals the full-batch step if the
+# statistics and the BatchNorm-backward sums are taken over ALL ranks. The train-mode kernels
+# (csrc/nfx_affine_train.hip) hand the host exact float64 pieces between passes:
+#   * statistics triples (n, mean, M2) per feature -> all_gather + Chan merge (merge_bn_stats)
+#   * backward sums (sum g, sum g x^) per feature   -> all_reduce SUM (allreduce_bn_sums)
+# Off by default: a single process reproduces the reference's single-process BatchNorm.
+# ---------------------------------------------------------------------------------------------
+_SYNC_BN = {"enabled": False, "group": None}
+
+
+def enable_sync_batchnorm(enabled=True, group=None):
+    """Take train-mode coupling BatchNorm statistics over every rank of `group` (SyncBN)."""
+    _SYNC_BN["enabled"] = bool(enabled)
+    _SYNC_BN["group"] = group
+
+
+def sync_bn_world():
+    """World size SyncBN reduces over (1 when disabled or not distributed)."""
+    if not _SYNC_BN["enabled"] or not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(_SYNC_BN["group"])
+
+
+def merge_bn_stats(stats):
+    """In place: per-rank float64 triples [..., 3] = (n, mean, M2) -> the triple of the union
+    of all ranks' samples (same on every rank; exact two-level merge in float64)."""
+    world = sync_bn_world()
+    if world == 1:
+        return stats
+    group = _SYNC_BN["group"]
+    parts = [torch.empty_like(stats) for _ in range(world)]
+    dist.all_gather(parts, stats.contiguous(), group=group)
+    g = torch.stack(parts)
+    n_r, mean_r, m2_r = g[..., 0], g[..., 1], g[..., 2]
+    n = n_r.sum(0)
+    mean = (n_r * mean_r).sum(0) / n.clamp_min(1.0)
+    m2 = m2_r.sum(0) + (n_r * (mean_r - mean) ** 2).sum(0)
+    stats[..., 0] = n
+    stats[..., 1] = mean
+    stats[..., 2] = m2
+    return stats
+
+
+def allreduce_bn_sums(t):
+    """In place SUM over the SyncBN group of a float64 block of BatchNorm-backward sums."""
+    if sync_bn_world() > 1:
+        dist.all_reduce(t, group=_SYNC_BN["group"])
+    return t

@@ -5,15 +5,60 @@ state_dict keys as the reference `CouplingLayer` (coupling_layer.py:5-111). On a
 in eval mode the layer runs as ONE fused gfx950 kernel (csrc/nfx_affine*.hip): both conditioner
 MLPs on fp32 MFMA with BatchNorm folded from its running statistics, the affine transform,
 the NaN/Inf guards and the log-det.
+
+In TRAIN mode (the reference's training loops, README.md:107-117 / plots/_common.py:194-211)
+the conditioner BatchNorm normalises with batch statistics; on a ROCm device that runs through
+the train-mode kernels (csrc/nfx_affine_train.hip, `_CouplingTrainFunction`): two statistics
+passes, the fused layer with the batch statistics folded in, and a three-pass fused backward
+(BatchNorm backward with batch statistics, weight gradients as MFMA contractions over the
+sample dimension). `nfs_amd.distributed.enable_sync_batchnorm()` takes those statistics over
+all data-parallel ranks (SyncBN).
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
 from .. import _lib
-from .flow import HipFlow
+from .. import distributed as _dist
+from .flow import HipFlow, STATS
 
 MAX_D = 8
 MAX_H = 128
+MAX_H_TRAIN = 64
+ctypes_vp = ctypes.c_void_p
+
+# (kernel-name, start-event, end-event) of every train-mode layer pass while a list is installed
+# here (bench.py roofline timing); None = no events.
+TRAIN_EVENTS = None
+
+
+def _pad_d(d):
+    return 2 if d <= 2 else (4 if d <= 4 else 8)
+
+
+class _CouplingTrainFunction(torch.autograd.Function):
+    """Train-mode CouplingLayer on the gfx950 kernels: forward (y, log_det) with batch-statistics
+    BatchNorm and running-statistics update; backward = the fused three-pass kernel."""
+
+    @staticmethod
+    def forward(ctx, layer, direction, x, *params):
+        y, ld, tpack, stats = layer._train_forward(x, direction)
+        ctx.layer = layer
+        ctx.direction = direction
+        ctx.tpack = tpack
+        ctx.stats = stats
+        ctx.save_for_backward(x)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, gy, gld):
+        (x,) = ctx.saved_tensors
+        gx, grads = ctx.layer._train_backward(x, gy, gld, ctx.direction, ctx.tpack, ctx.stats)
+        STATS["hip"] += 1
+        params = list(ctx.layer.parameters())
+        gparams = [g if p.requires_grad else None for p, g in zip(params, grads)]
+        return (None, None, gx, *gparams)
 
 
 class CouplingLayer(HipFlow):
@@ -66,9 +111,133 @@ class CouplingLayer(HipFlow):
         return self.s_net[0].out_features
 
     def _torch_only(self):
-        # Train-mode BatchNorm normalises with batch statistics (batch-global), which a
-        # per-sample fused kernel cannot reproduce; the eval hot path folds running stats.
+        # The eval kernel folds running statistics; train-mode BatchNorm goes through
+        # _dispatch -> _CouplingTrainFunction (or the composite when outside its family).
         return any(bn.training or bn.running_mean is None for bn in self._batchnorms())
+
+    # -- train mode (batch-statistics BatchNorm) ----------------------------------------------
+    def _train_ok(self, x):
+        bns = self._batchnorms()
+        if x.device.type != "cuda" or x.dtype != torch.float32 or x.dim() != 2:
+            return False
+        if not bns or not all(bn.training for bn in bns):
+            return False
+        if any(not bn.affine or not bn.track_running_stats or bn.momentum is None or bn.running_mean is None
+               for bn in bns):
+            return False
+        d, H = self.data_dim, self._hidden()
+        return x.shape[1] == d and d <= MAX_D and H <= MAX_H_TRAIN and x.shape[0] >= 2
+
+    def _dispatch(self, x, direction):
+        if self._train_ok(x):
+            STATS["hip"] += 1
+            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+                return _CouplingTrainFunction.apply(self, direction, x, *list(self.parameters()))
+            y, ld, _, _ = self._train_forward(x, direction)
+            return y, ld
+        return super()._dispatch(x, direction)
+
+    def _raw_nets(self):
+        s_raw, k1 = _lib.mlp_raw([self.s_net[0], self.s_net[3], self.s_net[6]], [self.s_net[1], self.s_net[4]])
+        b_raw, k2 = _lib.mlp_raw([self.b_net[0], self.b_net[3], self.b_net[6]], [self.b_net[1], self.b_net[4]])
+        return s_raw, b_raw, (k1, k2)
+
+    def _train_forward(self, x, direction):
+        """Batch statistics (2 passes, SyncBN merge between them), the fused layer with the
+        statistics folded in, running-statistics update. Returns (y, ld, tpack, stats)."""
+        L = _lib.lib()
+        x = x.detach().contiguous()
+        B, d = x.shape
+        H = self._hidden()
+        dev = x.device
+        st = _lib.stream_of(x)
+        s_raw, b_raw, keep = self._raw_nets()
+        mask = self.mask.detach().to(device=dev, dtype=torch.float32).contiguous()
+        nst = L.nfx_affine_train_stats_doubles(H)
+        stats = torch.empty(2, nst, device=dev, dtype=torch.float64)
+        tpack = torch.empty(L.nfx_affine_train_pack_floats(d, H), device=dev, dtype=torch.float32)
+        epack = torch.empty(L.nfx_affine_packed_floats(d, H), device=dev, dtype=torch.float32)
+        ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
+        ev = TRAIN_EVENTS
+        p = _lib.ptr
+        _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), None, None, d, H, p(tpack), None, st),
+                   "nfx_affine_train_pack")
+        for layer in (1, 2):
+            if ev is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            _lib.check(L.nfx_affine_train_stats(p(tpack), p(x), B, d, H, layer, p(stats[layer - 1]), p(ws), st),
+                       "nfx_affine_train_stats")
+            if ev is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                ev.append((f"affine_train_kernel<STATS{layer}>", e0, e1))
+            _dist.merge_bn_stats(stats[layer - 1].view(2, -1, 3))
+            _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), p(stats[0]),
+                                               p(stats[1]) if layer == 2 else None, d, H, p(tpack),
+                                               p(epack) if layer == 2 else None, st), "nfx_affine_train_pack")
+        y = torch.empty_like(x)
+        ld = torch.empty(B, device=dev, dtype=torch.float32)
+        if ev is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _lib.check(L.nfx_affine_coupling(p(epack), p(x), p(y), p(ld), B, d, H, int(direction), 0, st),
+                   "nfx_affine_coupling")
+        if ev is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            ev.append(("affine_coupling_kernel", e0, e1))
+        bns = [self.s_net[1], self.s_net[4], self.b_net[1], self.b_net[4]]
+        rm = (ctypes_vp * 4)(*[bn.running_mean.data_ptr() for bn in bns])
+        rv = (ctypes_vp * 4)(*[bn.running_var.data_ptr() for bn in bns])
+        _lib.check(L.nfx_affine_train_update_running(p(stats[0]), p(stats[1]), rm, rv, H,
+                                                     float(bns[0].momentum), st), "nfx_affine_train_update_running")
+        for bn in bns:
+            torch.autograd.graph.increment_version(bn.running_mean)
+            torch.autograd.graph.increment_version(bn.running_var)
+        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
+        tpack._nfx_keep = (keep, mask, epack, ws)  # sources alive while the kernels are queued
+        return y, ld, tpack, stats
+
+    def _train_backward(self, x, gy, gld, direction, tpack, stats):
+        """dL/dx and the parameter gradients (parameters() order) of one train-mode call."""
+        L = _lib.lib()
+        x = x.contiguous()
+        B, d = x.shape
+        H = self._hidden()
+        dev = x.device
+        st = _lib.stream_of(x)
+        gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
+        gld = torch.zeros(B, device=dev) if gld is None else gld.contiguous().float()
+        G = torch.empty(L.nfx_affine_train_grad_doubles(d, H), device=dev, dtype=torch.float64)
+        gx = torch.empty_like(x)
+        ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
+        Hp, D = 32 * ((H + 31) // 32), _pad_d(d)
+        s_blocks = {1: G[0:4 * Hp], 2: G[4 * Hp + 2 * (D * Hp + D):][:4 * Hp]}
+        p = _lib.ptr
+        ev = TRAIN_EVENTS
+        for stage in (1, 2, 3):
+            if ev is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            _lib.check(L.nfx_affine_train_backward(p(tpack), p(x), p(gy), p(gld), p(gx), B, d, H, int(direction),
+                                                   stage, p(stats[1]), p(G), p(ws), st), "nfx_affine_train_backward")
+            if ev is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                ev.append((f"affine_train_kernel<BWD{stage}>", e0, e1))
+            if stage in s_blocks:
+                _dist.allreduce_bn_sums(s_blocks[stage])
+        grads = torch.empty(L.nfx_affine_train_param_floats(d, H), device=dev, dtype=torch.float32)
+        _lib.check(L.nfx_affine_train_assemble(p(G), p(stats[0]), p(stats[1]), d, H, float(self.s_net[1].eps),
+                                               p(grads), st), "nfx_affine_train_assemble")
+        out, o = [], 0
+        for prm in self.parameters():
+            n = prm.numel()
+            out.append(grads[o:o + n].view_as(prm))
+            o += n
+        grads._nfx_keep = (ws, G)
+        return gx, out
 
     def _hip_supported(self, x):
         d, H = self.data_dim, self._hidden()

@@ -46,25 +46,27 @@ def made_masks(d, H, mult=2):
 # ---------------------------------------------------------------------------------------------
 # Affine coupling — src/flows/coupling/coupling_layer.py:40-96
 # ---------------------------------------------------------------------------------------------
-def _coupling_net(sd, p, x):
-    """Linear -> BatchNorm1d(eval) -> ReLU -> Linear -> BatchNorm1d(eval) -> ReLU -> Linear
-    (coupling_layer.py:18-35); BatchNorm in eval mode uses running statistics."""
+def _coupling_net(sd, p, x, training=False):
+    """Linear -> BatchNorm1d -> ReLU -> Linear -> BatchNorm1d -> ReLU -> Linear
+    (coupling_layer.py:18-35). Eval: BatchNorm uses running statistics. training=True: batch
+    statistics, and the running statistics in `sd` are updated in place (momentum 0.1), as
+    nn.BatchNorm1d does in train mode."""
     h = F.linear(x, sd[p + "0.weight"], sd[p + "0.bias"])
     h = F.batch_norm(h, sd[p + "1.running_mean"], sd[p + "1.running_var"], sd[p + "1.weight"],
-                     sd[p + "1.bias"], False, 0.1, 1e-5)
+                     sd[p + "1.bias"], training, 0.1, 1e-5)
     h = F.relu(h)
     h = F.linear(h, sd[p + "3.weight"], sd[p + "3.bias"])
     h = F.batch_norm(h, sd[p + "4.running_mean"], sd[p + "4.running_var"], sd[p + "4.weight"],
-                     sd[p + "4.bias"], False, 0.1, 1e-5)
+                     sd[p + "4.bias"], training, 0.1, 1e-5)
     h = F.relu(h)
     return F.linear(h, sd[p + "6.weight"], sd[p + "6.bias"])
 
 
-def coupling(sd, p, x, direction):
+def coupling(sd, p, x, direction, training=False):
     m = sd[p + "mask"]
     xa = x * m
-    s = torch.clamp(_coupling_net(sd, p + "s_net.", xa), min=-10.0, max=10.0)   # :50, :79
-    b = torch.clamp(_coupling_net(sd, p + "b_net.", xa), min=-10.0, max=10.0)   # :51, :80
+    s = torch.clamp(_coupling_net(sd, p + "s_net.", xa, training), min=-10.0, max=10.0)   # :50, :79
+    b = torch.clamp(_coupling_net(sd, p + "b_net.", xa, training), min=-10.0, max=10.0)   # :51, :80
     if direction > 0:
         y = xa + (1 - m) * (x * torch.exp(s) + b)                                # :55
         ld = ((1 - m) * s).sum(dim=1)                                             # :58
@@ -326,8 +328,9 @@ def flow_model(sd, spec, x, direction):
     return x, log_det_sum
 
 
-def realnvp_spec(n_layers, prefix="flow.flows."):
-    return [("coupling", f"{prefix}{i}.", {}) for i in range(n_layers)]
+def realnvp_spec(n_layers, prefix="flow.flows.", training=False):
+    kw = {"training": True} if training else {}
+    return [("coupling", f"{prefix}{i}.", kw) for i in range(n_layers)]
 
 
 def spline_model_spec(n_layers, K=10, prefix="flow.flows."):

@@ -19,6 +19,9 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
   g9_small.npz        d=4/H=16 layers of the reference's own tests (+ MAF/IAF d=10)
   g10_arqs.npz        ARQS (src/flows/spline/arqs.py) forward/inverse: d in {1,3,5,10}, H up to
                       128, K in {2,5,8,11}, scalar data_min/data_max, eval BatchNorm in MADE
+  g11_train.npz       TRAIN-mode coupling layers (batch-statistics BatchNorm, coupling_layer.py:18-35):
+                      RealNVP(2,8,64) inverse + NLL backward (grads, running stats) and 5 Adam steps
+                      on two-moons (README.md:107-117); CouplingLayer(4,16) both directions
   g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes
 
 Each npz holds the module's state_dict arrays under their reference keys (prefixed per case),
@@ -70,7 +73,7 @@ def sd_arrays(module, prefix):
     for k, v in module.state_dict().items():
         if v.dtype == torch.int64:  # num_batches_tracked
             continue
-        out[prefix + k] = v.detach().cpu().numpy()
+        out[prefix + k] = v.detach().cpu().numpy().copy()  # train mode mutates buffers in place
     return out
 
 
@@ -338,6 +341,67 @@ def g10(flows):
     np.savez_compressed(os.path.join(HERE, "g10_arqs.npz"), **out)
 
 
+def g11(flows, models):
+    """Train mode: BatchNorm1d normalises with batch statistics and updates running stats."""
+    from torch.distributions import MultivariateNormal
+    out = {}
+    torch.manual_seed(50)
+    m = models.RealNVP(2, 8, 64)
+    perturb(m, 0.03, 51)
+    m.train()
+    out.update(sd_arrays(m, "rn.init."))
+    x = torch.cat([moons(1900, 0.05, 42), torch.randn(100, 2, generator=torch.Generator().manual_seed(52))])
+    out["rn.x"] = x.numpy()
+    base = MultivariateNormal(torch.zeros(2), torch.eye(2))
+    z, ld = m.inverse(x)
+    loss = -(base.log_prob(z) + ld).mean()
+    loss.backward()
+    out.update({"rn.z": z.detach().numpy(), "rn.ld": ld.detach().numpy(), "rn.loss": np.float64(loss.item())})
+    for k, p in m.named_parameters():
+        out["rn.grad." + k] = p.grad.numpy()
+    out.update(sd_arrays(m, "rn.after."))
+    # 5 full-batch Adam steps from the same initial state (README.md:107-117)
+    torch.manual_seed(50)
+    m = models.RealNVP(2, 8, 64)
+    perturb(m, 0.03, 51)
+    m.train()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(5):
+        z, ld = m.inverse(x)
+        loss = -(base.log_prob(z) + ld).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    out["rn.adam_losses"] = np.asarray(losses, dtype=np.float64)
+    out.update(sd_arrays(m, "rn.adam5."))
+    # single layer, d = 4 (padded kernel width), both directions, loss with weights on y and ld
+    torch.manual_seed(53)
+    mask = torch.tensor([1.0, 0.0, 1.0, 0.0])
+    layer = flows.CouplingLayer(4, 16, mask)
+    perturb(layer, 0.2, 54)
+    layer.train()
+    out.update(sd_arrays(layer, "c4.init."))
+    g = torch.Generator().manual_seed(55)
+    xc = torch.randn(333, 4, generator=g) * 1.5
+    wy = torch.randn(333, 4, generator=g)
+    wl = torch.randn(333, generator=g)
+    out.update({"c4.x": xc.numpy(), "c4.wy": wy.numpy(), "c4.wl": wl.numpy()})
+    for name, fn in (("inv", layer.inverse), ("fwd", layer.forward)):
+        layer.zero_grad()
+        xr = xc.clone().requires_grad_(True)
+        y, ldc = fn(xr)
+        ((y * wy).sum() + (ldc * wl).sum()).backward()
+        out[f"c4.{name}.y"] = y.detach().numpy()
+        out[f"c4.{name}.ld"] = ldc.detach().numpy()
+        out[f"c4.{name}.gx"] = xr.grad.numpy()
+        for k, p in layer.named_parameters():
+            out[f"c4.{name}.grad.{k}"] = p.grad.numpy()
+    out.update(sd_arrays(layer, "c4.after."))  # running stats after the two calls
+    np.savez_compressed(os.path.join(HERE, "g11_train.npz"), **out)
+
+
 def g8(m2, m3, m5):
     """Full-scale NLL scalars (float64 mean of the reference's fp32 log_prob)."""
     torch.set_num_threads(8)
@@ -374,6 +438,9 @@ def main():
     flows, models = import_reference()
     if a.only == "g10":
         g10(flows)
+        return
+    if a.only == "g11":
+        g11(flows, models)
         return
     import src.utils as src_utils
     g1(flows)

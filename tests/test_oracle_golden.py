@@ -165,3 +165,40 @@ def test_arqs_g10(name):
             y, ld = oracle.arqs(sd, "", x, direction, K=K, batch_norm=bn, **rng)
         close(y, g[f"{name}.{key}_y"], rtol=1e-5, atol=1e-6)
         close(ld, g[f"{name}.{key}_ld"], rtol=1e-5, atol=1e-5)
+
+
+def test_train_mode_g11():
+    """Train-mode BatchNorm (batch statistics + running-statistics update) and the NLL gradients
+    of RealNVP(2,8,64) through the oracle vs the reference (G11), and a d=4 layer both ways."""
+    g = load_golden("g11_train.npz")
+    sd = oracle_sd(g, "rn.init.")
+    for k, v in sd.items():
+        if v.is_floating_point() and not k.endswith(("running_mean", "running_var", "mask")):
+            v.requires_grad_(True)
+    x = torch.from_numpy(g["rn.x"])
+    z, ld = oracle.flow_model(sd, oracle.realnvp_spec(8, training=True), x, -1)
+    loss = -oracle.gauss_log_prob(z, ld).mean()
+    loss.backward()
+    close(z.detach(), g["rn.z"], rtol=1e-5, atol=1e-5)
+    close(ld.detach(), g["rn.ld"], rtol=1e-5, atol=1e-5)
+    assert abs(loss.item() - float(g["rn.loss"])) < 1e-5
+    for k, v in sd.items():
+        if v.requires_grad:
+            ref = g["rn.grad." + k]
+            close(v.grad, ref, rtol=1e-4, atol=1e-4 * max(1.0, float(np.abs(ref).max())))
+        elif k.endswith(("running_mean", "running_var")):
+            close(v, g["rn.after." + k], rtol=1e-6, atol=1e-7)
+    sd4 = oracle_sd(g, "c4.init.")
+    for name, direction in (("inv", -1), ("fwd", 1)):
+        params = {k: v.clone().requires_grad_(True) if v.is_floating_point() and not k.endswith(
+            ("running_mean", "running_var", "mask")) else v for k, v in sd4.items()}
+        xr = torch.from_numpy(g["c4.x"]).clone().requires_grad_(True)
+        y, l4 = oracle.coupling(params, "", xr, direction, training=True)
+        ((y * torch.from_numpy(g["c4.wy"])).sum() + (l4 * torch.from_numpy(g["c4.wl"])).sum()).backward()
+        close(y.detach(), g[f"c4.{name}.y"], rtol=1e-5, atol=1e-5)
+        close(l4.detach(), g[f"c4.{name}.ld"], rtol=1e-5, atol=1e-5)
+        close(xr.grad, g[f"c4.{name}.gx"], rtol=1e-4, atol=1e-4)
+        sd4 = params  # running statistics carry over to the second call, as in the reference
+    for k in sd4:
+        if k.endswith(("running_mean", "running_var")):
+            close(sd4[k], g["c4.after." + k], rtol=1e-6, atol=1e-7)
