@@ -170,31 +170,58 @@ __global__ void affine_train_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const
     }
 }
 
-// stats[net][row][3] = Chan merge, in wave order, of the per-wave triples.
-__global__ void affine_train_stats_finish(const double* part, int64_t nw, int Hp, double* stats) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // net * Hp + row
-    if (i >= 2 * Hp) return;
+// stats[net][row][3] = Chan merge of the per-workgroup triples: 16 threads per feature merge
+// workgroups g, g+16, ... and the 16 results are merged in order (deterministic).
+__global__ __launch_bounds__(256) void affine_train_stats_finish(const double* part, int nw, int Hp, double* stats) {
+    __shared__ double red[16][16][3];
+    const int e = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int i = blockIdx.x * 16 + e;  // net * Hp + row
     double n = 0.0, mean = 0.0, m2 = 0.0;
-    for (int64_t w = 0; w < nw; ++w) {
-        const double* q = part + (w * 2 * Hp + i) * 3;
-        if (n == 0.0) {
-            n = q[0]; mean = q[1]; m2 = q[2];
-        } else {
-            chan_merge(n, mean, m2, q[0], q[1], q[2]);
+    if (i < 2 * Hp) {
+        for (int w = g; w < nw; w += 16) {
+            const double* q = part + ((size_t)w * 2 * Hp + i) * 3;
+            if (n == 0.0) {
+                n = q[0]; mean = q[1]; m2 = q[2];
+            } else {
+                chan_merge(n, mean, m2, q[0], q[1], q[2]);
+            }
         }
     }
-    stats[i * 3 + 0] = n;
-    stats[i * 3 + 1] = mean;
-    stats[i * 3 + 2] = m2;
+    red[g][e][0] = n;
+    red[g][e][1] = mean;
+    red[g][e][2] = m2;
+    __syncthreads();
+    if (g == 0 && i < 2 * Hp) {
+        for (int k = 1; k < 16; ++k) {
+            if (n == 0.0) {
+                n = red[k][e][0]; mean = red[k][e][1]; m2 = red[k][e][2];
+            } else {
+                chan_merge(n, mean, m2, red[k][e][0], red[k][e][1], red[k][e][2]);
+            }
+        }
+        stats[i * 3 + 0] = n;
+        stats[i * 3 + 1] = mean;
+        stats[i * 3 + 2] = m2;
+    }
 }
 
-// out[i] = sum_w part[w * len + i] in float64, wave order (deterministic).
-__global__ void affine_train_sum_finish(const float* part, int64_t nw, int len, double* out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= len) return;
+// out[i] = sum_w part[w * len + i] in float64: 16 threads per element over workgroups g, g+16, ...,
+// then the 16 partial sums in order (deterministic).
+__global__ __launch_bounds__(256) void affine_train_sum_finish(const float* part, int nw, int len, double* out) {
+    __shared__ double red[16][17];
+    const int e = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int i = blockIdx.x * 16 + e;
     double a = 0.0;
-    for (int64_t w = 0; w < nw; ++w) a += (double)part[w * len + i];
-    out[i] = a;
+    if (i < len) {
+#pragma unroll 4
+        for (int w = g; w < nw; w += 16) a += (double)part[(size_t)w * len + i];
+    }
+    red[g][e] = a;
+    __syncthreads();
+    if (g == 0 && i < len) {
+        for (int k = 1; k < 16; ++k) a += red[k][e];
+        out[i] = a;
+    }
 }
 
 // Parameter gradients in CouplingLayer.parameters() order, per net (s_net then b_net):
@@ -369,8 +396,8 @@ extern "C" int nfx_affine_train_stats(const float* tpack, const float* x, int64_
     k<<<g.grid, 256, lds, s>>>(tpack, x, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, workspace, B, d, 1,
                                g.ntiles);
     if ((rc = check_launch("affine_train_kernel(stats)"))) return rc;
-    affine_train_stats_finish<<<(2 * Hp + 127) / 128, 128, 0, s>>>(reinterpret_cast<const double*>(workspace),
-                                                                   g.nwaves, Hp, stats);
+    affine_train_stats_finish<<<(2 * Hp + 15) / 16, 256, 0, s>>>(reinterpret_cast<const double*>(workspace),
+                                                                 g.grid, Hp, stats);
     return check_launch("affine_train_stats_finish");
 }
 
@@ -416,8 +443,8 @@ extern "C" int nfx_affine_train_backward(const float* tpack, const float* x, con
     if ((rc = check_launch("affine_train_kernel(backward)"))) return rc;
     const int off = stage == 1 ? GL.g1s : (stage == 2 ? GL.g2s : GL.g3w);
     const int len = stage == 1 ? GL.len1 : (stage == 2 ? GL.len2 : GL.len3);
-    affine_train_sum_finish<<<(len + 255) / 256, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), g.nwaves,
-                                                              len, G + off);
+    affine_train_sum_finish<<<(len + 15) / 16, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), g.grid, len,
+                                                            G + off);
     return check_launch("affine_train_sum_finish");
 }
 

@@ -198,16 +198,58 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
         for (int j = 0; j < D; ++j) ac_b[n][j] = 0.f;
     }
 
+    // Software pipeline: the next tile's per-sample inputs (x row, upstream gradients, and in
+    // BWD3 the g_y1 tiles) are loaded while the current tile computes. Out-of-range lanes load
+    // a clamped valid address and zero the value.
+    constexpr bool GRADS = STAGE == TS_BWD1 || STAGE == TS_BWD2;
+    constexpr int NGQ = STAGE == TS_BWD3 ? 2 * HT * 16 : 1;
+    struct Fetch {
+        float xr[D];
+        float gyr[D];
+        float gl;
+        float gq[NGQ];
+    };
+    auto fetch = [&](int64_t tile, Fetch& f) {
+        const int64_t s = tile * 32 + col;
+        const bool ok = tile < ntiles && s < B;
+        const int64_t sc = ok ? s : 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const float v = j < d ? x[sc * d + j] : 0.f;
+            f.xr[j] = ok ? v : 0.f;
+        }
+        if constexpr (GRADS) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const float v = j < d ? gy[sc * d + j] : 0.f;
+                f.gyr[j] = ok ? v : 0.f;
+            }
+            const float v = gld[sc];
+            f.gl = ok ? v : 0.f;
+        }
+        if constexpr (STAGE == TS_BWD3) {
+            const int64_t tc = tile < ntiles ? tile : 0;
+            const float* gq = gbuf + (tc * 2 * HT * 16) * 64 + lane;
+#pragma unroll
+            for (int q = 0; q < NGQ; ++q) f.gq[q] = gq[q * 64];
+        }
+    };
+
     bool first = true;
+    Fetch cur;
+    fetch(wid, cur);
     for (int64_t tile = wid; tile < ntiles; tile += nwaves) {
         const int64_t base = tile * 32;
         const int64_t s = base + col;
         const bool valid = s < B;
         const float* smi = sm + opaque_zero();
+        const float* kci = kc + opaque_zero();  // keeps the BN constants in LDS, not in VGPRs
+        Fetch nxt;
+        fetch(tile + nwaves, nxt);
         // the lane's sample row (both lane halves hold the same sample)
         float xr[D];
 #pragma unroll
-        for (int j = 0; j < D; ++j) xr[j] = (valid && j < d) ? x[s * d + j] : 0.f;
+        for (int j = 0; j < D; ++j) xr[j] = cur.xr[j];
         float xb[KS1];  // layer-1 B operand: xa[sample col][2ks + h]
 #pragma unroll
         for (int ks = 0; ks < KS1; ++ks) {
@@ -317,10 +359,10 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                 for (int j = 0; j < D; ++j) outv[n][j] = halves_sum(pj[j], pj[j]) + P[L.b3 + j];
             }
             // ---- epilogue backward (coupling_layer.py:40-96 under autograd) ---------------
-            const float gl_in = valid ? gld[s] : 0.f;
+            const float gl_in = cur.gl;
             float gyr[D];
 #pragma unroll
-            for (int j = 0; j < D; ++j) gyr[j] = (valid && j < d) ? gy[s * d + j] : 0.f;
+            for (int j = 0; j < D; ++j) gyr[j] = cur.gyr[j];
             float dl[2][D], gxd[D];
             {
 #pragma clang fp contract(off)
@@ -427,8 +469,8 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                         }
                     } else {
                         // e2 = gamma2 (g_y2 - k1 - x^2 k2)  (BatchNorm backward with batch statistics)
-                        const f32x16 k1 = load_bias16(kc + (n * 2 + 0) * Hp + o * 32, h);
-                        const f32x16 k2 = load_bias16(kc + (n * 2 + 1) * Hp + o * 32, h);
+                        const f32x16 k1 = load_bias16(kci + (n * 2 + 0) * Hp + o * 32, h);
+                        const f32x16 k2 = load_bias16(kci + (n * 2 + 1) * Hp + o * 32, h);
 #pragma unroll
                         for (int r = 0; r < 16; ++r) {
                             const float v = g[r] * ((gy2[r] - k1[r]) - xh2[n][o][r] * k2[r]);
@@ -508,14 +550,13 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                 layer1(P, xh1);
 #pragma unroll
                 for (int kt = 0; kt < HT; ++kt) {
-                    const float* gq = gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64 + lane;
                     const f32x16 g = load_bias16(P + L.g1 + kt * 32, h);
-                    const f32x16 k1 = load_bias16(kc + (n * 2 + 0) * Hp + kt * 32, h);
-                    const f32x16 k2 = load_bias16(kc + (n * 2 + 1) * Hp + kt * 32, h);
+                    const f32x16 k1 = load_bias16(kci + (n * 2 + 0) * Hp + kt * 32, h);
+                    const f32x16 k2 = load_bias16(kci + (n * 2 + 1) * Hp + kt * 32, h);
                     f32x16 e1;
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const float v = g[r] * ((gq[r * 64] - k1[r]) - xh1[kt][r] * k2[r]);
+                        const float v = g[r] * ((cur.gq[(n * HT + kt) * 16 + r] - k1[r]) - xh1[kt][r] * k2[r]);
                         e1[r] = valid ? v : 0.f;
                     }
                     float Te[16];
@@ -546,100 +587,122 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
             }
         }
         first = false;
+        cur = nxt;
     }
 
-    // ---- per-wave partials ------------------------------------------------------------------
-    if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
-        // per lane (n, mean, M2) of its half's samples; merge the two halves (same features)
-        double* pw = reinterpret_cast<double*>(part) + wid * (2 * Hp * 3);
+    // ---- workgroup combine: the 4 waves add (merge) their partials into LDS in wave order,
+    // then the workgroup writes one partial; the finish kernels reduce workgroups in order ----
+    static_assert(GL.len1 <= PACKF && GL.len2 <= PACKF && GL.len3 <= PACKF && 12 * Hp <= PACKF,
+                  "reduction buffer must fit the pack region");
+    __syncthreads();  // every wave is done with the weight pack: reuse its LDS
+    float* red = sm;
+    double* redd = reinterpret_cast<double*>(sm);
+    constexpr int LEN = STAGE == TS_BWD1 ? GL.len1 : (STAGE == TS_BWD2 ? GL.len2 : (STAGE == TS_BWD3 ? GL.len3 : 0));
+    for (int rnd = 0; rnd < 4; ++rnd) {
+        if (wave == rnd) {
+            auto put = [&](int idx, float v) { red[idx] = rnd ? red[idx] + v : v; };
+            if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
+                // per lane (n, mean, M2) of its half's samples; merge the halves (same features)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+                for (int n = 0; n < 2; ++n)
 #pragma unroll
-            for (int ht = 0; ht < HT; ++ht) {
-                double cnt = st_n, mean = 0.0, m2 = 0.0;
-                if (cnt > 0.0) {
-                    mean = (double)st_c[n][ht] + st_s1[n][ht] / cnt;
-                    m2 = st_s2[n][ht] - st_s1[n][ht] * st_s1[n][ht] / cnt;
-                    if (m2 < 0.0) m2 = 0.0;
-                }
-                const double nb = __shfl_xor(cnt, 32, 64), mb = __shfl_xor(mean, 32, 64), qb = __shfl_xor(m2, 32, 64);
-                if (h == 0) {
-                    if (cnt == 0.0) { cnt = nb; mean = mb; m2 = qb; }
-                    else chan_merge(cnt, mean, m2, nb, mb, qb);
-                    double* q = pw + (n * Hp + 32 * ht + col) * 3;
-                    q[0] = cnt;
-                    q[1] = mean;
-                    q[2] = m2;
-                }
-            }
-    } else {
-        float* pw = reinterpret_cast<float*>(part);
-        if constexpr (STAGE == TS_BWD1) {
-            pw += wid * GL.len1;
-#pragma unroll
-            for (int n = 0; n < 2; ++n)
-#pragma unroll
-                for (int ht = 0; ht < HT; ++ht) {
-                    const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
-                    const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
-                    if (h == 0) {
-                        pw[(n * 2 + 0) * Hp + 32 * ht + col] = a;
-                        pw[(n * 2 + 1) * Hp + 32 * ht + col] = b;
+                    for (int ht = 0; ht < HT; ++ht) {
+                        double cnt = st_n, mean = 0.0, m2 = 0.0;
+                        if (cnt > 0.0) {
+                            mean = (double)st_c[n][ht] + st_s1[n][ht] / cnt;
+                            m2 = st_s2[n][ht] - st_s1[n][ht] * st_s1[n][ht] / cnt;
+                            if (m2 < 0.0) m2 = 0.0;
+                        }
+                        const double nb = __shfl_xor(cnt, 32, 64), mb = __shfl_xor(mean, 32, 64),
+                                     qb = __shfl_xor(m2, 32, 64);
+                        if (h == 0) {
+                            if (cnt == 0.0) {
+                                cnt = nb; mean = mb; m2 = qb;
+                            } else {
+                                chan_merge(cnt, mean, m2, nb, mb, qb);
+                            }
+                            double* q = redd + (n * Hp + 32 * ht + col) * 3;
+                            if (rnd == 0 || q[0] == 0.0) {
+                                q[0] = cnt; q[1] = mean; q[2] = m2;
+                            } else {
+                                double a = q[0], b = q[1], c = q[2];
+                                chan_merge(a, b, c, cnt, mean, m2);
+                                q[0] = a; q[1] = b; q[2] = c;
+                            }
+                        }
                     }
+            } else if constexpr (STAGE == TS_BWD1) {
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+#pragma unroll
+                    for (int ht = 0; ht < HT; ++ht) {
+                        const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
+                        const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
+                        if (h == 0) {
+                            put((n * 2 + 0) * Hp + 32 * ht + col, a);
+                            put((n * 2 + 1) * Hp + 32 * ht + col, b);
+                        }
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            const float w = halves_sum(ac_w[n][ht][j], ac_w[n][ht][j]);
+                            if (h == 0) put(4 * Hp + n * (D * Hp + D) + j * Hp + 32 * ht + col, w);
+                        }
+                    }
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
 #pragma unroll
                     for (int j = 0; j < D; ++j) {
-                        const float w = halves_sum(ac_w[n][ht][j], ac_w[n][ht][j]);
-                        if (h == 0) pw[4 * Hp + n * (D * Hp + D) + j * Hp + 32 * ht + col] = w;
+                        float v = ac_b[n][j];
+#pragma unroll
+                        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                        if (lane == 0) put(4 * Hp + n * (D * Hp + D) + D * Hp + j, v);
                     }
-                }
+            } else if constexpr (STAGE == TS_BWD2) {
 #pragma unroll
-            for (int n = 0; n < 2; ++n)
+                for (int n = 0; n < 2; ++n) {
 #pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    float v = ac_b[n][j];
-#pragma unroll
-                    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-                    if (lane == 0) pw[4 * Hp + n * (D * Hp + D) + D * Hp + j] = v;
-                }
-        } else if constexpr (STAGE == TS_BWD2) {
-            pw += wid * GL.len2;
-#pragma unroll
-            for (int n = 0; n < 2; ++n) {
-#pragma unroll
-                for (int ht = 0; ht < HT; ++ht) {
-                    const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
-                    const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
-                    const float c = halves_sum(ac_db[n][ht], ac_db[n][ht]);
-                    if (h == 0) {
-                        pw[(n * 2 + 0) * Hp + 32 * ht + col] = a;
-                        pw[(n * 2 + 1) * Hp + 32 * ht + col] = b;
-                        pw[4 * Hp + n * (Hp * Hp + Hp) + Hp * Hp + 32 * ht + col] = c;
+                    for (int ht = 0; ht < HT; ++ht) {
+                        const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
+                        const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
+                        const float c = halves_sum(ac_db[n][ht], ac_db[n][ht]);
+                        if (h == 0) {
+                            put((n * 2 + 0) * Hp + 32 * ht + col, a);
+                            put((n * 2 + 1) * Hp + 32 * ht + col, b);
+                            put(4 * Hp + n * (Hp * Hp + Hp) + Hp * Hp + 32 * ht + col, c);
+                        }
                     }
+                    const int pdw = 4 * Hp + n * (Hp * Hp + Hp);
+#pragma unroll
+                    for (int o = 0; o < HT; ++o)
+#pragma unroll
+                        for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                            for (int r = 0; r < 16; ++r)
+                                put(pdw + (32 * o + crow(r, h)) * Hp + 32 * kt + col, ac_dw[n][o][kt][r]);
                 }
-                float* pdw = pw + 4 * Hp + n * (Hp * Hp + Hp);
+            } else {
 #pragma unroll
-                for (int o = 0; o < HT; ++o)
+                for (int n = 0; n < 2; ++n)
 #pragma unroll
-                    for (int kt = 0; kt < HT; ++kt)
+                    for (int ht = 0; ht < HT; ++ht) {
+                        const float c = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
+                        if (h == 0) put(n * (D * Hp + Hp) + D * Hp + 32 * ht + col, c);
 #pragma unroll
-                        for (int r = 0; r < 16; ++r)
-                            pdw[(32 * o + crow(r, h)) * Hp + 32 * kt + col] = ac_dw[n][o][kt][r];
+                        for (int j = 0; j < D; ++j) {
+                            const float w = halves_sum(ac_w[n][ht][j], ac_w[n][ht][j]);
+                            if (h == 0) put(n * (D * Hp + Hp) + j * Hp + 32 * ht + col, w);
+                        }
+                    }
             }
-        } else {
-            pw += wid * GL.len3;
-#pragma unroll
-            for (int n = 0; n < 2; ++n)
-#pragma unroll
-                for (int ht = 0; ht < HT; ++ht) {
-                    const float c = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
-                    if (h == 0) pw[n * (D * Hp + Hp) + D * Hp + 32 * ht + col] = c;
-#pragma unroll
-                    for (int j = 0; j < D; ++j) {
-                        const float w = halves_sum(ac_w[n][ht][j], ac_w[n][ht][j]);
-                        if (h == 0) pw[n * (D * Hp + Hp) + j * Hp + 32 * ht + col] = w;
-                    }
-                }
         }
+        __syncthreads();
+    }
+    if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
+        double* pw = reinterpret_cast<double*>(part) + (int64_t)blockIdx.x * (2 * Hp * 3);
+        for (int i = threadIdx.x; i < 2 * Hp * 3; i += 256) pw[i] = redd[i];
+    } else {
+        float* pw = reinterpret_cast<float*>(part) + (int64_t)blockIdx.x * LEN;
+        for (int i = threadIdx.x; i < LEN; i += 256) pw[i] = red[i];
     }
 }
 
