@@ -277,9 +277,19 @@ def main():
     graphed = None
     if a.graph and not training:
         graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-5) if training else None
+    opt = torch.optim.Adam(model.parameters(), lr=1e-5, capturable=a.graph) if training else None
+    graphed_train = None
+    if a.graph and training:
+        if world > 1:
+            raise SystemExit("--graph training is single-GPU (the SyncBN / gradient collectives run eagerly)")
+        graphed_train = nfs_amd.GraphedTrainStep(flow, x, opt, warmup=a.warmup)
+
+    eager_only = [False]  # the per-kernel event pass runs eager steps (a graph replay records no events)
 
     def step():
+        if graphed_train is not None and not eager_only[0]:
+            loss = graphed_train()
+            return torch.stack([-loss.double() * B, torch.full((), float(B), device=dev, dtype=torch.float64)])
         if training:
             # data-parallel training step: HIP forward, fused HIP backward, one bucketed RCCL
             # all-reduce of the flat gradient (412 KB at cfg4), Adam
@@ -321,6 +331,7 @@ def main():
         # Kernel durations: the same K steps again with HIP events around every layer launch
         # on the launch stream. Kept out of the headline loop because each event record adds
         # ~5 us of GPU idle between kernels (measured, profiles/).
+        eager_only[0] = True
         if coupling_train:
             from nfs_amd.flows import coupling as _cp
             _cp.TRAIN_EVENTS = []
@@ -346,7 +357,7 @@ def main():
             torch.cuda.synchronize()
             events = flow.layer_events
             flow.layer_events = None
-    if nfs_amd.STATS["torch"] != 0 or (nfs_amd.STATS["hip"] == 0 and graphed is None):
+    if nfs_amd.STATS["torch"] != 0 or (nfs_amd.STATS["hip"] == 0 and graphed is None and graphed_train is None):
         raise RuntimeError(f"hot path did not run on the HIP kernels: {nfs_amd.STATS}")
     t_all = torch.tensor([t], device=dev, dtype=torch.float64)
     if world > 1:

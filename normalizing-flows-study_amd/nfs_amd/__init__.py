@@ -8,9 +8,9 @@ from .flows import (Flow, SequentialFlow, CouplingLayer, SplineCouplingLayer,
                     rational_quadratic_spline, ARQS, MaskedLinear, MADE, MaskedAutoregressiveFlow,
                     InverseAutoregressiveFlow, made_degrees, STATS, reset_stats)
 from .models import NormalizingFlowModel, RealNVP, RealNVPSpline, gauss_logprob
-from .graphs import GraphedFlow
+from .graphs import GraphedFlow, GraphedTrainStep
 
 __all__ = ["Flow", "SequentialFlow", "CouplingLayer", "SplineCouplingLayer",
            "rational_quadratic_spline", "ARQS", "MaskedLinear", "MADE", "MaskedAutoregressiveFlow",
            "InverseAutoregressiveFlow", "NormalizingFlowModel", "RealNVP", "RealNVPSpline",
-           "gauss_logprob", "made_degrees", "STATS", "reset_stats", "GraphedFlow"]
+           "gauss_logprob", "made_degrees", "STATS", "reset_stats", "GraphedFlow", "GraphedTrainStep"]

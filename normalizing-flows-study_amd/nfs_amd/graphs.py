@@ -18,6 +18,13 @@ The packed weight images are built before capture and baked into the graph. With
 `strict=True` (default) every call checks that no parameter or buffer changed since capture
 (in-place optimizer steps and load_state_dict bump tensor versions) and raises instead of
 replaying stale weights; `strict=False` skips that check.
+
+GraphedTrainStep captures a whole full-batch TRAINING step — loss = -log_prob(x).mean(),
+backward (the train-mode coupling kernels and the fused backward passes, BatchNorm running
+statistics included), optional gradient clipping, optimizer.step() — as one graph. The
+reference trains full-batch on a few thousand points (README.md:107-117: 5,000 two-moons
+samples; plots/_common.py:194-211: 2,000), where an eager step is bound by the ~150 kernel
+launches it issues, not by the GPU.
 """
 import torch
 
@@ -80,3 +87,57 @@ class GraphedFlow:
             self.static_in.copy_(x)
         self.graph.replay()
         return self.static_out
+
+
+class GraphedTrainStep:
+    """One captured training step: `loss_fn(model, x)` (default: -model.log_prob(x).mean()),
+    backward, `clip_grad_norm_` (if `clip_grad_norm` is set) and `optimizer.step()`.
+
+    The optimizer must be capturable (e.g. torch.optim.Adam(params, capturable=True)). The
+    `warmup` eager steps run before capture (on a side stream, as torch.cuda.graphs requires) are
+    REAL training steps: they update the parameters and optimizer state. Each call replays one
+    step on the static input (optionally refreshed from `x`) and returns the static loss tensor
+    (valid until the next replay)."""
+
+    def __init__(self, model, example, optimizer, loss_fn=None, clip_grad_norm=None, warmup=3):
+        if example.device.type != "cuda":
+            raise ValueError("GraphedTrainStep needs a ROCm device tensor")
+        self.model = model
+        self.optimizer = optimizer
+        self.loss_fn = loss_fn or (lambda m, x: -m.log_prob(x).mean())
+        self.clip = clip_grad_norm
+        self.static_in = example.detach().clone().contiguous()
+        params = [p for g in optimizer.param_groups for p in g["params"]]
+        self._params = params
+        dev = example.device
+        stream = torch.cuda.Stream(device=dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):
+            for _ in range(warmup):
+                self._step()
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        torch0 = _flows.STATS["torch"]
+        optimizer.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_loss = self._step(zero=False)
+        if _flows.STATS["torch"] != torch0:
+            raise RuntimeError("GraphedTrainStep: the captured step ran eager PyTorch layers, not the HIP kernels")
+
+    def _step(self, zero=True):
+        if zero:
+            self.optimizer.zero_grad(set_to_none=True)
+        loss = self.loss_fn(self.model, self.static_in)
+        loss.backward()
+        if self.clip is not None:
+            torch.nn.utils.clip_grad_norm_(self._params, self.clip)
+        self.optimizer.step()
+        return loss.detach()
+
+    def __call__(self, x=None):
+        if x is not None:
+            if x.shape != self.static_in.shape:
+                raise ValueError(f"GraphedTrainStep captured shape {tuple(self.static_in.shape)}, got {tuple(x.shape)}")
+            self.static_in.copy_(x)
+        self.graph.replay()
+        return self.static_loss

@@ -169,6 +169,8 @@ class NormalizingFlowModel(nn.Module):
         else:
             d = z.shape[1]
             logp = -0.5 * (d * math.log(2 * math.pi) + z.pow(2).sum(-1)) + ld
+            if not return_sums:  # (no host->device scalar copy: the step stays graph-capturable)
+                return logp
             sums = torch.stack([logp.detach().double().sum(),
                                 torch.tensor(float(z.shape[0]), dtype=torch.float64, device=z.device)])
         return (logp, sums) if return_sums else logp
