@@ -188,6 +188,30 @@ int nfx_made_affine_backward(const float* packed, const float* in, const float* 
                              int d, int H, int variant, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Training: backward of SplineCouplingLayer.forward/inverse
+ * (spline_coupling_layer.py:96-309 under autograd) in one fused kernel: the param MLP
+ * recomputed on MFMA, the rational-quadratic spline's adjoint per transformed element (softmax,
+ * knot cumsum with pinned ends, softplus, gather, RQ map / citardauq inverse, every clamp and
+ * NaN/Inf guard as autograd treats it), the data-gradient chain through the MLP and the weight
+ * gradients as contractions over the sample dimension. d <= 8, H <= 64, K <= 11, no data_min/
+ * data_max rescale, and at most 2 (H <= 32) / 1 (H <= 64) transformed dimensions
+ * (NFX_EUNSUPPORTED otherwise). packed: nfx_spline_pack_backward image; grads: fp32, the
+ * layer's parameters() order (param_net.0.weight, .0.bias, .2.weight, .2.bias, .4.weight,
+ * .4.bias); workspace: nfx_spline_backward_workspace_bytes(B, d, H, K) bytes.
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_spline_backward_packed_floats(int d, int H, int K);
+size_t nfx_spline_backward_param_floats(int d, int H, int K);
+size_t nfx_spline_backward_workspace_bytes(int64_t B, int d, int H, int K);
+int nfx_spline_pack_backward(const NfxMlpRaw* net, const float* mask, int d, int H, int K,
+                             float* packed, void* stream);
+int nfx_spline_coupling_backward(const float* packed, const float* mask, const float* in,
+                                 const float* grad_out, const float* grad_log_det, float* grad_in,
+                                 float* grads, void* workspace, int64_t B, int d, int H, int K,
+                                 int n_transformed, float bound, float min_bin_width,
+                                 float min_bin_height, float min_derivative, int direction,
+                                 void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Training (SURVEY.md §8(f) items 1 + 2): CouplingLayer in TRAIN mode — BatchNorm1d with
  * batch statistics (coupling_layer.py:18-35 under model.train(); the reference's training
  * loops README.md:107-117, plots/_common.py:194-211) — and its backward, for d <= 8, H <= 64

@@ -283,6 +283,11 @@ __global__ void affine_train_running_kernel(const double* stats1, const double* 
     if (p.rv[k]) p.rv[k][row] = (float)(momentum * var_u + (1.0 - momentum) * (double)p.rv[k][row]);
 }
 
+int train_sum_finish(const float* part, int nw, int len, double* out, hipStream_t s) {
+    affine_train_sum_finish<<<(len + 15) / 16, 256, 0, s>>>(part, nw, len, out);
+    return check_launch("affine_train_sum_finish");
+}
+
 static int pad_d(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 8 ? 8 : 0)); }
 
 static affine_train_kernel_t pick_train(int HT, int D, int stage) {

@@ -137,6 +137,8 @@ int num_cus();
 int resident_grid(const void* kernel, int threads, size_t lds_bytes, int64_t work_groups);
 // Raise the dynamic-LDS limit of `kernel` when it needs more than 64 KiB.
 int prepare_lds(const void* kernel, size_t bytes);
+// out[i] = sum_w part[w * len + i] (float partials of nw workgroups, float64 result, fixed order).
+int train_sum_finish(const float* part, int nw, int len, double* out, hipStream_t s);
 // Reduce n float64 partials into sums[0] = total, sums[1] = (double)B (one 256-thread block).
 int gauss_finish(const double* partials, int n, double* sums, int64_t B, hipStream_t s);
 }  // namespace nfx

@@ -40,6 +40,8 @@ EXPORTED_SYMBOLS = (
     "nfx_affine_train_param_floats", "nfx_affine_train_workspace_bytes", "nfx_affine_train_pack",
     "nfx_affine_train_stats", "nfx_affine_train_update_running", "nfx_affine_train_backward",
     "nfx_affine_train_assemble",
+    "nfx_spline_backward_packed_floats", "nfx_spline_backward_param_floats",
+    "nfx_spline_backward_workspace_bytes", "nfx_spline_pack_backward", "nfx_spline_coupling_backward",
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob",
 )
 
@@ -112,6 +114,12 @@ _SIGNATURES = {
     "nfx_affine_train_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp, _vp, _vp,
                                          _vp]),
     "nfx_affine_train_assemble": (_int, [_vp, _vp, _vp, _int, _int, _f, _vp, _vp]),
+    "nfx_spline_backward_packed_floats": (_sz, [_int, _int, _int]),
+    "nfx_spline_backward_param_floats": (_sz, [_int, _int, _int]),
+    "nfx_spline_backward_workspace_bytes": (_sz, [_i64, _int, _int, _int]),
+    "nfx_spline_pack_backward": (_int, [ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _int, _vp, _vp]),
+    "nfx_spline_coupling_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int,
+                                            _f, _f, _f, _f, _int, _vp]),
     "nfx_gauss_workspace_bytes": (_sz, [_i64]),
     "nfx_gauss_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _vp]),
 }

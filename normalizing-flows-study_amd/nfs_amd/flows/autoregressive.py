@@ -174,7 +174,7 @@ class _MadeAffineFlow(HipFlow):
         return (self._variant(direction) == _lib.NFX_MAF_INVERSE and d <= 64 and H <= 64
                 and not self.conditioner.batchnorms() and x.dtype == torch.float32)
 
-    def _hip_backward(self, x, gz, gld):
+    def _hip_backward(self, x, gz, gld, direction=-1):
         """dL/dx and the parameter gradients (in self.parameters() order) of the inverse pass."""
         x = x.contiguous()
         B, d = x.shape

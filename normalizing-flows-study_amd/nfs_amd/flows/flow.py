@@ -76,9 +76,9 @@ class HipFlowFunction(torch.autograd.Function):
         layer = ctx.layer
         params = [p for p in layer.parameters()]
         if getattr(layer, "_hip_backward_ok", None) is not None and layer._hip_backward_ok(x, ctx.direction):
-            # fused gfx950 backward (MAF density direction); parameter grads as plain GEMMs
+            # fused gfx950 backward (MAF density direction, spline coupling)
             STATS["hip"] += 1
-            gx, gparams = layer._hip_backward(x.detach(), gy, gld)
+            gx, gparams = layer._hip_backward(x.detach(), gy, gld, ctx.direction)
             gparams = [g if p.requires_grad else None for p, g in zip(params, gparams)]
             return (None, None, gx, *gparams)
         with torch.enable_grad():
@@ -193,15 +193,16 @@ class HipFlow(Flow):
             key.append(None if t is None else (t.data_ptr(), t._version))
         return tuple(key)
 
-    def _packed(self, device, build):
+    def _packed(self, device, build, slot="_nfx_pack_cache"):
         """Return the cached device weight image, rebuilding it when any parameter/buffer
-        changed (in-place optimizer steps and load_state_dict bump tensor versions)."""
+        changed (in-place optimizer steps and load_state_dict bump tensor versions). `slot`
+        names the cache, so a layer can keep several images (forward, backward)."""
         key = self._state_key(device)
-        cache = self.__dict__.get("_nfx_pack_cache")
+        cache = self.__dict__.get(slot)
         if cache is not None and cache[0] == key:
             return cache[1]
         packed = build(device)
-        object.__setattr__(self, "_nfx_pack_cache", (key, packed))
+        object.__setattr__(self, slot, (key, packed))
         return packed
 
     def _torch_only(self):

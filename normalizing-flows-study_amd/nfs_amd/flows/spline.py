@@ -19,6 +19,10 @@ from .flow import HipFlow, STATS
 MAX_K = 11        # 3K-1 <= 32: one MFMA row tile of spline parameters per transformed dim
 MAX_D = 8
 MAX_H = 128
+MAX_H_BWD = 64    # fused backward: dW accumulators of <= 2 (H <= 32) / 1 (H <= 64) transformed dims
+# (kernel-name, start-event, end-event) of every fused backward while a list is installed here
+# (bench.py roofline timing); None = no events.
+BACKWARD_EVENTS = None
 
 
 def _cum_knots(w, bound):
@@ -200,6 +204,70 @@ class SplineCouplingLayer(HipFlow):
                                      _lib.stream_of(packed)), "nfx_spline_pack")
         packed._nfx_keep = (keep, mask)
         return packed
+
+    # -- fused backward (training) ---------------------------------------
+    def _hip_backward_ok(self, x, direction):
+        d, H, K = self.data_dim, self._hidden(), self.num_bins
+        nt = self._n_transformed()
+        ntmax = 2 if H <= 32 else 1
+        return (x.dtype == torch.float32 and d <= MAX_D and H <= MAX_H_BWD and 2 <= K <= MAX_K
+                and nt <= ntmax and (self.data_min is None or self.data_max is None))
+
+    def _n_transformed(self):
+        """Number of transformed (mask == 0) dimensions, cached per mask version (no sync)."""
+        m = self.mask
+        key = (m.data_ptr(), m._version)
+        c = self.__dict__.get("_nfx_nt")
+        if c is None or c[0] != key:
+            c = (key, int((m == 0).sum()))
+            object.__setattr__(self, "_nfx_nt", c)
+        return c[1]
+
+    def _build_bwd_pack(self, device):
+        d, H, K = self.data_dim, self._hidden(), self.num_bins
+        L = _lib.lib()
+        packed = torch.empty(L.nfx_spline_backward_packed_floats(d, H, K), device=device, dtype=torch.float32)
+        raw, keep = _lib.mlp_raw([self.param_net[0], self.param_net[2], self.param_net[4]])
+        mask = self.mask.detach().to(device=device, dtype=torch.float32).contiguous()
+        _lib.check(L.nfx_spline_pack_backward(raw, _lib.ptr(mask), d, H, K, _lib.ptr(packed),
+                                              _lib.stream_of(packed)), "nfx_spline_pack_backward")
+        packed._nfx_keep = (keep, mask)
+        return packed, mask
+
+    def _hip_backward(self, x, gy, gld, direction):
+        """dL/dx and the parameter gradients (parameters() order) of one forward/inverse call:
+        nfx_spline_coupling_backward (MLP recompute, spline adjoint, data-gradient chain and the
+        weight-gradient contractions in one kernel, then a fixed-order workgroup reduction)."""
+        x = x.contiguous()
+        B, d = x.shape
+        H, K = self._hidden(), self.num_bins
+        gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
+        gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
+        packed, mask = self._packed(x.device, self._build_bwd_pack, slot="_nfx_bwd_pack_cache")
+        L = _lib.lib()
+        gx = torch.empty_like(x)
+        grads = torch.empty(L.nfx_spline_backward_param_floats(d, H, K), device=x.device, dtype=torch.float32)
+        ws = torch.empty(L.nfx_spline_backward_workspace_bytes(B, d, H, K), device=x.device, dtype=torch.uint8)
+        nt = self._n_transformed()
+        ev = BACKWARD_EVENTS
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _lib.check(L.nfx_spline_coupling_backward(
+            _lib.ptr(packed), _lib.ptr(mask), _lib.ptr(x), _lib.ptr(gy), _lib.ptr(gld), _lib.ptr(gx),
+            _lib.ptr(grads), _lib.ptr(ws), B, d, H, K, nt, float(self.bound), float(self.min_bin_width),
+            float(self.min_bin_height), float(self.min_derivative), int(direction), _lib.stream_of(x)),
+            "nfx_spline_coupling_backward")
+        if ev is not None:
+            e1.record()
+            ev.append(("spline_bwd_kernel", e0, e1))
+        out, o = [], 0
+        for prm in self.parameters():
+            n = prm.numel()
+            out.append(grads[o:o + n].view_as(prm))
+            o += n
+        grads._nfx_keep = ws
+        return gx, out
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
         packed = self._packed(x.device, self._build_pack)
