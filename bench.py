@@ -138,6 +138,14 @@ def build(config):
         # training step: forward recompute + data-gradient chain in the fused backward kernel
         return m, d, 2 * f, spec, "cfg4t 5x MaskedAutoregressiveFlow(63, 64) training step " \
                                   "(-log_prob mean, fused backward, Adam), train mode"
+    if config == "cfg3t":
+        m, d, _, spec, _ = build("cfg3")
+        H, P = 64, 3 * 8 - 1
+        # fused spline backward per sample: MLP recompute (H + H^2 + H P), data-gradient chain
+        # (P H + H^2 + H) and weight-gradient contractions (P H + H^2 + H), 2 flop each
+        f = 2 * (3 * H * H + 3 * H + 3 * H * P)
+        return m, d, f, spec, "cfg3t 8x SplineCouplingLayer(2, 64, K=8) training step " \
+                              "(-log_prob mean, fused spline backward, Adam)"
     if config in ("cfg5f", "cfg5i"):
         torch.manual_seed(40)
         m = nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)])
@@ -154,7 +162,8 @@ def build(config):
     raise ValueError(config)
 
 # per-GPU batch of each config (weak scaling unit)
-DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "cfg3": 1_000_000, "cfg4": 500_000,
+DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
+                 "cfg4": 500_000,
                  "cfg4t": 500_000, "cfg5f": 524_288,
                  "cfg5i": 8_192, "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000,
                  "sample4k_iaf": 4_000}
@@ -235,7 +244,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg2t", "train5k", "cfg3", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
+                    choices=["cfg2", "cfg2t", "train5k", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
                              "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
@@ -255,7 +264,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     model, d, f_layer, spec, desc = build(a.config)
-    training = a.config in ("cfg4t", "cfg2t", "train5k")
+    training = a.config in ("cfg4t", "cfg2t", "train5k", "cfg3t")
     coupling_train = a.config in ("cfg2t", "train5k")
     if coupling_train and world > 1:
         from nfs_amd.distributed import enable_sync_batchnorm
@@ -314,6 +323,8 @@ def main():
         return sums
 
     from nfs_amd.flows import autoregressive as _ar
+    from nfs_amd.flows import spline as _sp
+    bwd_mod = _sp if a.config == "cfg3t" else _ar
     with torch.set_grad_enabled(training):
         for _ in range(a.warmup):
             step()
@@ -341,12 +352,12 @@ def main():
             events = [e for e in _cp.TRAIN_EVENTS if e[0].endswith("<BWD2>")]
             _cp.TRAIN_EVENTS = None
         elif training:
-            _ar.BACKWARD_EVENTS = []
+            bwd_mod.BACKWARD_EVENTS = []
             for _ in range(a.steps):
                 step()
             torch.cuda.synchronize()
-            events = _ar.BACKWARD_EVENTS
-            _ar.BACKWARD_EVENTS = None
+            events = bwd_mod.BACKWARD_EVENTS
+            bwd_mod.BACKWARD_EVENTS = None
         else:
             flow.layer_events = []
             for _ in range(a.steps):
@@ -420,6 +431,12 @@ def main():
             if world > 1:
                 result["config"]["parallelism"] = (f"dp{world} (sample shards, SyncBN: 4 all-gathers/all-reduces "
                                                    f"of <= 3 KB per layer + 1 bucketed gradient all-reduce)")
+        elif a.config == "cfg3t":
+            result["metric"] = "training samples/sec/GPU (8x RQ-spline coupling d=2 density step)"
+            result["nll_f64"] = None
+            result["roofline"]["note"] = ("dominant kernel = the fused spline backward (MLP recompute, "
+                                          "spline adjoint, data-gradient chain and the sample-contraction "
+                                          "weight gradients on MFMA, 3x the layer's forward MLP flops)")
         elif training:
             result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
             result["nll_f64"] = None
