@@ -10,6 +10,9 @@
 // weight gradients as MFMA contractions over the sample dimension (per-wave LDS transposes, as
 // in nfx_affine_train_kernel.h). Reference: src/flows/spline/spline_coupling_layer.py:96-309.
 #pragma once
+#ifndef NFX_SBWD_EXPT
+#define NFX_SBWD_EXPT 0
+#endif
 #include "nfx_affine_train_kernel.h"  // transpose_tile, kTS
 #include "nfx_spline_kernel.h"        // SplineConsts, tsoftplus, crow/mfma helpers
 
@@ -538,7 +541,13 @@ __global__ __launch_bounds__(256) void spline_bwd_kernel(
                 float o, gp[32], gvs;
                 // z_dt is non-finite only when the spline fell back to a non-finite input: the
                 // layer guard then blocks the output gradient
+#if NFX_SBWD_EXPT == 1
+                o = v; gvs = go;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) gp[i] = prm[i] * go + cur.gl;
+#else
                 rq_spline_adjoint<K, INV>(v, prm, C, nonfinite(v) ? 0.f : go, cur.gl, o, gp, gvs);
+#endif
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     zr[j] = (j == dt) ? o : zr[j];
@@ -562,6 +571,7 @@ __global__ __launch_bounds__(256) void spline_bwd_kernel(
 #pragma unroll
                 for (int q = 0; q < 16; ++q) sb += Te[q];
                 a_b3[t] += sb;
+#if NFX_SBWD_EXPT != 2
 #pragma unroll
                 for (int kt = 0; kt < HT; ++kt) {
                     float Th[16];
@@ -569,6 +579,7 @@ __global__ __launch_bounds__(256) void spline_bwd_kernel(
 #pragma unroll
                     for (int q = 0; q < 16; ++q) a_w3[t][kt] = mfma32(Te[q], Th[q], a_w3[t][kt]);
                 }
+#endif
             }
         }
         // layer 2: delta2 = relu'(h2) g2; dW2 += delta2 h1^T; dL/dh1 = W2^T delta2
@@ -583,6 +594,7 @@ __global__ __launch_bounds__(256) void spline_bwd_kernel(
             for (int q = 0; q < 16; ++q) sb += Te2[o2][q];
             a_b2[o2] += sb;
         }
+#if NFX_SBWD_EXPT != 2
 #pragma unroll
         for (int kt = 0; kt < HT; ++kt) {
             float Th[16];
@@ -592,6 +604,7 @@ __global__ __launch_bounds__(256) void spline_bwd_kernel(
 #pragma unroll
                 for (int q = 0; q < 16; ++q) a_w2[o2][kt] = mfma32(Te2[o2][q], Th[q], a_w2[o2][kt]);
         }
+#endif
         float gxp[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) gxp[j] = 0.f;
