@@ -161,7 +161,8 @@ size_t nfx_made_packed_floats(int d, int H);
 int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
 int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
                     int64_t B, int d, int H, int variant, int accumulate, void* stream);
-/* NFX_MAF_INVERSE (d <= 64) + fused log_prob epilogue (see nfx_affine_coupling_logprob);
+/* Density direction + fused log_prob epilogue (see nfx_affine_coupling_logprob):
+ * NFX_MAF_INVERSE with d <= 64 or H <= 64, NFX_IAF_INVERSE (sequential) with H <= 64;
  * NFX_EUNSUPPORTED otherwise (use nfx_gauss_logprob after nfx_made_affine). */
 int nfx_made_affine_logprob(const float* packed, const float* in, float* out, float* log_det,
                             float* logp, double* sums, void* workspace, int64_t B, int d, int H,

@@ -2,7 +2,7 @@
 // Kernels: nfx_made_kernel.h (parallel instantiations in nfx_made_par.hip).
 #include "nfx_made_kernel.h"
 #include "nfx_made_wide_kernel.h"
-#include "nfx_made_seqg_kernel.h"
+#include "nfx_made_seqs_kernel.h"
 #include "nfx_pack.h"
 
 namespace nfx {
@@ -137,11 +137,12 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
 }
 
 template <int HT>
-made_seq_kernel_t made_seqg_pick_ht(int variant) {
-    return variant == NFX_MAF_FORWARD ? made_seqg_kernel<HT, NFX_MAF_FORWARD> : made_seqg_kernel<HT, NFX_IAF_INVERSE>;
+made_seqs_kernel_t made_seqs_pick_ht(int variant, bool logp) {
+    if (variant == NFX_MAF_FORWARD) return made_seqs_kernel<HT, NFX_MAF_FORWARD, false>;
+    return logp ? made_seqs_kernel<HT, NFX_IAF_INVERSE, true> : made_seqs_kernel<HT, NFX_IAF_INVERSE, false>;
 }
-template made_seq_kernel_t made_seqg_pick_ht<1>(int);
-template made_seq_kernel_t made_seqg_pick_ht<2>(int);
+template made_seqs_kernel_t made_seqs_pick_ht<1>(int, bool);
+template made_seqs_kernel_t made_seqs_pick_ht<2>(int, bool);
 
 template <int HT, int VAR>
 static made_seq_kernel_t seq_var() {
@@ -229,9 +230,11 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     const bool parallel = variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD;
     const size_t wide_lds_bytes = (size_t)wide_lds(L, HT).total * sizeof(float);
     const bool wide = parallel && d > kTileMaxD && HT <= 2 && wide_lds_bytes <= kLdsBytes;
-    if (fused && (variant != NFX_MAF_INVERSE || (d > kTileMaxD && !wide)))
+    const bool seqs = (variant == NFX_MAF_FORWARD || variant == NFX_IAF_INVERSE) && HT <= 2;
+    if (fused && !((variant == NFX_MAF_INVERSE && (d <= kTileMaxD || wide)) || (variant == NFX_IAF_INVERSE && seqs)))
         return set_error(NFX_EUNSUPPORTED,
-                         "made_affine_logprob: fused log_prob needs MAF inverse with d <= %d or H <= 64", kTileMaxD);
+                         "made_affine_logprob: fused log_prob needs MAF inverse with d <= %d or H <= 64, "
+                         "or IAF inverse with H <= 64", kTileMaxD);
     if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "made_affine_logprob: null logp/workspace");
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, s) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "made_affine: null pointer");
@@ -284,14 +287,17 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, nullptr, nullptr, 0.f);
         return check_launch("made_parallel_kernel");
     }
-    if (HT <= 2) {
-        made_seq_kernel_t k = HT == 1 ? made_seqg_pick_ht<1>(variant) : made_seqg_pick_ht<2>(variant);
-        const size_t lds = (size_t)seqg_lds(L.Hp).total * sizeof(float);
+    if (seqs) {
+        made_seqs_kernel_t k = HT == 1 ? made_seqs_pick_ht<1>(variant, fused) : made_seqs_pick_ht<2>(variant, fused);
+        const size_t lds = (size_t)seqs_lds(L.Hp).total * sizeof(float);
         int rc = prepare_lds((const void*)k, lds);
         if (rc) return rc;
-        const int grid = resident_grid((const void*)k, 512, lds, (B + 4 * kSeqgWaves - 1) / (4 * kSeqgWaves));
-        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate);
-        return check_launch("made_seqg_kernel");
+        int grid = resident_grid((const void*)k, 512, lds, (B + 4 * kSeqsWaves - 1) / (4 * kSeqsWaves));
+        if (grid > kMaxPartials) grid = kMaxPartials;
+        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials, gauss_const(d));
+        rc = check_launch("made_seqs_kernel");
+        if (rc || !fused) return rc;
+        return gauss_finish(partials, grid, sums, B, s);
     }
     made_seq_kernel_t k = pick_seq(HT, variant);
     if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no sequential kernel for H=%d", H);

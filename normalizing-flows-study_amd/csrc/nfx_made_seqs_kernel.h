@@ -1,0 +1,509 @@
+// Sequential MADE-affine directions, segment-parallel (MAF.forward = sampling, IAF.inverse =
+// density; H <= 64).
+//
+// Reference: masked_autoregressive_flow.py:46-78, inverse_autoregressive_flow.py:65-103 (d full
+// MADE calls on the partially filled vector). As in made_seq_kernel (nfx_made_kernel.h) every
+// hidden unit is computed once, when the input of its degree is known (made.py:56,63: unit a of
+// every hidden layer sees only inputs <= deg(a)), so a sample costs ONE MADE evaluation. What
+// this kernel adds is the observation that between two completion events the last hidden layer
+// does not change: output i reads only units with deg < i (made.py:72-78), so all steps in
+// (D_g, D_{g+1}] -- a "segment", ~d/H steps -- take their mu/alpha from the same h3 and are
+// mutually independent. They are evaluated together, in chunks of up to 16 steps:
+//   1. a 16-lane DPP row owns one sample (4 samples per wave); lane `sub` owns the hidden units
+//      of completion rank sub + 16k (k < Hp/16). For every step of the chunk each lane forms its
+//      partial mu/alpha dot products over its COMPLETED units only, register r holding step
+//      (r XOR sub); a 4-stage butterfly reduce-scatter (partners lane^8, ^7, ^2, ^1: row_ror:8,
+//      row_half_mirror, quad perms) leaves lane j with the full sums of step j -- 15 DPP adds
+//      per 16 steps, no dependency chain through the steps;
+//   2. lane j evaluates step j's affine map;
+//   3. the rank-1 updates of the layer-1 pre-activations with the chunk's new inputs, in step
+//      order, over the lane's INCOMPLETE units only (W1[a][i] is masked to zero for i > deg(a));
+//   4. the units of degree D_{g+1} complete (layer 1, then 2, then 3, row all-reduces).
+// Owning ranks sub + 16k (interleaved) keeps the completed/incomplete split within one unit per
+// lane at every segment, so the skipping in 1 and 3 is lane-uniform: with c completed units a
+// lane has floor(c/16) or ceil(c/16) completed slots, and steps 1/3 run ceil(c/16) resp.
+// Hp/16 - floor(c/16) slots (template-specialised, ~half the FMAs and LDS reads of dense).
+// The log-det and the fused Gaussian term are summed in step order (the reference's sequential
+// fp32 `ld -= alpha_i` and nfx_gauss_logprob's in-order z^2 sum), so results equal the
+// per-step formulation's up to the reduction order inside each mu/alpha dot product.
+// A non-finite step poisons every later step (the reference feeds NaN/Inf through the dense
+// masked matmul: 0*NaN = NaN), found per chunk with a wave ballot.
+// Weights (permuted to rank order on the fly): W2/W3, biases and the degree tables LDS-resident;
+// per-step rows (W1^T column, W4 mu/alpha rows, b4) staged in 64-step blocks into an LDS double
+// buffer by LDS-DMA, the next block in flight while the current one is processed; mu/alpha
+// weights interleaved per slot so the pair of dot products is one packed FMA (v_pk_fma_f32).
+#pragma once
+#include "nfx_made_kernel.h"
+
+namespace nfx {
+
+constexpr int kSeqsWaves = 8;  // 512-thread workgroups, 4 samples per wave
+constexpr int kSeqsStep = 64;  // steps per staged block
+constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * 16;  // per wave: x, z, alpha block tiles; chunk v
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Row stride of the interleaved (mu, alpha) W4 block rows: 2 Hp, padded by 4 floats at Hp = 64
+// so that the 16 lanes of a row group, reading slots of 16 different rows, hit 16 different
+// 16-byte bank granules: (33 (r ^ s) + 2 s) mod 16 is a permutation of s for every r. At Hp = 32
+// the unpadded (16 (r ^ s) + s) mod 16 = s already is.
+__host__ __device__ constexpr int seqs_w4_stride(int Hp) { return 2 * Hp + (Hp == 64 ? 4 : 0); }
+
+struct SeqsLds {
+    int w2, w3, b1, b2, b3, deg, gend, blk, blkf, wv, total;
+};
+
+// LDS image (floats). Unit of completion rank p sits at position pos(p) = (p % 16) * UPL + p / 16
+// inside a row (lane sub's slots k = 0..UPL-1 are contiguous); W2/W3 rows are indexed by rank.
+// Block image: w1t [64][Hp] | w4 [64][Hp][mu, alpha] (+4 pad floats per row: the phase-1 reads
+// of 16 different rows by the 16 lanes of a row group are then bank-conflict free) | b4 [mu 64 |
+// alpha 64].
+__host__ __device__ inline SeqsLds seqs_lds(int Hp) {
+    SeqsLds S{};
+    int o = 0;
+    S.w2 = o; o += Hp * Hp;
+    S.w3 = o; o += Hp * Hp;
+    S.b1 = o; o += Hp;    // by position
+    S.b2 = o; o += Hp;    // by rank
+    S.b3 = o; o += Hp;    // by rank
+    S.deg = o; o += Hp;   // degree by rank (padded units 1e9)
+    S.gend = o; o += Hp;  // first rank after rank p's degree group
+    S.blk = o; S.blkf = kSeqsStep * Hp + kSeqsStep * seqs_w4_stride(Hp) + 2 * kSeqsStep; o += 2 * S.blkf;
+    S.wv = o; o += kSeqsWaves * kSeqsTile;
+    S.total = o;
+    return S;
+}
+
+// One global_load_lds_dword: lane l's dword from `src` (per lane) to LDS lds_dst + 4l. Issued as
+// inline asm so the compiler does not know an LDS write is in flight: the builtin makes it wait
+// vmcnt(0) before every later ds_read (it cannot tell the DMA targets the other buffer), which
+// would expose the load latency once per block. Completion is waited for explicitly
+// (seqs_dma_wait) before the barrier that publishes the buffer.
+__device__ __forceinline__ void seqs_dma_dword(const float* src, float* lds_dst) {
+    const uint32_t m = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) float*)lds_dst);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(m))
+        : "memory");
+}
+__device__ __forceinline__ void seqs_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Keeps the compiler from moving LDS accesses across this point. A wave's DS operations execute
+// in order, so wave-private tiles need nothing more -- and, unlike a fence, this emits no
+// s_waitcnt vmcnt that would drain the next block's LDS-DMA in flight.
+__device__ __forceinline__ void seqs_lds_order() { asm volatile("" ::: "memory"); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 16 lanes of a DPP row; every lane of the row ends with the total.
+__device__ __forceinline__ float row16_allsum(float v) {
+    v = v + dpp<0xB1>(v);   // quad xor 1
+    v = v + dpp<0x4E>(v);   // quad xor 2
+    v = v + dpp<0x141>(v);  // row_half_mirror
+    v = v + dpp<0x140>(v);  // row_mirror
+    return v;
+}
+
+// N consecutive floats of a lane's slots starting at slot K0 (16-byte aligned row base).
+template <int K0, int N, int UPL>
+__device__ __forceinline__ void seqs_slots(const float* row, float (&w)[UPL]) {
+    if constexpr (N == 0) {
+        return;
+    } else if constexpr (K0 == 0 && N >= 3 && UPL == 4) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(row);
+        w[0] = t[0]; w[1] = t[1]; w[2] = t[2]; w[3] = t[3];
+    } else if constexpr (K0 % 2 == 0 && N >= 2) {
+        const float2 t = *reinterpret_cast<const float2*>(row + K0);
+        w[K0] = t.x; w[K0 + 1] = t.y;
+        if constexpr (N > 2) seqs_slots<K0 + 2, N - 2, UPL>(row, w);
+    } else {
+        w[K0] = row[K0];
+        if constexpr (N > 1) seqs_slots<K0 + 1, N - 1, UPL>(row, w);
+    }
+}
+
+// Reduce-scatter over a 16-lane row. On entry lane l, register r holds its partial for slot
+// (r ^ l); on exit p[0] of lane l holds the row total of slot l. Stage with partner l ^ m keeps
+// the registers whose index has the stage's bit clear and adds the partner's register r ^ m,
+// which holds the same slot: (r ^ m) ^ (l ^ m) = r ^ l.
+__device__ __forceinline__ void row16_reduce_scatter(float (&p)[16]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) p[r] = p[r] + dpp<0x128>(p[r + 8]);  // row_ror:8 = lane ^ 8
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = p[r] + dpp<0x141>(p[7 - r]);  // half mirror = lane ^ 7
+#pragma unroll
+    for (int r = 0; r < 2; ++r) p[r] = p[r] + dpp<0x4E>(p[r + 2]);   // lane ^ 2
+    p[0] = p[0] + dpp<0xB1>(p[1]);                                    // lane ^ 1
+}
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, float b, f32x2 c) {
+    return __builtin_elementwise_fma(a, f32x2{b, b}, c);
+}
+
+// Step 1 for KC completed slots. p[r] = this lane's (mu, alpha) row pairs of step ii + (r ^ sub):
+// 2*KC floats; the pair products are packed FMAs (v_pk_fma_f32: mu and alpha of one slot).
+// All 16 rows are read before any is used (sched_barrier): at two waves per SIMD the LDS
+// latency is hidden by reads in flight, not by the other wave.
+template <int KC, int UPL>
+__device__ __forceinline__ void seqs_dots(const float* w4r, const int (&offs)[16], const float (&h3v)[UPL],
+                                          float (&pm)[16], float (&pa)[16]) {
+    f32x4 ta[16], tb[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float* p = w4r + offs[r];
+        if constexpr (KC == 1) {
+            const f32x2 t = *reinterpret_cast<const f32x2*>(p);
+            ta[r] = f32x4{t[0], t[1], 0.f, 0.f};
+        } else {
+            ta[r] = *reinterpret_cast<const f32x4*>(p);
+        }
+        if constexpr (KC == 3) {
+            const f32x2 u = *reinterpret_cast<const f32x2*>(p + 4);
+            tb[r] = f32x4{u[0], u[1], 0.f, 0.f};
+        } else if constexpr (KC == 4) {
+            tb[r] = *reinterpret_cast<const f32x4*>(p + 4);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        f32x2 acc = {0.f, 0.f};
+        acc = pk_fma(f32x2{ta[r][0], ta[r][1]}, h3v[0], acc);
+        if constexpr (KC >= 2) acc = pk_fma(f32x2{ta[r][2], ta[r][3]}, h3v[1], acc);
+        if constexpr (KC >= 3) acc = pk_fma(f32x2{tb[r][0], tb[r][1]}, h3v[2], acc);
+        if constexpr (KC >= 4) acc = pk_fma(f32x2{tb[r][2], tb[r][3]}, h3v[3], acc);
+        pm[r] = acc[0];
+        pa[r] = acc[1];
+    }
+}
+
+// Step 3 for slots k >= K0 (the others are completed in every lane): pre1 += W1t[i] * v_i in
+// step order; w1r = this lane's slot 0 of step ii's row; pairs of slots as packed FMAs. Rows
+// read ahead of use as in seqs_dots.
+template <int K0, int UPL>
+__device__ __forceinline__ void seqs_rank1(const float* w1r, int Hp, const float (&cv)[16],
+                                           f32x2 (&pre1)[UPL / 2]) {
+    constexpr int NW = UPL - K0;
+    float w[16][UPL];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) seqs_slots<K0, NW, UPL>(w1r + j * Hp, w[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if constexpr (K0 % 2 == 1) pre1[K0 / 2][1] = fmaf(w[j][K0], cv[j], pre1[K0 / 2][1]);
+#pragma unroll
+        for (int k = (K0 + 1) / 2; k < UPL / 2; ++k)
+            pre1[k] = pk_fma(f32x2{w[j][2 * k], w[j][2 * k + 1]}, cv[j], pre1[k]);
+    }
+}
+
+template <int HT, int VAR, bool LOGP>
+__global__ __launch_bounds__(512) void made_seqs_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int d, int H, int accumulate, float* __restrict__ logp,
+    double* __restrict__ partials, float cgauss) {
+    constexpr int Hp = 32 * HT;
+    constexpr int UPL = Hp / 16;  // hidden-unit slots per lane
+    constexpr int RS4 = seqs_w4_stride(Hp);
+    constexpr int W4F = kSeqsStep * Hp;  // block image offsets
+    constexpr int B4F = W4F + kSeqsStep * RS4;
+    const MadeLayout L = made_layout(d, HT);
+    const SeqsLds S = seqs_lds(Hp);
+    extern __shared__ f32x4 lds4[];
+    float* lds = reinterpret_cast<float*>(lds4);
+    const float* P = packed;
+    const float* ordD = P + L.s_deg + Hp;      // degree of the rank-p unit
+    const float* ordU = P + L.s_deg + 2 * Hp;  // its unit index
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id(), slot = lane >> 4, sub = lane & 15;
+    auto rank_at = [](int pos) { return (pos % UPL) * 16 + pos / UPL; };
+
+    // rank-ordered resident image
+    for (int e = threadIdx.x; e < Hp * Hp; e += 512) {
+        const int p = e / Hp, q = rank_at(e % Hp);
+        const int a = (int)ordU[p], b = (int)ordU[q];
+        lds[S.w2 + e] = P[L.s_w2 + a * Hp + b];
+        lds[S.w3 + e] = P[L.s_w3 + a * Hp + b];
+    }
+    for (int p = threadIdx.x; p < Hp; p += 512) {
+        lds[S.b1 + p] = P[L.s_b1 + (int)ordU[rank_at(p)]];
+        lds[S.b2 + p] = P[L.s_b2 + (int)ordU[p]];
+        lds[S.b3 + p] = P[L.s_b3 + (int)ordU[p]];
+        lds[S.deg + p] = ordD[p];
+        int q = p + 1;
+        while (q < H && ordD[q] == ordD[p]) ++q;
+        lds[S.gend + p] = (float)q;
+    }
+    __syncthreads();
+    const float* degR = lds + S.deg;
+    const float* gendR = lds + S.gend;
+    float* xin_t = lds + S.wv + wave * kSeqsTile;  // [4][64] inputs of the block
+    float* zout_t = xin_t + 4 * kSeqsStep;         // [4][64] guarded outputs of the block
+    float* at_t = zout_t + 4 * kSeqsStep;          // [4][64] clamped alphas of the block
+    float* cv_t = at_t + 4 * kSeqsStep;            // [4][16] chunk: raw values (MADE inputs)
+    const int nblk = (d + kSeqsStep - 1) / kSeqsStep;
+    // staged-row columns of this lane: w1t rows by position l % Hp; w4 rows interleave
+    // (mu, alpha) per position, instruction `half` of a row covers positions 32 half + l / 2
+    const int colW1 = (int)ordU[rank_at(lane % Hp)];
+    const int colW4a = (int)ordU[rank_at((lane / 2) % Hp)];
+    const int colW4b = (int)ordU[rank_at((32 + lane / 2) % Hp)];
+    // phase-1 row offsets: register r <-> step (r ^ sub), this lane's slot pairs
+    int offs[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) offs[r] = (r ^ sub) * RS4 + sub * 2 * UPL;
+
+    // Block staging by LDS-DMA (global_load_lds_dword: lane-linear LDS destination, per-lane
+    // source): each wave-instruction fills 64 consecutive floats of the block image (a w1t row
+    // piece, half or all of a padded w4 row, a b4 half), columns gathered into rank positions.
+    // Rows past the end of d re-read the last valid row (finite; multiplied by exact zeros or
+    // discarded). Issued a block ahead into the other buffer.
+    constexpr int IPR = 2 * Hp / 64;  // instructions per w4 row
+    constexpr int NI = Hp + kSeqsStep * IPR + 2;
+    auto blk_stage = [&](int kb, int buf) {
+        const int i0 = kb * kSeqsStep;
+        const int n = d - i0 < kSeqsStep ? d - i0 : kSeqsStep;
+        float* dst = lds + S.blk + buf * S.blkf;
+        for (int j = wave; j < NI; j += kSeqsWaves) {
+            size_t src;
+            int off;
+            if (j < Hp) {
+                int row = (j * 64 + lane) / Hp;
+                row = row < n ? row : n - 1;
+                src = (size_t)L.s_w1t + (size_t)(i0 + row) * Hp + colW1;
+                off = 64 * j;
+            } else if (j < Hp + kSeqsStep * IPR) {
+                const int jj = j - Hp, half = jj % IPR;
+                int row = jj / IPR;
+                off = W4F + row * RS4 + 64 * half;
+                row = row < n ? row : n - 1;
+                const int h = lane & 1;
+                src = (size_t)L.s_w4 + (size_t)(h * d + i0 + row) * Hp + (half ? colW4b : colW4a);
+            } else {
+                const int c = lane < n ? lane : n - 1, jb = j - (Hp + kSeqsStep * IPR);
+                src = (size_t)L.s_b4 + (size_t)jb * d + i0 + c;
+                off = B4F + 64 * jb;
+            }
+            seqs_dma_dword(P + src, dst + off);
+        }
+    };
+    auto x_load = [&](int64_t gb, int kb, float (&xr)[4]) {
+        const int i0 = kb * kSeqsStep;
+        const int n = d - i0 < kSeqsStep ? d - i0 : kSeqsStep;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t sr = gb + wave * 4 + q;
+            xr[q] = (sr < B && lane < n) ? in[sr * d + i0 + lane] : 0.f;
+        }
+    };
+
+    double lpacc = 0.0;
+    for (int64_t gb = (int64_t)blockIdx.x * kSeqsWaves * 4; gb < B; gb += (int64_t)gridDim.x * kSeqsWaves * 4) {
+        const int64_t s = gb + wave * 4 + slot;  // this row's sample
+        const bool valid = s < B;
+        f32x2 pre1[UPL / 2];
+        float h1v[UPL], h2v[UPL], h3v[UPL];
+#pragma unroll
+        for (int k = 0; k < UPL; ++k) {
+            pre1[k / 2][k % 2] = lds[S.b1 + sub * UPL + k];
+            h1v[k] = h2v[k] = h3v[k] = 0.f;
+        }
+        float ld = 0.f, zsq = 0.f;
+        bool poisoned = false;
+        int gi = 0;  // completed units (ranks < gi)
+        int nextdeg = __builtin_amdgcn_readfirstlane(H > 0 ? (int)degR[0] : d);
+
+        float xr[4];
+        x_load(gb, 0, xr);
+        __syncthreads();  // previous group's readers of the staging buffers are done
+        blk_stage(0, 0);
+        seqs_dma_wait();
+        __syncthreads();
+
+        for (int kb = 0; kb < nblk; ++kb) {
+            const int i0 = kb * kSeqsStep;
+            const int n = d - i0 < kSeqsStep ? d - i0 : kSeqsStep;
+            const float* blk = lds + S.blk + (kb & 1) * S.blkf;
+            const float* w1b = blk;
+            const float* w4b = blk + W4F;
+            const float* bmb = blk + B4F;
+            const float* bab = bmb + kSeqsStep;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xin_t[q * kSeqsStep + lane] = xr[q];
+                if (lane >= n) zout_t[q * kSeqsStep + lane] = at_t[q * kSeqsStep + lane] = 0.f;
+            }
+            const bool more = kb + 1 < nblk;
+            if (more) {
+                blk_stage(kb + 1, (kb + 1) & 1);  // its readers finished the previous block
+                x_load(gb, kb + 1, xr);
+            }
+            seqs_lds_order();
+
+            for (int ii = 0; ii < n;) {
+                const int i = i0 + ii;
+                int nc = n - ii < 16 ? n - ii : 16;
+                if (nextdeg - i + 1 < nc) nc = nextdeg - i + 1;
+                // 1. partial mu/alpha dot products over the completed slots
+                float pm[16], pa[16];
+                const float* w4r = w4b + ii * RS4;
+                const int kc1 = (gi + 15) >> 4;
+                switch (kc1 < UPL ? kc1 : UPL) {
+                    case 0:
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) pm[r] = pa[r] = 0.f;
+                        break;
+                    case 1: seqs_dots<1, UPL>(w4r, offs, h3v, pm, pa); break;
+                    case 2: seqs_dots<2, UPL>(w4r, offs, h3v, pm, pa); break;
+                    case 3: if constexpr (UPL >= 3) seqs_dots<(UPL >= 3 ? 3 : 1), UPL>(w4r, offs, h3v, pm, pa); break;
+                    default: seqs_dots<UPL, UPL>(w4r, offs, h3v, pm, pa); break;
+                }
+                row16_reduce_scatter(pm);
+                row16_reduce_scatter(pa);
+                // 2. lane sub evaluates step ii + sub (lanes past the chunk compute garbage, unused)
+                const bool vj = sub < nc;
+                const int rj = ii + sub;
+                float mu = pm[0] + bmb[rj];
+                float al = pa[0] + bab[rj];
+                if (poisoned) {
+                    mu = __builtin_nanf("");
+                    al = mu;
+                }
+                const float xin = xin_t[slot * kSeqsStep + rj];
+                float vi, vo, a;
+                if constexpr (VAR == NFX_MAF_FORWARD) {
+                    // masked_autoregressive_flow.py:57-65
+                    a = tclamp(al, -3.f, 3.f);
+                    vi = xin * exp_fast(a) + mu;
+                } else {
+                    // inverse_autoregressive_flow.py:79-88
+                    a = tclamp(al, -2.f, 2.f);
+                    const float m = tclamp(mu, -10.f, 10.f);
+                    vi = (xin - m) * exp_fast(-a);
+                }
+                // the first non-finite step of the chunk poisons the later ones (and the rest)
+                const uint64_t bad = __ballot(vj && nonfinite(vi));
+                const unsigned rowbad = (unsigned)(bad >> (slot * 16)) & 0xFFFFu;
+                if (rowbad) {
+                    if (sub > __builtin_ctz(rowbad)) {
+                        vi = __builtin_nanf("");
+                        a = vi;
+                    }
+                    poisoned = true;
+                }
+                if constexpr (VAR == NFX_MAF_FORWARD) vo = nonfinite(vi) ? 0.f : vi;
+                else vo = nonfinite(vi) ? xin : vi;
+                cv_t[slot * 16 + sub] = vj ? vi : 0.f;
+                if (vj) {
+                    zout_t[slot * kSeqsStep + rj] = vo;
+                    at_t[slot * kSeqsStep + rj] = a;
+                }
+                seqs_lds_order();
+                float cv[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const f32x4 tv = *reinterpret_cast<const f32x4*>(cv_t + slot * 16 + 4 * q);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) cv[4 * q + c] = tv[c];
+                }
+                // 3. rank-1 updates of the incomplete slots' layer-1 pre-activations, step order
+                const float* w1r = w1b + ii * Hp + sub * UPL;
+                const int kc3 = gi >> 4;
+                switch (kc3 < UPL ? kc3 : UPL) {
+                    case 0: seqs_rank1<0, UPL>(w1r, Hp, cv, pre1); break;
+                    case 1: seqs_rank1<1, UPL>(w1r, Hp, cv, pre1); break;
+                    case 2: if constexpr (UPL > 2) seqs_rank1<2, UPL>(w1r, Hp, cv, pre1); break;
+                    case 3: if constexpr (UPL > 3) seqs_rank1<3, UPL>(w1r, Hp, cv, pre1); break;
+                    default: break;
+                }
+                seqs_lds_order();  // the chunk tile is rewritten by the next chunk
+                // 4. the units of degree nextdeg (ranks gi .. q-1) complete: layer 1, 2, 3
+                if (i + nc - 1 == nextdeg) {
+                    const int q = __builtin_amdgcn_readfirstlane((int)gendR[gi]);
+#pragma unroll
+                    for (int k = 0; k < UPL; ++k) {
+                        const int p = sub + 16 * k;
+                        if (p >= gi && p < q) h1v[k] = trelu(pre1[k / 2][k % 2]);
+                    }
+                    for (int p = gi; p < q; ++p) {
+                        float w[UPL];
+                        seqs_slots<0, UPL, UPL>(lds + S.w2 + p * Hp + sub * UPL, w);
+                        float v = 0.f;
+#pragma unroll
+                        for (int k = 0; k < UPL; ++k) v = fmaf(w[k], h1v[k], v);
+                        v = trelu(row16_allsum(v) + lds[S.b2 + p]);
+#pragma unroll
+                        for (int k = 0; k < UPL; ++k)
+                            if (p == sub + 16 * k) h2v[k] = v;
+                    }
+                    for (int p = gi; p < q; ++p) {
+                        float w[UPL];
+                        seqs_slots<0, UPL, UPL>(lds + S.w3 + p * Hp + sub * UPL, w);
+                        float v = 0.f;
+#pragma unroll
+                        for (int k = 0; k < UPL; ++k) v = fmaf(w[k], h2v[k], v);
+                        v = trelu(row16_allsum(v) + lds[S.b3 + p]);
+#pragma unroll
+                        for (int k = 0; k < UPL; ++k)
+                            if (p == sub + 16 * k) h3v[k] = v;
+                    }
+                    gi = q;
+                    nextdeg = __builtin_amdgcn_readfirstlane(gi < H ? (int)degR[gi] : d);
+                }
+                ii += nc;
+            }
+            seqs_lds_order();
+            // log-det and z^2 of the block in step order (steps past d hold exact zeros)
+#pragma unroll 4
+            for (int j = 0; j < kSeqsStep; j += 4) {
+                const f32x4 ta = *reinterpret_cast<const f32x4*>(at_t + slot * kSeqsStep + j);
+                const f32x4 tz = *reinterpret_cast<const f32x4*>(zout_t + slot * kSeqsStep + j);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if constexpr (VAR == NFX_MAF_FORWARD) ld = ld + ta[c];
+                    else ld = ld - ta[c];
+                    if constexpr (LOGP) zsq = gauss_sq(zsq, tz[c]);
+                }
+            }
+            // this wave's 4 output rows for the block (coalesced)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t so = gb + wave * 4 + q;
+                if (so < B && lane < n) out[so * d + i0 + lane] = zout_t[q * kSeqsStep + lane];
+            }
+            seqs_dma_wait();  // the next block's LDS-DMA has landed
+            __syncthreads();  // ... for every wave; and every wave is done with this block
+        }
+        if (valid && sub == 0) {
+            if (nonfinite(ld)) ld = 0.f;
+            ld = (VAR == NFX_MAF_FORWARD) ? tclamp(ld, -100.f, 100.f) : tclamp(ld, -50.f, 50.f);
+            const float ldt = accumulate ? logdet[s] + ld : ld;
+            logdet[s] = ldt;
+            if constexpr (LOGP) {
+                const float lp = gauss_lp(zsq, cgauss, ldt);
+                logp[s] = lp;
+                lpacc += (double)lp;
+            }
+        }
+    }
+    if constexpr (LOGP) {
+        const double t = block_sum_f64<512>(lpacc);
+        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+    }
+}
+
+typedef void (*made_seqs_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int, float*,
+                                   double*, float);
+
+template <int HT>
+made_seqs_kernel_t made_seqs_pick_ht(int variant, bool logp);
+
+}  // namespace nfx

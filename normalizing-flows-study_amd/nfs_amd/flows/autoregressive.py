@@ -223,8 +223,6 @@ class _MadeAffineFlow(HipFlow):
 
     def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
         variant = self._variant(-1)
-        if variant != _lib.NFX_MAF_INVERSE:
-            return False  # sequential IAF inverse: separate Gaussian pass
         packed = self._packed(x.device, self._build_pack)
         rc = _lib.lib().nfx_made_affine_logprob(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), _lib.ptr(logp),

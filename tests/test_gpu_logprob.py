@@ -2,7 +2,7 @@
 
 NormalizingFlowModel.log_prob runs the last layer of the inverse chain through its
 `*_logprob` entry point when it has one (affine coupling, spline coupling, MAF inverse with
-d <= 64 or H <= 64)
+d <= 64 or H <= 64, the sequential IAF inverse with H <= 64)
 and through nfx_gauss_logprob otherwise. Both evaluate
     logp = -0.5 * (fp32(d log 2pi) + sum_j z_j^2) + log_det
 with the same sequential fp32 sum, so the fused per-sample logp must be BIT-identical to
@@ -60,18 +60,25 @@ def _model(kind):
         return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 8), 100, False
     if kind == "iaf10_sequential":
         fl = [nfs_amd.InverseAutoregressiveFlow(10, 32) for _ in range(2)]
-        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 7), 10, False
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 7), 10, True
+    if kind == "iaf150_sequential":
+        fl = [nfs_amd.InverseAutoregressiveFlow(150, 64) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 9), 150, True
+    if kind == "iaf20_h96_sequential":
+        fl = [nfs_amd.InverseAutoregressiveFlow(20, 96) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 10), 20, False
     raise ValueError(kind)
 
 
 KINDS = ["realnvp", "realnvp_bn_between", "affine_d5_h96", "spline_k5", "maf63",
-         "maf80_wide", "maf100_h128_chunked", "iaf10_sequential"]
+         "maf80_wide", "maf100_h128_chunked", "iaf10_sequential", "iaf150_sequential",
+         "iaf20_h96_sequential"]
 
 
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("B", [0, 1, 77, 4099, 300_001])
 def test_fused_logprob_matches_unfused(cuda_device, kind, B):
-    if kind == "iaf10_sequential" and B > 4099:
+    if kind.startswith("iaf") and B > 4099:
         pytest.skip("sequential IAF inverse: small batches only")
     m, d, fused_expected = _model(kind)
     m = m.to(cuda_device).eval()

@@ -91,7 +91,8 @@ def test_small_made_flows(cuda_device, name, kind):
 
 
 @pytest.mark.parametrize("d,H,B", [(5, 16, 1), (33, 32, 65), (63, 96, 130), (100, 128, 257), (7, 64, 1000),
-                                   (65, 64, 129), (100, 32, 700), (200, 64, 1500), (784, 64, 77)])
+                                   (65, 64, 129), (100, 32, 700), (200, 64, 1500), (784, 64, 77),
+                                   (300, 16, 33), (130, 48, 70), (129, 64, 35)])
 def test_made_shapes_vs_oracle(cuda_device, d, H, B):
     torch.manual_seed(d * 31 + H)
     for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
