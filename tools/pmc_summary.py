@@ -18,7 +18,7 @@ import statistics
 import sys
 
 HOT = ("affine_coupling_kernel", "spline_coupling_kernel", "made_parallel_kernel", "made_tile_kernel", "made_seq_kernel",
-       "made_wide_kernel", "made_seqg_kernel", "gauss_logprob_kernel", "rqs_unit_kernel")
+       "made_wide_kernel", "made_seqs_kernel", "gauss_logprob_kernel", "rqs_unit_kernel")
 
 
 def rows(path_glob):
