@@ -21,6 +21,7 @@ namespace nfx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Row of register r in lane-half h of a 32x32 fp32 MFMA accumulator.
 __host__ __device__ constexpr int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }

@@ -41,7 +41,7 @@ constexpr int kSeqsWaves = 8;  // 512-thread workgroups, 4 samples per wave
 constexpr int kSeqsStep = 64;  // steps per staged block
 constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * 16;  // per wave: x, z, alpha block tiles; chunk v
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 
 // Row stride of the interleaved (mu, alpha) W4 block rows: 2 Hp, padded by 4 floats at Hp = 64
 // so that the 16 lanes of a row group, reading slots of 16 different rows, hit 16 different
