@@ -94,93 +94,41 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 
     // Layer 2 (H x H) tile by tile; each finished tile is ReLU'd and folded into the
     // output-layer partial dot products right away (keeps one tile of h2 live).
+    float part[D][2];
+#pragma unroll
+    for (int j = 0; j < D; ++j) part[j][0] = part[j][1] = 0.f;
     const f32x4* wg = reinterpret_cast<const f32x4*>(P + L.w2) + lane;
-    if constexpr (D <= 2) {
-        // part[j][e] = (sample tile 0, sample tile 1) partial sums over even / odd hidden rows:
-        // one packed FMA (v_pk_fma_f32, per element the same fmaf) per hidden row serves both
-        // sample tiles; rows outer / outputs inner gives 2D independent chains (a dependent
-        // packed FMA needs a wait state) with one w3 quad per output live (VGPRs <= 168: three
-        // waves per SIMD). Halves the output layer's vector instructions.
-        f32x2 part[D][2];
 #pragma unroll
-        for (int j = 0; j < D; ++j) part[j][0] = part[j][1] = f32x2{0.f, 0.f};
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a0, a1;
+        a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
 #pragma unroll
-        for (int hto = 0; hto < HT; ++hto) {
-            f32x16 a0, a1;
-            a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
-#pragma unroll
-            for (int kt = 0; kt < HT; ++kt) {
-#pragma unroll
-                for (int rq = 0; rq < 4; ++rq) {
-                    // (a one-group-ahead weight prefetch here measured 5% slower: the compiler
-                    // then interleaves both nets at 217 VGPRs = 2 waves/SIMD instead of 3)
-                    const f32x4 w = wg[((hto * HT + kt) * 4 + rq) * 64];
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
-                        a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
-                    }
-                }
-            }
-            const f32x4* w3q = reinterpret_cast<const f32x4*>(P + L.w3 + hto * 32 + 16 * h);
+        for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
             for (int rq = 0; rq < 4; ++rq) {
-                f32x4 w3[D];
-#pragma unroll
-                for (int j = 0; j < D; ++j) w3[j] = w3q[j * HT * 8 + rq];
+                // (a one-group-ahead weight prefetch here measured 5% slower: the compiler
+                // then interleaves both nets at 217 VGPRs = 2 waves/SIMD instead of 3)
+                const f32x4 w = wg[((hto * HT + kt) * 4 + rq) * 64];
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
-                    const int r = 4 * rq + rr;
-                    const f32x2 h2 = {trelu(a0[r]), trelu(a1[r])};
-#pragma unroll
-                    for (int j = 0; j < D; ++j)
-                        part[j][r & 1] = __builtin_elementwise_fma(h2, f32x2{w3[j][rr], w3[j][rr]}, part[j][r & 1]);
+                    a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
+                    a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
                 }
             }
         }
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const f32x2 t = part[j][0] + part[j][1];
-            res[j] = tclamp(halves_sum(t[0], t[1]) + P[L.b3 + j], -10.f, 10.f);
-        }
-    } else {
-        // wider outputs: scalar chains, one w3 row of 16 live at a time (no register room for
-        // the packed form's row pairs)
-        float part[D][2];
+            const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + hto) * 32, h);
 #pragma unroll
-        for (int j = 0; j < D; ++j) part[j][0] = part[j][1] = 0.f;
-#pragma unroll
-        for (int hto = 0; hto < HT; ++hto) {
-            f32x16 a0, a1;
-            a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
-#pragma unroll
-            for (int kt = 0; kt < HT; ++kt) {
-#pragma unroll
-                for (int rq = 0; rq < 4; ++rq) {
-                    // (a one-group-ahead weight prefetch here measured 5% slower: the compiler
-                    // then interleaves both nets at 217 VGPRs = 2 waves/SIMD instead of 3)
-                    const f32x4 w = wg[((hto * HT + kt) * 4 + rq) * 64];
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
-                        a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + hto) * 32, h);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    part[j][0] = fmaf(w3[r], trelu(a0[r]), part[j][0]);
-                    part[j][1] = fmaf(w3[r], trelu(a1[r]), part[j][1]);
-                }
+            for (int r = 0; r < 16; ++r) {
+                part[j][0] = fmaf(w3[r], trelu(a0[r]), part[j][0]);
+                part[j][1] = fmaf(w3[r], trelu(a1[r]), part[j][1]);
             }
         }
-#pragma unroll
-        for (int j = 0; j < D; ++j)
-            res[j] = tclamp(halves_sum(part[j][0], part[j][1]) + P[L.b3 + j], -10.f, 10.f);
     }
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        res[j] = tclamp(halves_sum(part[j][0], part[j][1]) + P[L.b3 + j], -10.f, 10.f);
 }
 
 // LOGP: fused log_prob epilogue for the last layer of an inverse chain — logp = -0.5*(c +
