@@ -1,5 +1,7 @@
 // Affine-coupling kernel template (see nfx_affine.hip for the design notes).
 #pragma once
+#include <type_traits>
+
 #include "nfx_common.h"
 
 namespace nfx {
@@ -64,8 +66,9 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v
 }
 
 // Conditioner MLP of one net for a 64-sample chunk; returns clamp(net(x*m), -10, 10)[j] for the
-// lane's own sample (lane l <-> sample chunk*64 + l).
-template <int HT, int D>
+// lane's own sample (lane l <-> sample chunk*64 + l). TILES = 1: a 32-sample half chunk (sample
+// tile 1 is skipped; lanes 32..63 return unused values).
+template <int HT, int D, int TILES = 2>
 __device__ __forceinline__ void affine_net(const float* __restrict__ P, const AffineLayout& L,
                                            const float (&xb)[2][(D + 1) / 2], float (&res)[D]) {
     constexpr int KS1 = (D + 1) / 2;
@@ -81,12 +84,12 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
         for (int ks = 0; ks < KS1; ++ks) {
             const float w = P[L.w1 + (ht * KS1 + ks) * 64 + lane];
             a0 = mfma32(w, xb[0][ks], a0);
-            a1 = mfma32(w, xb[1][ks], a1);
+            if constexpr (TILES == 2) a1 = mfma32(w, xb[1][ks], a1);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             a0[r] = trelu(a0[r]);
-            a1[r] = trelu(a1[r]);
+            if constexpr (TILES == 2) a1[r] = trelu(a1[r]);
         }
         h1[ht][0] = a0;
         h1[ht][1] = a1;
@@ -112,7 +115,7 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
-                    a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
+                    if constexpr (TILES == 2) a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
                 }
             }
         }
@@ -122,7 +125,7 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 part[j][0] = fmaf(w3[r], trelu(a0[r]), part[j][0]);
-                part[j][1] = fmaf(w3[r], trelu(a1[r]), part[j][1]);
+                if constexpr (TILES == 2) part[j][1] = fmaf(w3[r], trelu(a1[r]), part[j][1]);
             }
         }
     }
@@ -156,27 +159,40 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
 #pragma unroll
     for (int ks = 0; ks < KS1; ++ks) mkb[ks] = (2 * ks + h < D) ? sm[L.mask + 2 * ks + h] : 0.f;
 
-    // Software pipeline: the x rows (both layouts) and the incoming log-det of chunk c + nwaves
-    // are loaded while chunk c computes, so HBM latency never sits in front of the MFMAs.
+    // Work split: every wave takes F = nchunks / nwaves whole 64-sample chunks (grid-stride); the
+    // R leftover chunks go out as 2R 32-sample half chunks, one to each of the first 2R waves
+    // (when 2R <= nwaves), so a SIMD's last round is half a chunk instead of a whole one: at
+    // B = 1M, 15.26 chunks per SIMD ran as 16, now as 15.5. (Otherwise the first R waves take
+    // one more whole chunk.)
+    const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t F = nchunks / nwaves, R = nchunks - F * nwaves;
+    const bool split = 2 * R <= nwaves;
+    const int64_t nfull = split ? F : F + (wv < R ? 1 : 0);
+    const bool half = split && wv < 2 * R;
+    const int64_t half_base = F * nwaves * 64 + wv * 32;
+
+    // Software pipeline: the x rows (both layouts) and the incoming log-det of the next unit are
+    // loaded while the current one computes, so HBM latency never sits in front of the MFMAs.
     struct Fetch {
-        float xb[2][KS1];  // layer-1 B operands x[sample base+32st+col][2ks+h] (unmasked)
+        float xb[2][KS1];  // layer-1 B operands x[base+32st+col][2ks+h] (unmasked)
         float xr[D];       // the lane's own sample row
         float ldin;        // log-det accumulated so far (accumulate = 1)
     };
-    auto fetch = [&](int64_t c, Fetch& f) {
-        const int64_t base = c * 64;
-        const bool live = c < nchunks;
+    // unit u < nfull: chunk wv + u nwaves (64 samples); u == nfull: the half chunk, if any
+    auto fetch = [&](int64_t u, Fetch& f) {
+        const int64_t base = u < nfull ? (wv + u * nwaves) * 64 : half_base;
+        const int nsamp = u < nfull ? 64 : (u == nfull && half ? 32 : 0);
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
             const int64_t s = base + 32 * st + col;
 #pragma unroll
             for (int ks = 0; ks < KS1; ++ks) {
                 const int k = 2 * ks + h;
-                f.xb[st][ks] = (live && k < D && s < B) ? in[s * D + k] : 0.f;
+                f.xb[st][ks] = (32 * st + col < nsamp && k < D && s < B) ? in[s * D + k] : 0.f;
             }
         }
         const int64_t so = base + lane;
-        if (live && so < B) {
+        if (lane < nsamp && so < B) {
             load_row<D>(in + so * D, f.xr);
             f.ldin = accumulate ? logdet[so] : 0.f;
         } else {
@@ -186,15 +202,11 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
         }
     };
 
-    int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    Fetch cur;
-    fetch(c, cur);
     double lpacc = 0.0;
-    for (; c < nchunks; c += nwaves) {
-        const int64_t base = c * 64;
+    // one unit: 2 sample tiles (TILES = 2) or the half chunk (TILES = 1, lanes 0..31)
+    auto unit = [&](auto tiles_c, int64_t base, const Fetch& cur) {
+        constexpr int TILES = decltype(tiles_c)::value;
         const float* smi = sm + opaque_zero();
-        Fetch nxt;
-        fetch(c + nwaves, nxt);
         float xb[2][KS1];
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -203,11 +215,11 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
         }
 
         float sv[D], bv[D];
-        affine_net<HT, D>(smi, L, xb, sv);
-        affine_net<HT, D>(smi + L.net, L, xb, bv);
+        affine_net<HT, D, TILES>(smi, L, xb, sv);
+        affine_net<HT, D, TILES>(smi + L.net, L, xb, bv);
 
         const int64_t so = base + lane;
-        if (so < B) {
+        if (lane < 32 * TILES && so < B) {
 #pragma clang fp contract(off)  // separate mul/add roundings, as the reference's torch ops
             float y[D];
             float ld = 0.f;
@@ -239,8 +251,17 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
                 lpacc += (double)lp;
             }
         }
+    };
+
+    Fetch cur;
+    fetch(0, cur);
+    for (int64_t u = 0; u < nfull; ++u) {
+        Fetch nxt;
+        fetch(u + 1, nxt);
+        unit(std::integral_constant<int, 2>{}, (wv + u * nwaves) * 64, cur);
         cur = nxt;
     }
+    if (half) unit(std::integral_constant<int, 1>{}, half_base, cur);
     if constexpr (LOGP) {
         const double t = block_sum_f64<256>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
