@@ -1,21 +1,32 @@
 """Benchmark: log_prob throughput of the gfx950 flow-transform hot path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5f|cfg5i]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5f|cfg5i|...]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-One step = one log_prob pass over the per-GPU batch: every flow layer's fused kernel
-(conditioner MLP on fp32 MFMA + transform + log-det accumulate), the fused Gaussian base term
-with the float64 NLL partial sum, and (N > 1) ONE RCCL all-reduce of the 16-byte partial
-[sum log p, count] — the whole data-parallel exchange of the path.
-Weak scaling: each rank owns a fixed 1M-sample shard (configs[1] of BASELINE.json at N=1).
-cfg5f / cfg5i (BASELINE configs[4], IAF(784, 64)): one step = the sampling pass forward(z)
-(parallel MADE kernel) / the density pass log_prob(x) through the sequential IAF inverse.
+One step = one log_prob pass over the batch: every flow layer's fused kernel (conditioner MLP
+on fp32 MFMA + transform + log-det accumulate), the fused Gaussian base term with the float64
+NLL partial sum, and (N > 1) ONE RCCL all-reduce of the 16-byte partial [sum log p, count] —
+the whole data-parallel exchange of the path.
+
+Scaling (default STRONG, north_star's ">= 6x strong scaling at 8 GPUs"): the BASELINE batch
+(cfg2 1M, cfg4 4M, cfg5 8,192 / 524,288) is split over the ranks; `--weak` gives every rank the
+whole batch instead. The weights are the reference's own (tests/golden/*.npz, produced by
+importing the reference) and the input is the G8 seeded batch, so the line also carries the
+global NLL against the reference's full-scale NLL ("test-NLL match", BASELINE.json metric).
+Eval passes replay a captured HIP graph by default (`--eager` for per-layer launches): at
+125k samples per GPU the ~20 us per-layer host issue cost would otherwise rival the kernels.
+
+At the default config (cfg2, RealNVP d=2) the line nests the second half of the metric, MAF
+d=63 (cfg4, 5x MAF(63,64), 4M samples split over the ranks), with its own roofline and CPU
+baseline under "maf_d63".
 
 Rank 0 prints ONE JSON line with the throughput, the roofline of the dominant kernel (HIP
 events on the launch stream, over the timed steps) and, at N=1, the oracle CPU baseline timed on
-this host on a bounded sample of the same workload.
+this host (threads = physical cores within this process's CPU allotment) on a bounded sample of
+the same workload.
 """
 import argparse
+import glob
 import json
 import math
 import os
@@ -161,12 +172,11 @@ def build(config):
         return m, d, f, spec, "cfg5i IAF(784, 64) log_prob (sequential inverse), eval"
     raise ValueError(config)
 
-# per-GPU batch of each config (weak scaling unit)
+# Batch of each config: the BASELINE global batch (strong scaling splits it over the ranks,
+# --weak gives every rank all of it).
 DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
-                 "cfg4": 500_000,
-                 "cfg4t": 500_000, "cfg5f": 524_288,
-                 "cfg5i": 8_192, "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000,
-                 "sample4k_iaf": 4_000}
+                 "cfg4": 4_000_000, "cfg4t": 500_000, "cfg5f": 524_288, "cfg5i": 8_192,
+                 "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000, "sample4k_iaf": 4_000}
 # The reference's only published throughput (assets/benchmark.png via
 # plots/_common.py:264-274): RealNVP(2,10,128) sampling, model.forward(z) on n = 4,000, CPU.
 # The same figure's other sampling numbers: Spline = RealNVPSpline(2,8,64) K=10,
@@ -175,22 +185,103 @@ PUBLISHED_SAMPLING = {"sample4k": ("RealNVP(2,10,128)", 186_000.0),
                       "sample4k_spline": ("RealNVPSpline(2,8,64), K=10", 334_000.0),
                       "sample4k_maf": ("6x MAF(2,64)", 602_000.0),
                       "sample4k_iaf": ("6x IAF(2,64)", 1_121_000.0)}
+# Reference-pinned workloads: weights from the golden fixture (written by importing the
+# reference, tests/golden/make_golden.py), input = the G8 seeded batch, result vs the reference's
+# own full-scale NLL / checksums (tests/golden/g8_full_nll.json).
+REFERENCE_RUN = {
+    "cfg2": {"npz": "g2_realnvp.npz", "prefix": "", "sub": "", "g8": "cfg2_realnvp_d2_B1M"},
+    "cfg3": {"npz": "g3_spline.npz", "prefix": "k8.", "sub": "", "g8": "cfg3_spline_k8_d2_B1M"},
+    "cfg4": {"npz": "g5_maf63.npz", "prefix": "", "sub": "", "g8": "cfg4_maf_d63_B4M"},
+    "cfg5i": {"npz": "g6_iaf784.npz", "prefix": "", "sub": "flows.0.", "g8": "cfg5i_iaf_d784_B8192"},
+    "cfg5f": {"npz": "g6_iaf784.npz", "prefix": "", "sub": "flows.0.", "g8": "cfg5f_iaf_d784_B524288"},
+}
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=262144):
+def load_reference_weights(model, config):
+    import numpy as np
+    spec = REFERENCE_RUN[config]
+    with np.load(os.path.join(GOLDEN, spec["npz"]), allow_pickle=False) as z:
+        arrs = {k: z[k] for k in z.files}
+    sd = {}
+    for k, v in model.state_dict().items():
+        gk = spec["prefix"] + (k[len(spec["sub"]):] if spec["sub"] and k.startswith(spec["sub"]) else k)
+        sd[k] = torch.from_numpy(np.array(arrs[gk])) if gk in arrs else v
+    model.load_state_dict(sd)
+
+
+def g8_meta(config):
+    with open(os.path.join(GOLDEN, "g8_full_nll.json")) as fh:
+        return json.load(fh)[REFERENCE_RUN[config]["g8"]]
+
+
+def made_executed_flop_per_sample(d, H):
+    """fp32 MFMA flops per sample the MADE tile kernel actually issues: per output tile of 32
+    rows, the k-loop stops at the last 32x32 block with a nonzero masked weight (structural
+    zeros of the sorted MADE degrees, DESIGN.md 'Structural zeros'); 16 v_mfma_f32_32x32x2_f32
+    (4,096 flop each) per block per 32 samples."""
+    from nfs_amd.flows.autoregressive import made_degrees
+    deg = torch.tensor(made_degrees(d, H))
+    i = torch.arange(d)
+    masks = [(i[None, :] <= deg[:, None]), (deg[None, :] <= deg[:, None]), (deg[None, :] <= deg[:, None]),
+             (deg[None, :] < i[:, None]), (deg[None, :] < i[:, None])]  # W1, W2, W3, W4 mu rows, W4 alpha rows
+    blocks = 0
+    for m in masks:
+        R, C = m.shape
+        for t in range((R + 31) // 32):
+            rows = m[32 * t:32 * t + 32]
+            nz = [kb for kb in range((C + 31) // 32) if bool(rows[:, 32 * kb:32 * kb + 32].any())]
+            blocks += (max(nz) + 1) if nz else 0
+    return blocks * 16 * 4096 / 32
+
+
+def cpu_info():
+    """Host CPU facts for the baseline: model, physical cores, logical CPUs, this process's
+    allotment (affinity / OMP_NUM_THREADS), and the thread count used = physical cores capped by
+    the allotment (the GPU box grants 16 CPUs per GPU via OMP_NUM_THREADS; more threads would
+    oversubscribe a host shared with other jobs)."""
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cores = set()
+    for cpu in glob.glob("/sys/devices/system/cpu/cpu[0-9]*/topology"):
+        try:
+            with open(os.path.join(cpu, "core_id")) as a, open(os.path.join(cpu, "physical_package_id")) as b:
+                cores.add((a.read().strip(), b.read().strip()))
+        except OSError:
+            pass
+    physical = len(cores) or (os.cpu_count() or 1)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    allot = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    return {"cpu_model": model, "physical_cores": physical, "logical_cpus": os.cpu_count(),
+            "affinity_cpus": affinity, "omp_num_threads": omp, "threads": max(1, min(physical, allot))}
+
+
+def cpu_baseline(model, spec, x_cpu, budget_s=20.0, forward=False, bn_prefix=None):
     """The oracle (op-for-op CPU restatement of the reference) timed on this host."""
     import oracle
-    threads = min(16, os.cpu_count() or 1)
+    info = cpu_info()
+    threads = info["threads"]
     torch.set_num_threads(threads)
-    n = min(x_gpu.shape[0], max_rows)
-    x = x_gpu[:n].float().cpu()
+    n = x_cpu.shape[0]
+    x = x_cpu.float()
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     times = []
 
     def run():
         if forward:
-            return oracle.flow_model(sd, spec, x, 1)
-        z, ld = oracle.flow_model(sd, spec, x, -1)
+            return oracle.flow_model(sd, spec, x, 1, bn_prefix=bn_prefix)
+        z, ld = oracle.flow_model(sd, spec, x, -1, bn_prefix=bn_prefix)
         return z, oracle.gauss_log_prob(z, ld)
 
     with torch.no_grad():
@@ -202,16 +293,19 @@ def cpu_baseline(model, spec, x_gpu, budget_s=12.0, forward=False, max_rows=2621
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     what = "forward (sampling)" if forward else "log_prob"
-    return {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} rows of the same seeded batch, {what} via oracle/flows_ref.py "
-                      f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}, \
-        (None if forward else oracle.nll_f64(lp)), x
+    out = {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
+           "sample": f"{n} rows of the same seeded batch, {what} via oracle/flows_ref.py "
+                     f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}
+    out.update({k: info[k] for k in ("cpu_model", "physical_cores", "logical_cpus", "affinity_cpus",
+                                     "omp_num_threads")})
+    return out, (None if forward else oracle.nll_f64(lp))
 
 
 def cpu_training_baseline(model, spec, x_gpu, budget_s=12.0, max_rows=32768):
     """One training step of the oracle on this host: autograd through oracle/flows_ref.py."""
     import oracle
-    threads = min(16, os.cpu_count() or 1)
+    info = cpu_info()
+    threads = info["threads"]
     torch.set_num_threads(threads)
     n = min(x_gpu.shape[0], max_rows)
     x = x_gpu[:n].detach().float().cpu()
@@ -233,62 +327,58 @@ def cpu_training_baseline(model, spec, x_gpu, budget_s=12.0, max_rows=32768):
             run()
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
-    return {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} rows, loss + backward via autograd through oracle/flows_ref.py "
-                      f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}
+    out = {"value": n / med, "unit": "samples/s", "cores": threads, "kind": "port",
+           "sample": f"{n} rows, loss + backward via autograd through oracle/flows_ref.py "
+                     f"(torch CPU, {threads} threads), median of {len(times)} runs after 1 warm-up"}
+    out.update({k: info[k] for k in ("cpu_model", "physical_cores", "logical_cpus", "affinity_cpus",
+                                     "omp_num_threads")})
+    return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg2t", "train5k", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
-                             "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
-    ap.add_argument("--batch", type=int, default=None,
-                    help="samples per GPU (default 1M; 500k cfg4; 512Ki cfg5f; 8Ki cfg5i)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the captured HIP graph of the pass (nfs_amd.GraphedFlow) instead of eager launches")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: split ONE global batch (default 1M) over the ranks")
-    a = ap.parse_args()
+# CPU-baseline sample per config (rows of the same batch): the full batch where one oracle pass
+# takes a few seconds; cfg4 times 1M of the 4M rows (the full batch would be ~4x the 20 s budget);
+# the IAF d=784 passes are bounded by the oracle's sequential inverse (0.7k samples/s).
+CPU_ROWS = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 1_000_000, "cfg5f": 16_384, "cfg5i": 1_024}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
-    model, d, f_layer, spec, desc = build(a.config)
-    training = a.config in ("cfg4t", "cfg2t", "train5k", "cfg3t")
-    coupling_train = a.config in ("cfg2t", "train5k")
+def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
+    """One benchmark line (dict on rank 0, None elsewhere)."""
+    model, d, f_layer, spec, desc = build(config)
+    training = config in ("cfg4t", "cfg2t", "train5k", "cfg3t")
+    coupling_train = config in ("cfg2t", "train5k")
+    sampling = config == "cfg5f" or config.startswith("sample4k")
+    pinned = config in REFERENCE_RUN
+    if pinned:
+        load_reference_weights(model, config)
     if coupling_train and world > 1:
         from nfs_amd.distributed import enable_sync_batchnorm
         enable_sync_batchnorm(True)  # batch statistics over all ranks = the full-batch step
     model = model.to(dev).train(training)
     from nfs_amd.distributed import average_gradients, broadcast_parameters, shard_range
     broadcast_parameters(model)  # replicate rank 0's weights (one-time, < 1 MB)
-    B_unit = a.batch or DEFAULT_BATCH[a.config]
-    sampling = a.config == "cfg5f" or a.config.startswith("sample4k")
-    if a.strong:
+    B_unit = (a.batch if config == a.config else None) or DEFAULT_BATCH[config]
+    if strong:
         lo, hi = shard_range(B_unit, rank, world)
         B, B_global = hi - lo, B_unit
     else:
+        lo, hi = 0, B_unit
         B, B_global = B_unit, B_unit * world
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    x = torch.randn(B, d, device=dev, generator=g)
+    x_ref = None
+    if pinned and B_unit == g8_meta(config)["B"]:
+        meta = g8_meta(config)
+        x_ref = torch.randn(meta["B"], meta["d"], generator=torch.Generator().manual_seed(meta["seed"]))
+        x = x_ref[lo:hi].to(dev)
+    else:
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        x = torch.randn(B, d, device=dev, generator=g)
     flow = model.flow if hasattr(model, "flow") else model
 
     graphed = None
-    if a.graph and not training:
+    if graph and not training:
         graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-5, capturable=a.graph) if training else None
+    opt = torch.optim.Adam(model.parameters(), lr=1e-5, capturable=graph) if training else None
     graphed_train = None
-    if a.graph and training:
+    if graph and training:
         if world > 1:
             raise SystemExit("--graph training is single-GPU (the SyncBN / gradient collectives run eagerly)")
         graphed_train = nfs_amd.GraphedTrainStep(flow, x, opt, warmup=a.warmup)
@@ -306,7 +396,7 @@ def main():
             logp = flow.log_prob(x)
             loss = -logp.mean()
             loss.backward()
-            average_gradients(model)
+            average_gradients(model, local_count=B)
             opt.step()
             return torch.stack([-loss.detach().double() * B, torch.tensor(float(B), device=dev, dtype=torch.float64)])
         if graphed is not None:
@@ -324,7 +414,7 @@ def main():
 
     from nfs_amd.flows import autoregressive as _ar
     from nfs_amd.flows import spline as _sp
-    bwd_mod = _sp if a.config == "cfg3t" else _ar
+    bwd_mod = _sp if config == "cfg3t" else _ar
     with torch.set_grad_enabled(training):
         for _ in range(a.warmup):
             step()
@@ -334,11 +424,13 @@ def main():
         nfs_amd.reset_stats()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            sums = step()
+            out = step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t = time.perf_counter() - t0
+        torch_calls = nfs_amd.STATS["torch"]
+        hip_calls = nfs_amd.STATS["hip"]
         # Kernel durations: the same K steps again with HIP events around every layer launch
         # on the launch stream. Kept out of the headline loop because each event record adds
         # ~5 us of GPU idle between kernels (measured, profiles/).
@@ -368,7 +460,7 @@ def main():
             torch.cuda.synchronize()
             events = flow.layer_events
             flow.layer_events = None
-    if nfs_amd.STATS["torch"] != 0 or (nfs_amd.STATS["hip"] == 0 and graphed is None and graphed_train is None):
+    if torch_calls != 0 or (hip_calls == 0 and graphed is None and graphed_train is None):
         raise RuntimeError(f"hot path did not run on the HIP kernels: {nfs_amd.STATS}")
     t_all = torch.tensor([t], device=dev, dtype=torch.float64)
     if world > 1:
@@ -380,78 +472,159 @@ def main():
     kname = events[0][0] if events else "?"
     mean_ms = sum(durs) / max(1, len(durs))
     achieved = f_layer * B / (mean_ms * 1e-3) / 1e12
-    nll = None if sampling else -float(sums[0] / sums[1])
 
-    result = None
+    # result vs the reference's own full-scale run (global over ranks)
+    ref_check = None
+    nll = None
+    if sampling and x_ref is not None:
+        with torch.no_grad():
+            xo, ldo = flow.forward(x)
+            cs = torch.stack([xo.double().sum(), xo.double().abs().sum(), ldo.double().sum()])
+        if world > 1:
+            dist.all_reduce(cs)
+        meta = g8_meta(config)
+        scale = 1 if strong else world
+        cs = [float(v) / scale for v in cs.cpu()]
+        ref_check = {"out_abs_sum_rel_diff": abs(cs[1] - meta["out_abs_sum_f64"]) / meta["out_abs_sum_f64"],
+                     "out_sum_diff_rel_to_abs_sum": abs(cs[0] - meta["out_sum_f64"]) / meta["out_abs_sum_f64"],
+                     "ld_mean_abs_diff": abs(cs[2] - meta["ld_sum_f64"]) / meta["B"],
+                     "source": "tests/golden/g8_full_nll.json " + REFERENCE_RUN[config]["g8"]}
+    elif not sampling and not training:
+        sums = out  # the last timed step's [sum log p, count], all-reduced over the ranks
+        nll = -float(sums[0] / sums[1])
+        if x_ref is not None:
+            meta = g8_meta(config)
+            tol = 1e-5 if config in ("cfg2", "cfg3") else 1e-6 * abs(meta["nll_f64"])
+            ref_check = {"nll_gpu": nll, "nll_reference": meta["nll_f64"], "abs_diff": abs(nll - meta["nll_f64"]),
+                         "tolerance": tol, "match": abs(nll - meta["nll_f64"]) <= tol,
+                         "source": "tests/golden/g8_full_nll.json " + REFERENCE_RUN[config]["g8"]}
+
+    if rank != 0:
+        return None
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
+    if os.path.exists(tp):
+        with open(tp) as fh:
+            tj = json.load(fh)
+        spl = tj.get("samples_per_launch")
+        if spl:
+            traffic = tj["hbm_bytes_per_launch"] / spl * B
+    result = {
+        "metric": METRIC,
+        "value": B_global * a.steps / t_max,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * t_max / a.steps,
+        "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": ("synthetic: the reference's seeded G8 batch (torch.randn, CPU generator) with the reference's own "
+                 "weights from tests/golden (written by importing the reference)") if x_ref is not None else
+                ("synthetic: x ~ N(0,1) generated on device (seed 1234+rank); seeded random-init weights "
+                 "perturbed N(0, sigma^2) with non-trivial BatchNorm running stats"),
+        "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B_global,
+                   "parallelism": (f"dp{world} (sample shards, 1 bucketed RCCL all-reduce of the flat gradient per step)"
+                                   if training else f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"),
+                   "launch": "hip-graph replay" if graph else "eager"},
+        "nll_f64": nll,
+        "reference_check": ref_check,
+        "roofline": {"bound": "mfma", "pipe": "valu" if config == "cfg5i" else "mfma",
+                     "kernel": kname, "achieved": achieved,
+                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
+                     "traffic": traffic, "flop_per_sample_per_launch": f_layer,
+                     "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs),
+                     "traffic_source": os.path.relpath(tp, ROOT) if traffic is not None else None},
+        "cpu_baseline": None,
+    }
+    if config == "cfg4":
+        fe = made_executed_flop_per_sample(63, 64)
+        ach_e = fe * B / (mean_ms * 1e-3) / 1e12
+        result["roofline"]["note"] = (
+            "frac counts the dense algorithmic flops of SURVEY §8(d) (the masked GEMMs as dense); the tile "
+            "kernel skips 32x32 blocks that are structurally zero under the MADE mask, so the MFMA pipe "
+            "executes fewer flops: achieved_executed / frac_executed")
+        result["roofline"].update({"flop_per_sample_executed": fe, "achieved_executed": ach_e,
+                                   "frac_executed": ach_e / PEAK_FP32_TFLOPS})
+    if config in PUBLISHED_SAMPLING:
+        mname, pub = PUBLISHED_SAMPLING[config]
+        result["metric"] = f"sampling samples/sec ({mname}, n=4000 per forward call)"
+        result["vs_baseline"] = result["value"] / pub
+        result["published_baseline"] = {"value": pub, "unit": "samples/s", "hardware": "CPU (unspecified)",
+                                        "source": "assets/benchmark.png via plots/_common.py:264-274"}
+        result["nll_f64"] = None
+    if coupling_train:
+        result["metric"] = "training samples/sec/GPU (RealNVP d=2 train-mode step)"
+        result["nll_f64"] = None
+        result["roofline"]["note"] = ("dominant kernel = BWD2 of the train-mode coupling backward "
+                                      "(layer-2 recompute, W2^T e2 and the sample-contraction dW2 on "
+                                      "MFMA); a layer runs STATS1, STATS2, the fused forward, BWD1-3")
+        if world > 1:
+            result["config"]["parallelism"] = (f"dp{world} (sample shards, SyncBN: 4 all-gathers/all-reduces "
+                                               f"of <= 3 KB per layer + 1 bucketed gradient all-reduce)")
+    elif config == "cfg3t":
+        result["metric"] = "training samples/sec/GPU (8x RQ-spline coupling d=2 density step)"
+        result["nll_f64"] = None
+        result["roofline"]["note"] = ("dominant kernel = the fused spline backward (MLP recompute, "
+                                      "spline adjoint, data-gradient chain and the sample-contraction "
+                                      "weight gradients on MFMA, 3x the layer's forward MLP flops)")
+    elif training:
+        result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
+        result["nll_f64"] = None
+        result["roofline"]["note"] = ("dominant kernel = the fused backward (forward recompute + "
+                                      "data-gradient chain, 2x the layer's forward flops); the "
+                                      "weight gradients run as batched library GEMMs")
+    if world == 1 and with_cpu and training:
+        result["cpu_baseline"] = cpu_training_baseline(model, spec, x)
+    elif world == 1 and with_cpu:
+        rows = CPU_ROWS.get(config, 4000 if config.startswith("sample4k") else 262144)
+        xs = (x_ref if x_ref is not None else x.cpu())[:rows]
+        cb, cpu_nll = cpu_baseline(model, spec, xs, forward=sampling)
+        if not sampling:
+            gpu_nll = flow.nll(xs.to(dev))
+            cb["nll_abs_diff_vs_gpu"] = abs(cpu_nll - gpu_nll)
+        result["cpu_baseline"] = cb
+    return result
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2",
+                    choices=["cfg2", "cfg2t", "train5k", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
+                             "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
+    ap.add_argument("--batch", type=int, default=None,
+                    help="global batch (default: the BASELINE batch, 1M; 4M cfg4; 512Ki cfg5f; 8Ki cfg5i)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="training configs: replay the captured HIP graph of the step (nfs_amd.GraphedTrainStep)")
+    ap.add_argument("--eager", action="store_true",
+                    help="eval configs: eager per-layer launches instead of the captured HIP graph (GraphedFlow)")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: every rank processes the whole batch")
+    ap.add_argument("--strong", action="store_true", help="(default) strong scaling: split the batch over the ranks")
+    ap.add_argument("--no-secondary", action="store_true", help="cfg2: skip the nested MAF d=63 (cfg4) line")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    training = a.config in ("cfg4t", "cfg2t", "train5k", "cfg3t")
+    graph = a.graph if training else not a.eager
+    strong = not a.weak
+    result = run_config(a.config, a, world, rank, dev, strong, graph, not a.no_cpu)
+    if a.config == "cfg2" and not a.no_secondary:
+        sec = run_config("cfg4", a, world, rank, dev, strong, graph, not a.no_cpu)
+        if rank == 0:
+            result["maf_d63"] = sec
     if rank == 0:
-        traffic = None
-        tp = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
-        if os.path.exists(tp):
-            with open(tp) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
-        result = {
-            "metric": METRIC,
-            "value": B_global * a.steps / t_max,
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": 1e3 * t_max / a.steps,
-            "higher_is_better": True,
-            "scaling": "strong" if a.strong else "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic: x ~ N(0,1) generated on device (seed 1234+rank); seeded random-init "
-                    "weights perturbed N(0, 0.1^2) with non-trivial BatchNorm running stats",
-            "config": {"workload": desc, "batch_per_gpu": B, "global_batch": B_global,
-                       "parallelism": (f"dp{world} (sample shards, 1 bucketed RCCL all-reduce of the flat gradient per step)"
-                            if training else f"dp{world} (sample shards, 1 RCCL all-reduce of 16 B per step)"),
-                       "launch": "hip-graph replay" if a.graph else "eager"},
-            "nll_f64": nll,
-            "roofline": {"bound": "mfma", "pipe": "valu" if a.config == "cfg5i" else "mfma",
-                         "kernel": kname, "achieved": achieved,
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
-                         "traffic": traffic, "flop_per_sample_per_launch": f_layer,
-                         "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs)},
-            "cpu_baseline": None,
-        }
-        if a.config in PUBLISHED_SAMPLING:
-            mname, pub = PUBLISHED_SAMPLING[a.config]
-            result["metric"] = f"sampling samples/sec ({mname}, n=4000 per forward call)"
-            result["vs_baseline"] = result["value"] / pub
-            result["published_baseline"] = {"value": pub, "unit": "samples/s", "hardware": "CPU (unspecified)",
-                                            "source": "assets/benchmark.png via plots/_common.py:264-274"}
-            result["nll_f64"] = None
-        if coupling_train:
-            result["metric"] = "training samples/sec/GPU (RealNVP d=2 train-mode step)"
-            result["nll_f64"] = None
-            result["roofline"]["note"] = ("dominant kernel = BWD2 of the train-mode coupling backward "
-                                          "(layer-2 recompute, W2^T e2 and the sample-contraction dW2 on "
-                                          "MFMA); a layer runs STATS1, STATS2, the fused forward, BWD1-3")
-            if world > 1:
-                result["config"]["parallelism"] = (f"dp{world} (sample shards, SyncBN: 4 all-gathers/all-reduces "
-                                                   f"of <= 3 KB per layer + 1 bucketed gradient all-reduce)")
-        elif a.config == "cfg3t":
-            result["metric"] = "training samples/sec/GPU (8x RQ-spline coupling d=2 density step)"
-            result["nll_f64"] = None
-            result["roofline"]["note"] = ("dominant kernel = the fused spline backward (MLP recompute, "
-                                          "spline adjoint, data-gradient chain and the sample-contraction "
-                                          "weight gradients on MFMA, 3x the layer's forward MLP flops)")
-        elif training:
-            result["metric"] = "training samples/sec/GPU (MAF d=63 density step)"
-            result["nll_f64"] = None
-            result["roofline"]["note"] = ("dominant kernel = the fused backward (forward recompute + "
-                                          "data-gradient chain, 2x the layer's forward flops); the "
-                                          "weight gradients run as batched library GEMMs")
-        if world == 1 and not a.no_cpu and training:
-            result["cpu_baseline"] = cpu_training_baseline(model, spec, x)
-        elif world == 1 and not a.no_cpu:
-            rows = {"cfg5f": 16384, "cfg5i": 256}.get(a.config, 4000 if a.config.startswith("sample4k") else 262144)
-            cb, cpu_nll, xs = cpu_baseline(model, spec, x, forward=sampling, max_rows=rows)
-            if not sampling:
-                gpu_nll = flow.nll(xs.to(dev))
-                cb["nll_abs_diff_vs_gpu"] = abs(cpu_nll - gpu_nll)
-            result["cpu_baseline"] = cb
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

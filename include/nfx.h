@@ -271,6 +271,35 @@ size_t nfx_gauss_workspace_bytes(int64_t B);
 int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
                       void* workspace, int64_t B, int d, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Between-layer BatchNorm of NormalizingFlowModel(batch_norm_between_layers=True)
+ * (src/models/normalizing_flow_model.py:67-128), an invertible per-feature affine with the
+ * RUNNING statistics and a batch-constant log-det c = sum_j log|g_j| - 0.5 log(rv_j + eps):
+ *   nfx_flowbn_apply   forward  out = (in - rm)/sqrt(rv + eps)*g + b, log_det[i] += c
+ *                      (replaces _apply_batch_norm + _batch_norm_log_det_jacobian, :35-44);
+ *                      inverse  out = (in - b)/g*sqrt(rv + eps) + rm, log_det[i] -= c (:55-60).
+ *                      d <= 1024.
+ * Train mode (forward direction, :74-79), before the apply:
+ *   nfx_flowbn_moments        stats[d][3] = float64 (n, mean, M2) of the batch per feature
+ *                             (SyncBN: merge the triples over ranks before the update)
+ *   nfx_flowbn_update_running running = running*(1 - momentum) + momentum*batch (biased var)
+ * Autograd of one apply w.r.t. the input and (weight, bias) — the running statistics are
+ * buffers — from grad_out [B,d] and grad_log_det [B] (either may be NULL = zero):
+ *   nfx_flowbn_backward       grad_in [B,d], grad_gamma [d], grad_beta [d]
+ * `workspace` holds nfx_flowbn_workspace_bytes(B, d) bytes.
+ * ------------------------------------------------------------------------------------- */
+size_t nfx_flowbn_workspace_bytes(int64_t B, int d);
+int nfx_flowbn_apply(const float* in, float* out, float* log_det, const float* gamma, const float* beta,
+                     const float* running_mean, const float* running_var, float eps, int64_t B, int d,
+                     int direction, void* stream);
+int nfx_flowbn_moments(const float* x, int64_t B, int d, double* stats, void* workspace, void* stream);
+int nfx_flowbn_update_running(const double* stats, float* running_mean, float* running_var,
+                              double momentum, int d, void* stream);
+int nfx_flowbn_backward(const float* in, const float* grad_out, const float* grad_log_det, float* grad_in,
+                        const float* gamma, const float* beta, const float* running_mean,
+                        const float* running_var, float eps, float* grad_gamma, float* grad_beta,
+                        int64_t B, int d, int direction, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -93,18 +93,23 @@ __device__ __forceinline__ double block_sum_f64(double v) {
     return t;
 }
 
-// exp(x) for x <= 87 (the callers clamp or bound the argument: softmax numerators <= 0,
-// softplus below its threshold 20, the affine/MADE scale exponents within +-10): x*log2(e) is
-// carried as a compensated pair (t, e), the hardware exp2 takes the rounded t and the
-// product's rounding error is folded back as exp2(t) * (1 + e*ln2). A few ulp like expf, in 6
-// instructions instead of OCML's 13 (range reduction and overflow paths are not needed here;
-// results below 2^-126 may flush). NaN propagates.
+// exp(x) for finite x <= 87 (the affine/MADE callers clamp the scale exponent to +-10 first):
+// x*log2(e) is carried as a compensated pair (t, e), the hardware exp2 takes the rounded t and
+// the product's rounding error is folded back as exp2(t) * (1 + e*ln2). A few ulp like expf, in
+// 6 instructions instead of OCML's 13 (range reduction and overflow paths are not needed here;
+// results below 2^-126 flush to 0 where expf returns a subnormal). NaN propagates. An infinite
+// argument gives NaN (inf - inf in the correction): use exp_safe where x may be -inf.
 __device__ __forceinline__ float exp_fast(float x) {
     const float t = x * 1.44269502f;
     const float e = __builtin_fmaf(x, 1.44269502f, -t) + x * 1.9259629e-8f;
     const float r = __builtin_amdgcn_exp2f(t);
     return __builtin_fmaf(r, e * 0.693147182f, r);
 }
+// exp_fast for arguments that may be -inf or hugely negative (spline softmax numerators
+// p_k - max p, softplus inputs): one NaN-propagating max first, so exp(-inf) = 0 like expf.
+// Below -103.3 expf is already 0; between -103.3 and -87.3 it is subnormal and this flushes
+// (the spline consumers add min_bin_width / min_derivative = 1e-3 to it, so no output changes).
+__device__ __forceinline__ float exp_safe(float x) { return exp_fast(tmax(x, -128.f)); }
 
 // fp32(d * log(2*pi)) exactly as torch's MultivariateNormal.log_prob rounds it.
 inline float gauss_const(int d) { return (float)((double)d * 1.8378770664093453); }

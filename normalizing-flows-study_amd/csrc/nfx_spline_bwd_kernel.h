@@ -81,7 +81,7 @@ __device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32],
         for (int k = 1; k < K; ++k) m = tmax(m, p[k]);
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < K; ++k) { sw[k] = exp_fast(p[k] - m); s = s + sw[k]; }
+        for (int k = 0; k < K; ++k) { sw[k] = exp_safe(p[k] - m); s = s + sw[k]; }
         const float inv = 1.f / s;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -96,7 +96,7 @@ __device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32],
         for (int k = 1; k < K; ++k) m = tmax(m, p[K + k]);
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < K; ++k) { sh[k] = exp_fast(p[K + k] - m); s = s + sh[k]; }
+        for (int k = 0; k < K; ++k) { sh[k] = exp_safe(p[K + k] - m); s = s + sh[k]; }
         const float inv = 1.f / s;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -373,7 +373,7 @@ __device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32],
 #pragma unroll
     for (int k = 0; k < K - 1; ++k) {
         const float u = p[2 * K + k];
-        const float z = exp_fast(u);
+        const float z = exp_safe(u);
         const float sp = u > 20.f ? 1.f : z / (z + 1.f);
         gp[2 * K + k] = dpre[k] >= eps ? gdk[k + 1] * sp : 0.f;
     }

@@ -69,7 +69,7 @@ struct SplineConsts {
 // the double-float log1pf (which dominated the spline's vector time).
 __device__ __forceinline__ float tsoftplus(float x) {
 #pragma clang fp contract(off)
-    const float u = exp_fast(x);
+    const float u = exp_safe(x);
     const float w = 1.f + u;
     const float wm1 = w - 1.f;
     const float l = wm1 == 0.f ? u : logf(w) * (u * __builtin_amdgcn_rcpf(wm1));
@@ -96,7 +96,7 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
             for (int k = 1; k < K; ++k) m = tmax(m, p[k]);
             float s = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) { w[k] = exp_fast(p[k] - m); s = s + w[k]; }
+            for (int k = 0; k < K; ++k) { w[k] = exp_safe(p[k] - m); s = s + w[k]; }
             const float inv = 1.f / s;
 #pragma unroll
             for (int k = 0; k < K; ++k) w[k] = tclamp_min(C.min_w + C.cw * (w[k] * inv), eps);
@@ -107,7 +107,7 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
             for (int k = 1; k < K; ++k) m = tmax(m, p[K + k]);
             float s = 0.f;
 #pragma unroll
-            for (int k = 0; k < K; ++k) { h[k] = exp_fast(p[K + k] - m); s = s + h[k]; }
+            for (int k = 0; k < K; ++k) { h[k] = exp_safe(p[K + k] - m); s = s + h[k]; }
             const float inv = 1.f / s;
 #pragma unroll
             for (int k = 0; k < K; ++k) h[k] = tclamp_min(C.min_h + C.ch * (h[k] * inv), eps);

@@ -24,7 +24,12 @@ def broadcast_parameters(module, src=0, group=None):
         return
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
-            dist.broadcast(t.data, src=src, group=group)
+            dist.broadcast(t, src=src, group=group)
+            # the collective writes behind autograd's back: bump the version so any packed
+            # weight image keyed on (data_ptr, _version) is rebuilt from the broadcast values
+            torch.autograd.graph.increment_version(t)
+    from .flows.flow import drop_pack_caches
+    drop_pack_caches(module)
 
 
 def sharded_nll(model, x_local, group=None, return_log_prob=False):
@@ -41,11 +46,16 @@ def sharded_nll(model, x_local, group=None, return_log_prob=False):
     return (nll, logp) if return_log_prob else nll
 
 
-def average_gradients(module, group=None):
+def average_gradients(module, group=None, local_count=None):
     """Data-parallel training exchange: average every parameter gradient over the ranks with
     ONE bucketed all-reduce of the flattened gradients (412 KB for 5 x MAF(63, 64); a single
-    message is latency-optimal on xGMI at that size). With equal shards and a mean loss per
-    rank this equals the full-batch gradient. Parameters without a gradient are skipped."""
+    message is latency-optimal on xGMI at that size). Parameters without a gradient are skipped.
+
+    Each rank's loss is a mean over its own shard. With `local_count` (this rank's sample
+    count, e.g. from shard_range, which hands out shards differing by one when n % world != 0)
+    every rank's gradient is weighted by its count and the counts ride in the same all-reduce,
+    so the result is exactly the full-batch mean-loss gradient: sum_r n_r g_r / sum_r n_r.
+    Without it the ranks are assumed to hold equal shards (plain mean over ranks)."""
     if not (dist.is_available() and dist.is_initialized()):
         return
     world = dist.get_world_size(group)
@@ -54,15 +64,21 @@ def average_gradients(module, group=None):
     params = [p for p in module.parameters() if p.grad is not None]
     if not params:
         return
-    flat = torch.cat([p.grad.reshape(-1) for p in params])
-    dist.all_reduce(flat, group=group)
-    flat /= world
+    grads = [p.grad.reshape(-1) for p in params]
+    if local_count is None:
+        flat = torch.cat(grads)
+        dist.all_reduce(flat, group=group)
+        flat /= world
+    else:
+        n = torch.full((1,), float(local_count), device=grads[0].device, dtype=grads[0].dtype)
+        flat = torch.cat([torch.cat(grads) * n, n])
+        dist.all_reduce(flat, group=group)
+        flat = flat[:-1] / flat[-1]
     o = 0
     for p in params:
         n = p.numel()
         p.grad.copy_(flat[o:o + n].view_as(p))
         o += n
-
 
 
 # ---------------------------------------------------------------------------------------------

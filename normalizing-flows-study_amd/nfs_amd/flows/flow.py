@@ -9,8 +9,8 @@ Routing (HipFlow._route):
     If autograd needs gradients, the kernel still computes the outputs and the backward pass
     recomputes through the layer's torch composite (HipFlowFunction).
   * CPU tensors or fp64 (gradcheck)  -> the layer's torch composite (same math as the reference).
-  * train-mode BatchNorm in a conditioner (CouplingLayer) -> torch composite: the batch
-    statistics are batch-global (out of the eval hot path).
+  * train-mode BatchNorm in a conditioner (CouplingLayer) -> the train-mode kernels
+    (batch statistics, running-stat update, fused backward; coupling._CouplingTrainFunction).
 A shape outside the compiled kernel family raises NotImplementedError on the GPU instead of
 silently running eager (set nfs_amd.flows.flow.ALLOW_TORCH_FALLBACK = True to permit it).
 """
@@ -209,8 +209,24 @@ class HipFlow(Flow):
         return False
 
 
+def drop_pack_caches(module):
+    """Forget every cached packed-weight image under `module`, so the next call re-packs from
+    the live parameters. Needed after writes the version counters cannot see (a collective or
+    `p.data.copy_()` writing through `.data`, a graph replay whose optimizer step updated the
+    parameters) and before a graph capture that must record the pack kernels."""
+    for m in module.modules():
+        if isinstance(m, HipFlow):
+            for k in [k for k in m.__dict__ if k.startswith("_nfx_") and k.endswith("pack_cache")]:
+                del m.__dict__[k]
+
+
 class SequentialFlow(Flow):
-    """A sequence of flows applied in order (src/flows/flow/sequential_flow.py:5-34)."""
+    """A sequence of flows applied in order (src/flows/flow/sequential_flow.py:5-34).
+
+    The reference accumulates into torch.zeros(B) (f32) with one `+=` per layer. When every
+    layer routes to its gfx950 kernel (and no gradient is needed) the chain runs the kernels
+    back to back with the log-det accumulated IN PLACE into that zero vector (accumulate=1):
+    0 + ld_0 + ld_1 + ... in the same float32 order, no intermediate tensors."""
 
     def __init__(self, flows):
         super().__init__()
@@ -219,6 +235,8 @@ class SequentialFlow(Flow):
         self.flows = nn.ModuleList(flows)
 
     def forward(self, z):
+        if self._hip_chain_ok(z):
+            return self._hip_chain(z, 1)
         total_log_det = torch.zeros(z.size(0), device=z.device)
         for flow in self.flows:
             z, log_det = flow.forward(z)
@@ -226,11 +244,30 @@ class SequentialFlow(Flow):
         return z, total_log_det
 
     def inverse(self, x):
+        if self._hip_chain_ok(x):
+            return self._hip_chain(x, -1)
         total_log_det = torch.zeros(x.size(0), device=x.device)
         for flow in reversed(self.flows):
             x, log_det = flow.inverse(x)
             total_log_det += log_det
         return x, total_log_det
+
+    def _hip_chain_ok(self, x):
+        if x.device.type != "cuda" or x.dtype != torch.float32 or x.dim() != 2 or len(self.flows) == 0:
+            return False
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return False  # per-layer autograd Functions handle gradients
+        return all(isinstance(f, HipFlow) and f._route(x) == "hip" for f in self.flows)
+
+    def _hip_chain(self, x, direction):
+        x = x.contiguous()
+        ld = torch.zeros(x.shape[0], device=x.device, dtype=torch.float32)
+        bufs = [torch.empty_like(x), torch.empty_like(x)]
+        cur, k = x, 0
+        for f in (self.flows if direction > 0 else reversed(self.flows)):
+            f._hip_launch_counted(cur, bufs[k], ld, direction, accumulate=True)
+            cur, k = bufs[k], k ^ 1
+        return cur, ld
 
 
 def stream_ptr(t):

@@ -118,11 +118,26 @@ class GraphedTrainStep:
         torch.cuda.current_stream(dev).wait_stream(stream)
         torch0 = _flows.STATS["torch"]
         optimizer.zero_grad(set_to_none=True)
+        # The pack kernels must be IN the graph: every replay's optimizer step changes the
+        # parameters, and the next replay has to re-pack them. A cache left from an earlier
+        # eager call (e.g. warmup=0 after an eval pass) would otherwise be baked in as a
+        # constant image and every replay would silently run the forward on stale weights.
+        _flows.drop_pack_caches(model)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_loss = self._step(zero=False)
         if _flows.STATS["torch"] != torch0:
             raise RuntimeError("GraphedTrainStep: the captured step ran eager PyTorch layers, not the HIP kernels")
+        # Replays update the parameters without bumping their versions, so the image packed
+        # during capture would look current to a later eager call: forget it now and after
+        # every replay (the graph keeps its own buffers).
+        self._hipflows = [m for m in model.modules() if isinstance(m, _flows.HipFlow)]
+        self._forget()
+
+    def _forget(self):
+        for m in self._hipflows:
+            for k in [k for k in m.__dict__ if k.startswith("_nfx_") and k.endswith("pack_cache")]:
+                del m.__dict__[k]
 
     def _step(self, zero=True):
         if zero:
@@ -140,4 +155,5 @@ class GraphedTrainStep:
                 raise ValueError(f"GraphedTrainStep captured shape {tuple(self.static_in.shape)}, got {tuple(x.shape)}")
             self.static_in.copy_(x)
         self.graph.replay()
+        self._forget()
         return self.static_loss

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from ..distributed import merge_bn_stats, sync_bn_world
 from ..flows.flow import HipFlow, STATS
 
 
@@ -44,6 +45,12 @@ class NormalizingFlowModel(nn.Module):
             log_det_jacobian_sum += log_det_jacobian
             if self.batch_norm_between_layers and i < len(self.flows) - 1:
                 bn = self.batch_norms[i]
+                if _bn_hip_ok(z):
+                    if self.training:
+                        _bn_update_running_hip(bn, z)
+                    z, log_det_jacobian_sum = _FlowBatchNormFn.apply(
+                        z, _as_ld(log_det_jacobian_sum, z), bn.weight, bn.bias, bn, 1)
+                    continue
                 z = self._apply_batch_norm(bn, z)
                 log_det_jacobian_sum += self._batch_norm_log_det_jacobian(bn, z)
         return z, log_det_jacobian_sum
@@ -55,19 +62,28 @@ class NormalizingFlowModel(nn.Module):
         for i, flow in reversed(list(enumerate(self.flows))):
             if self.batch_norm_between_layers and i < len(self.flows) - 1:
                 bn = self.batch_norms[i]
-                x = self._inverse_batch_norm(bn, x)
-                log_det_jacobian_sum -= self._batch_norm_log_det_jacobian(bn, x)
+                if _bn_hip_ok(x):
+                    x, log_det_jacobian_sum = _FlowBatchNormFn.apply(
+                        x, _as_ld(log_det_jacobian_sum, x), bn.weight, bn.bias, bn, -1)
+                else:
+                    x = self._inverse_batch_norm(bn, x)
+                    log_det_jacobian_sum -= self._batch_norm_log_det_jacobian(bn, x)
             x, log_det_jacobian = flow.inverse(x)
             log_det_jacobian_sum += log_det_jacobian
         return x, log_det_jacobian_sum
 
     # -- between-layer BatchNorm (normalizing_flow_model.py:67-128) ----------------------------
+    # Composite torch versions (CPU, float64); fp32 ROCm tensors run csrc/nfx_flowbn.hip.
     def _apply_batch_norm(self, bn_layer, x):
         if self.training:
             with torch.no_grad():
                 momentum = bn_layer.momentum if bn_layer.momentum is not None else 0.1
-                bn_layer.running_mean.mul_(1 - momentum).add_(momentum * x.mean(dim=0))
-                bn_layer.running_var.mul_(1 - momentum).add_(momentum * x.var(dim=0, unbiased=False))
+                if sync_bn_world() > 1:  # SyncBN: the moments of every rank's shard
+                    mean, var = _synced_moments(x)
+                else:
+                    mean, var = x.mean(dim=0), x.var(dim=0, unbiased=False)
+                bn_layer.running_mean.mul_(1 - momentum).add_(momentum * mean)
+                bn_layer.running_var.mul_(1 - momentum).add_(momentum * var)
         gamma = bn_layer.weight.view(1, -1)
         beta = bn_layer.bias.view(1, -1)
         mean = bn_layer.running_mean.view(1, -1)
@@ -99,6 +115,8 @@ class NormalizingFlowModel(nn.Module):
         for f in self.flows:
             if not isinstance(f, HipFlow) or f._route(x) != "hip":
                 return False
+        if self.batch_norm_between_layers and len(self.flows) > 1 and not _bn_hip_ok(x):
+            return False
         return True
 
     def _hip_chain(self, x, direction, logprob=None):
@@ -115,12 +133,10 @@ class NormalizingFlowModel(nn.Module):
         cur, k, first, fused = x, 0, True, False
         for i in order:
             if direction < 0 and self.batch_norm_between_layers and i < n - 1:
-                bn = self.batch_norms[i]
-                cur = self._inverse_batch_norm(bn, cur).contiguous()
-                if first:
-                    ld.zero_()
-                    first = False
-                ld.sub_(self._batch_norm_log_det_jacobian(bn, cur))
+                # (never the first op: the last flow has no BatchNorm, so ld is initialised)
+                out = bufs[k] if bufs[k] is not cur else bufs[k ^ 1]
+                _bn_launch(self.batch_norms[i], cur, out, ld, -1)
+                cur = out
             out = bufs[k]
             if out is cur:
                 k ^= 1
@@ -142,8 +158,11 @@ class NormalizingFlowModel(nn.Module):
             cur, k = out, k ^ 1
             if direction > 0 and self.batch_norm_between_layers and i < n - 1:
                 bn = self.batch_norms[i]
-                cur = self._apply_batch_norm(bn, cur).contiguous()
-                ld.add_(self._batch_norm_log_det_jacobian(bn, cur))
+                if self.training:
+                    _bn_update_running_hip(bn, cur)
+                out = bufs[k] if bufs[k] is not cur else bufs[k ^ 1]
+                _bn_launch(bn, cur, out, ld, 1)
+                cur = out
         if logprob is not None:
             return cur, ld, fused
         return cur, ld
@@ -202,3 +221,104 @@ def gauss_logprob(z, ld, logp=None, sums=None, ws=None):
                                    _lib.ptr(ws), B, d, _lib.stream_of(z)), "nfx_gauss_logprob")
     STATS["hip"] += 1
     return logp, sums
+
+
+# ---------------------------------------------------------------------------------------------
+# Between-layer BatchNorm on the GPU (csrc/nfx_flowbn.hip)
+# ---------------------------------------------------------------------------------------------
+_FLOWBN_MAX_D = 1024
+
+
+def _bn_hip_ok(x):
+    return x.device.type == "cuda" and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] <= _FLOWBN_MAX_D
+
+
+def _bn_ptrs(bn):
+    return (_lib.ptr(bn.weight), _lib.ptr(bn.bias), _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var))
+
+
+def _bn_launch(bn, x, out, ld, direction):
+    """out = BN affine of x (running statistics), ld -+= the scalar log-det, in place."""
+    B, d = x.shape
+    w, b, rm, rv = _bn_ptrs(bn)
+    _lib.check(_lib.lib().nfx_flowbn_apply(_lib.ptr(x), _lib.ptr(out), _lib.ptr(ld), w, b, rm, rv,
+                                           float(bn.eps), B, d, direction, _lib.stream_of(x)),
+               "nfx_flowbn_apply")
+    STATS["hip"] += 1
+
+
+def _bn_workspace(B, d, device):
+    return torch.empty(_lib.lib().nfx_flowbn_workspace_bytes(B, d), device=device, dtype=torch.uint8)
+
+
+def _bn_update_running_hip(bn, x):
+    """Train mode (normalizing_flow_model.py:74-79): fold the batch moments of x into the running
+    statistics; with SyncBN enabled the moments are those of every rank's shard."""
+    x = x.detach().contiguous()
+    B, d = x.shape
+    L = _lib.lib()
+    stats = torch.empty(d, 3, device=x.device, dtype=torch.float64)
+    ws = _bn_workspace(B, d, x.device)
+    st = _lib.stream_of(x)
+    _lib.check(L.nfx_flowbn_moments(_lib.ptr(x), B, d, _lib.ptr(stats), _lib.ptr(ws), st), "nfx_flowbn_moments")
+    merge_bn_stats(stats)
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    with torch.no_grad():
+        _lib.check(L.nfx_flowbn_update_running(_lib.ptr(stats), _lib.ptr(bn.running_mean),
+                                               _lib.ptr(bn.running_var), float(momentum), d, st),
+                   "nfx_flowbn_update_running")
+        # the kernel writes the buffers behind autograd's back; bump their versions so every
+        # version-keyed cache (packed images, graph strict checks) sees the change
+        torch.autograd.graph.increment_version(bn.running_mean)
+        torch.autograd.graph.increment_version(bn.running_var)
+    STATS["hip"] += 2
+
+
+def _synced_moments(x):
+    """(mean, biased var) of x over every rank's shard (float64 Chan merge, cast to x's dtype)."""
+    xd = x.detach().double()
+    n = torch.full((x.shape[1],), float(x.shape[0]), dtype=torch.float64, device=x.device)
+    mean = xd.mean(0)
+    m2 = ((xd - mean) ** 2).sum(0)
+    stats = torch.stack([n, mean, m2], dim=1)
+    merge_bn_stats(stats)
+    return stats[:, 1].to(x.dtype), (stats[:, 2] / stats[:, 0]).to(x.dtype)
+
+
+def _as_ld(ld, x):
+    """The running log-det sum as a [B] fp32 tensor (the reference starts it as the int 0)."""
+    if isinstance(ld, torch.Tensor):
+        return ld
+    return torch.full((x.shape[0],), float(ld), device=x.device, dtype=x.dtype)
+
+
+class _FlowBatchNormFn(torch.autograd.Function):
+    """One between-layer BatchNorm call on the GPU with a HIP backward: (x, ld) -> (y, ld +- c)."""
+
+    @staticmethod
+    def forward(ctx, x, ld, weight, bias, bn, direction):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        ld_out = ld.detach().to(torch.float32).contiguous().clone()
+        _bn_launch(bn, x, y, ld_out, direction)
+        ctx.direction = direction
+        ctx.eps = float(bn.eps)
+        ctx.save_for_backward(x, weight, bias, bn.running_mean.detach().clone(), bn.running_var.detach().clone())
+        return y, ld_out
+
+    @staticmethod
+    def backward(ctx, gy, gld):
+        x, weight, bias, rm, rv = ctx.saved_tensors
+        B, d = x.shape
+        gx = torch.empty_like(x)
+        dg = torch.empty(d, device=x.device, dtype=torch.float32)
+        db = torch.empty(d, device=x.device, dtype=torch.float32)
+        gy = gy.contiguous() if gy is not None else None
+        gld_c = gld.contiguous() if gld is not None else None
+        ws = _bn_workspace(B, d, x.device)
+        _lib.check(_lib.lib().nfx_flowbn_backward(
+            _lib.ptr(x), _lib.ptr(gy), _lib.ptr(gld_c), _lib.ptr(gx), _lib.ptr(weight.detach()),
+            _lib.ptr(bias.detach()), _lib.ptr(rm), _lib.ptr(rv), ctx.eps, _lib.ptr(dg), _lib.ptr(db), B, d,
+            ctx.direction, _lib.ptr(ws), _lib.stream_of(x)), "nfx_flowbn_backward")
+        STATS["hip"] += 1
+        return gx, gld, dg, db, None, None

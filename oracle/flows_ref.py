@@ -11,7 +11,7 @@ import torch.nn.functional as F
 
 __all__ = [
     "made_degrees", "made_masks", "coupling", "spline_coupling", "rqs_unit", "made", "made_bn", "maf", "iaf", "arqs",
-    "flow_model", "gauss_log_prob", "nll_f64", "realnvp_spec", "spline_model_spec", "maf_spec",
+    "flow_model", "sequential_flow", "gauss_log_prob", "nll_f64", "realnvp_spec", "spline_model_spec", "maf_spec",
 ]
 
 
@@ -319,13 +319,63 @@ def arqs(sd, p, x, direction, K=8, data_min=None, data_max=None, batch_norm=Fals
 _LAYER = {"coupling": coupling, "spline": spline_coupling, "maf": maf, "iaf": iaf, "arqs": arqs}
 
 
-def flow_model(sd, spec, x, direction):
+def flow_model(sd, spec, x, direction, bn_prefix=None, training=False):
+    """NormalizingFlowModel.forward/inverse (src/models/normalizing_flow_model.py:25-65).
+
+    bn_prefix (e.g. "flow.batch_norms.") enables the between-layer BatchNorm of layers
+    i < n-1 (:35-44, :55-60, :67-128); training=True updates its running statistics in `sd` in
+    place before the forward affine (:74-79)."""
     log_det_sum = 0                                   # :30 / :53 — python int, then f32 tensor
+    n = len(spec)
+    order = range(n) if direction > 0 else reversed(range(n))
+    for i in order:
+        kind, p, kw = spec[i]
+        if direction < 0 and bn_prefix is not None and i < n - 1:
+            q = f"{bn_prefix}{i}."
+            x = _bn_inverse(sd, q, x)                                       # :58
+            log_det_sum -= _bn_log_det(sd, q)                                # :60
+        x, ld = _LAYER[kind](sd, p, x, direction, **kw)
+        log_det_sum += ld
+        if direction > 0 and bn_prefix is not None and i < n - 1:
+            q = f"{bn_prefix}{i}."
+            x = _bn_apply(sd, q, x, training)                               # :43
+            log_det_sum += _bn_log_det(sd, q)                                # :44
+    return x, log_det_sum
+
+
+def _bn_apply(sd, q, x, training, momentum=0.1, eps=1e-5):
+    """normalizing_flow_model.py:67-85: running-stat update in train mode, then the affine with
+    the (updated) running statistics."""
+    if training:
+        with torch.no_grad():
+            sd[q + "running_mean"].mul_(1 - momentum).add_(momentum * x.mean(dim=0))
+            sd[q + "running_var"].mul_(1 - momentum).add_(momentum * x.var(dim=0, unbiased=False))
+    gamma, beta = sd[q + "weight"].view(1, -1), sd[q + "bias"].view(1, -1)
+    mean, var = sd[q + "running_mean"].view(1, -1), sd[q + "running_var"].view(1, -1)
+    return (x - mean) / torch.sqrt(var + eps) * gamma + beta
+
+
+def _bn_log_det(sd, q, eps=1e-5):
+    """normalizing_flow_model.py:87-108: sum_j log|g_j| - 0.5 log(rv_j + eps) (a scalar)."""
+    return (torch.log(torch.abs(sd[q + "weight"])) - 0.5 * torch.log(sd[q + "running_var"] + eps)).sum()
+
+
+def _bn_inverse(sd, q, y, eps=1e-5):
+    """normalizing_flow_model.py:110-128."""
+    gamma, beta = sd[q + "weight"].view(1, -1), sd[q + "bias"].view(1, -1)
+    mean, var = sd[q + "running_mean"].view(1, -1), sd[q + "running_var"].view(1, -1)
+    return (y - beta) / gamma * torch.sqrt(var + eps) + mean
+
+
+def sequential_flow(sd, spec, x, direction):
+    """SequentialFlow.forward/inverse (src/flows/flow/sequential_flow.py:15-34): the accumulator
+    is torch.zeros(B) (f32), layers in order (forward) or reverse order (inverse)."""
+    total = torch.zeros(x.size(0))
     layers = spec if direction > 0 else list(reversed(spec))
     for kind, p, kw in layers:
         x, ld = _LAYER[kind](sd, p, x, direction, **kw)
-        log_det_sum += ld
-    return x, log_det_sum
+        total += ld
+    return x, total
 
 
 def realnvp_spec(n_layers, prefix="flow.flows.", training=False):

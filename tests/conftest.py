@@ -52,22 +52,28 @@ def cuda_device():
     return torch.device("cuda:0")
 
 
-def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=5e-4, what=""):
-    """Error model for ill-conditioned fp32 math (RQ spline chains).
+def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=5e-4, what="", kind=None, max_ill=0.02):
+    """Parity of ill-conditioned fp32 math (RQ spline chains) in two tiers.
 
-    The reference's own fp32 result (cpu32) is not exact: for some inputs the softmax/exp/log
-    chain and the citardauq root lose up to ~1e-3 in log-det against the float64 evaluation of
-    the same math (ref64 = the oracle run in double). A kernel rounding differently lands on a
-    different but equally-conditioned value, so the check is statistical over the tensor:
-      per element  |gpu - ref64| <= 8 |cpu32 - ref64| + slack (1 + |ref64|)
-      mean         mean|gpu - ref64| <= 1.5 mean|cpu32 - ref64| + 1e-7
-      max          max|gpu - ref64|  <= 4 max|cpu32 - ref64| + slack
-      floor        every element within floor (1 + |ref64|) of the float64 value
-    i.e. the kernel is as accurate as the reference's fp32, never systematically worse. The
-    per-element 8x bound is waived below `floor`: near a knot with steep end derivatives the
-    log-det has a condition number ~100 per ulp of the knot position (measured: a 1-ulp
-    softmax/exp difference moves ld by 1e-4 while the reference happens to land within 1e-6).
-    NaN patterns must agree with the reference."""
+    Tier 1 — SURVEY §8(c)'s fixed tolerances. Every element where the reference's own fp32
+    result (cpu32) is within 1e-5 of the float64 evaluation of the same math (ref64 = the oracle
+    run in double) — 1e-5 (1 + |ref|) for values, 1e-5 absolute for log-dets — is
+    well-conditioned, and there the kernel must match the reference at the fixed tolerances:
+      values   |gpu - cpu32| <= 1e-5 (1 + |cpu32|)        log-dets   |gpu - cpu32| <= 1e-4
+    At most `max_ill` (2 %) of the elements may fall outside tier 1 (at least 3 elements are
+    always allowed, for the knot/edge rows of the small fixtures).
+    Tier 2 — the ill-conditioned remainder: near a knot with steep end derivatives the
+    softmax/exp/log chain and the citardauq root lose up to ~1e-3 against float64 even in the
+    reference (a 1-ulp knot difference moves ld by ~1e-4), so there the kernel is judged by an
+    error model — it must be as accurate as the reference, not systematically worse:
+      per element  |gpu - ref64| <= 8 |cpu32 - ref64| + slack (1 + |ref64|), waived below
+                   floor (1 + |ref64|)
+    and over the whole tensor: mean|gpu - ref64| <= 1.5 mean|cpu32 - ref64| + 1e-7,
+    max|gpu - ref64| <= 4 max|cpu32 - ref64| + slack. NaN patterns must agree with the
+    reference. `kind` ("y" or "ld") defaults from `what`. Returns the tier counts."""
+    import re
+    if kind is None:
+        kind = "ld" if re.search(r"\bld\b|log_det", what) else "y"
     g = np.asarray(gpu, np.float64).ravel()
     c = np.asarray(cpu32, np.float64).ravel()
     r = np.asarray(ref64, np.float64).ravel()
@@ -75,11 +81,27 @@ def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=5e-4, what=""):
     ok = ~np.isnan(c) & ~np.isnan(r)
     g, c, r = g[ok], c[ok], r[ok]
     if g.size == 0:
-        return
-    eg, ec = np.abs(g - r), np.abs(c - r)
+        return {"n": 0, "ill": 0}
+    ec_ = np.abs(c - r)
+    if kind == "y":
+        well = ec_ <= 1e-5 * (1 + np.abs(r))
+        bad1 = well & (np.abs(g - c) > 1e-5 * (1 + np.abs(c)))
+    else:
+        well = ec_ <= 1e-5
+        bad1 = well & (np.abs(g - c) > 1e-4)
+    n_ill = int((~well).sum())
+    assert not bad1.any(), (f"{what}: {int(bad1.sum())} well-conditioned elements exceed the fixed "
+                            f"{'1e-5(1+|ref|)' if kind == 'y' else '1e-4'} tolerance; worst "
+                            f"{np.abs(g - c)[bad1].max():.3g}")
+    assert n_ill <= max(3, max_ill * g.size), (f"{what}: {n_ill}/{g.size} elements are ill-conditioned "
+                                              f"(> {max_ill:.0%})")
+    eg, ec = np.abs(g - r), ec_
     bound = np.maximum(8 * ec + slack * (1 + np.abs(r)), floor * (1 + np.abs(r)))
-    bad = eg > bound
-    assert not bad.any(), (f"{what}: {bad.sum()} elements exceed the fp32 error model; worst "
+    bad = (~well) & (eg > bound)
+    assert not bad.any(), (f"{what}: {bad.sum()} ill-conditioned elements exceed the fp32 error model; worst "
                            f"{eg[bad].max():.3g} (ref err {ec[bad][eg[bad].argmax()]:.3g})")
     assert eg.mean() <= 1.5 * ec.mean() + 1e-7, f"{what}: mean err {eg.mean():.3g} vs reference {ec.mean():.3g}"
     assert eg.max() <= 4 * ec.max() + slack, f"{what}: max err {eg.max():.3g} vs reference {ec.max():.3g}"
+    print(f"[fp32 parity] {what}: {g.size - n_ill}/{g.size} well-conditioned at the fixed tolerance, "
+          f"{n_ill} ({n_ill / g.size:.2%}) by the error model")
+    return {"n": int(g.size), "ill": n_ill}

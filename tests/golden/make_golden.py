@@ -22,7 +22,13 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
   g11_train.npz       TRAIN-mode coupling layers (batch-statistics BatchNorm, coupling_layer.py:18-35):
                       RealNVP(2,8,64) inverse + NLL backward (grads, running stats) and 5 Adam steps
                       on two-moons (README.md:107-117); CouplingLayer(4,16) both directions
-  g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes
+  g12_flowbn.npz      between-layer BatchNorm (normalizing_flow_model.py:67-128): RealNVP(2,8,64,True),
+                      RealNVPSpline(2,8,64,True) and 3x MAF(10,16) with BatchNorm between layers, eval
+                      both directions + log_prob, and a train-mode forward (running-stat update)
+  g13_sequential.npz  SequentialFlow (sequential_flow.py:5-34): 4 CouplingLayers d=2 as in
+                      examples/visualization_demo.py:26-36, and a mixed d=5 chain
+  g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes (+ cfg5: IAF(784,64)
+                      inverse NLL at B=8192 and forward checksums at B=524288)
 
 Each npz holds the module's state_dict arrays under their reference keys (prefixed per case),
 inputs and expected outputs. Nothing pickled; load with numpy.load(allow_pickle=False).
@@ -402,6 +408,117 @@ def g11(flows, models):
     np.savez_compressed(os.path.join(HERE, "g11_train.npz"), **out)
 
 
+def g12(flows, models):
+    """Between-layer BatchNorm: invertible affine with running stats, scalar log-det."""
+    out = {}
+    g = torch.Generator().manual_seed(60)
+    x = torch.cat([moons(1000, 0.05, 42), torch.randn(1000, 2, generator=g) * 1.5, edge_rows(2)[:24]])
+    z = torch.randn(1024, 2, generator=g)
+    cases = [("rn", lambda: models.RealNVP(2, 8, 64, batch_norm_between_layers=True), 0.1, x, z),
+             ("rs", lambda: models.RealNVPSpline(2, 8, 64, batch_norm_between_layers=True), 0.1, x, z),
+             ("maf", lambda: models.NormalizingFlowModel([flows.MaskedAutoregressiveFlow(10, 16) for _ in range(3)],
+                                                         batch_norm_between_layers=True), 0.05,
+              torch.randn(512, 10, generator=g), torch.randn(256, 10, generator=g))]
+    for i, (name, ctor, sigma, xi, zi) in enumerate(cases):
+        torch.manual_seed(600 + i)
+        m = ctor()
+        perturb(m, sigma, 610 + i)
+        bns = m.flow.batch_norms if hasattr(m, "flow") else m.batch_norms
+        with torch.no_grad():  # gamma away from 1 so the log-det term is non-trivial
+            for bn in bns:
+                bn.weight.copy_(0.6 + 0.8 * torch.rand(bn.weight.shape, generator=g))
+                bn.bias.copy_(0.2 * torch.randn(bn.bias.shape, generator=g))
+        m.eval()
+        out.update(sd_arrays(m, name + "."))
+        out.update({f"{name}.x": xi.numpy(), f"{name}.z": zi.numpy()})
+        out.update({f"{name}.{k}": v for k, v in run_model(m, xi, zi).items()})
+        # train mode: forward(z) updates the between-layer running statistics (and, for RealNVP,
+        # normalises the conditioner BatchNorms with batch statistics)
+        m.train()
+        with torch.no_grad():
+            xt, ldt = m.forward(zi)
+        out.update({f"{name}.train_fwd_x": xt.numpy(), f"{name}.train_fwd_ld": ldt.numpy()})
+        out.update(sd_arrays(m, name + ".after_train."))
+    np.savez_compressed(os.path.join(HERE, "g12_flowbn.npz"), **out)
+
+
+def g13(flows):
+    """SequentialFlow: zeros(B) accumulator, layers in order / reverse order."""
+    SequentialFlow = flows.SequentialFlow
+    out = {}
+    g = torch.Generator().manual_seed(70)
+
+    def alt(dim, even):
+        mask = torch.zeros(dim)
+        if even:
+            mask[::2] = 1
+        else:
+            mask[1::2] = 1
+        return mask
+
+    torch.manual_seed(700)
+    s2 = SequentialFlow([flows.CouplingLayer(2, 32, alt(2, i % 2 == 0)) for i in range(4)])
+    torch.manual_seed(701)
+    s5 = SequentialFlow([flows.CouplingLayer(5, 32, alt(5, True)),
+                         flows.SplineCouplingLayer(5, 32, alt(5, False), num_bins=8),
+                         flows.MaskedAutoregressiveFlow(5, 16),
+                         flows.InverseAutoregressiveFlow(5, 16)])
+    for name, m, d in (("s2", s2, 2), ("s5", s5, 5)):
+        perturb(m, 0.1, 710 + d)
+        m.eval()
+        xi = torch.cat([torch.randn(500, d, generator=g) * 1.3, torch.zeros(1, d), torch.full((1, d), 4.0)])
+        zi = torch.randn(300, d, generator=g)
+        with torch.no_grad():
+            zo, ldi = m.inverse(xi)
+            xo, ldf = m.forward(zi)
+        out.update(sd_arrays(m, name + "."))
+        out.update({f"{name}.x": xi.numpy(), f"{name}.z": zi.numpy(), f"{name}.inv_z": zo.numpy(),
+                    f"{name}.inv_ld": ldi.numpy(), f"{name}.fwd_x": xo.numpy(), f"{name}.fwd_ld": ldf.numpy()})
+    np.savez_compressed(os.path.join(HERE, "g13_sequential.npz"), **out)
+
+
+def g8_cfg5(f6):
+    """cfg5 IAF(784,64) (G6 weights): inverse NLL at B=8192 (seed 1237) and forward checksums at
+    B=524288 (seed 1238); merged into g8_full_nll.json."""
+    torch.set_num_threads(8)
+    path = os.path.join(HERE, "g8_full_nll.json")
+    with open(path) as fh:
+        res = json.load(fh)
+    B, d = 8192, 784
+    x = torch.randn(B, d, generator=torch.Generator().manual_seed(1237))
+    t0 = time.time()
+    tot = 0.0
+    with torch.no_grad():
+        for s in range(0, B, 1024):
+            z, ld = f6.inverse(x[s:s + 1024])
+            tot += mvn_logp(z, ld).double().sum().item()
+    res["cfg5i_iaf_d784_B8192"] = {"B": B, "d": d, "seed": 1237, "input_sum_f64": float(x.double().sum()),
+                                   "input_head": [float(v) for v in x.view(-1)[:8]], "nll_f64": -tot / B,
+                                   "ref_seconds": time.time() - t0}
+    print("cfg5i", res["cfg5i_iaf_d784_B8192"], flush=True)
+    B = 524288
+    z = torch.randn(B, d, generator=torch.Generator().manual_seed(1238))
+    t0 = time.time()
+    sx = sax = sld = 0.0
+    with torch.no_grad():
+        for s in range(0, B, 65536):
+            xf, ldf = f6.forward(z[s:s + 65536])
+            sx += xf.double().sum().item()
+            sax += xf.double().abs().sum().item()
+            sld += ldf.double().sum().item()
+            if s == 0:
+                head_x = [float(v) for v in xf[:4].reshape(-1)]
+                head_ld = [float(v) for v in ldf[:64]]
+    res["cfg5f_iaf_d784_B524288"] = {"B": B, "d": d, "seed": 1238, "input_sum_f64": float(z.double().sum()),
+                                     "input_head": [float(v) for v in z.view(-1)[:8]], "out_sum_f64": sx,
+                                     "out_abs_sum_f64": sax, "ld_sum_f64": sld, "out_head_rows4": head_x,
+                                     "ld_head64": head_ld, "ref_seconds": time.time() - t0}
+    print("cfg5f", {k: v for k, v in res["cfg5f_iaf_d784_B524288"].items() if "head" not in k}, flush=True)
+    res["_meta"]["weights_cfg5"] = "g6_iaf784.npz"
+    with open(path, "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
 def g8(m2, m3, m5):
     """Full-scale NLL scalars (float64 mean of the reference's fp32 log_prob)."""
     torch.set_num_threads(8)
@@ -442,18 +559,30 @@ def main():
     if a.only == "g11":
         g11(flows, models)
         return
+    if a.only == "g12":
+        g12(flows, models)
+        return
+    if a.only == "g13":
+        g13(flows)
+        return
+    if a.only == "g8_cfg5":
+        g8_cfg5(g6(flows))
+        return
     import src.utils as src_utils
     g1(flows)
     m2 = g2(models)
     m3 = g3(flows, models)
     g4(flows)
     m5 = g5(flows, models)
-    g6(flows)
+    f6 = g6(flows)
     g7(models, src_utils)
     g9(flows, models)
     g10(flows)
+    g12(flows, models)
+    g13(flows)
     if not a.skip_full:
         g8(m2, m3, m5)
+        g8_cfg5(f6)
     print("golden fixtures written to", HERE)
 
 

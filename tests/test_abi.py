@@ -54,6 +54,13 @@ def test_invalid_arguments_fail_before_any_launch():
     assert rc == -2
     # B == 0 is a valid no-op
     assert L.nfx_affine_coupling(None, None, None, None, 0, 2, 64, 1, 0, None) == 0
+    # between-layer BatchNorm
+    rc = L.nfx_flowbn_apply(None, None, None, 1, 1, 1, 1, 1e-5, 16, 2, 0, None)
+    assert rc == -1 and b"direction" in L.nfx_last_error()
+    rc = L.nfx_flowbn_apply(None, None, None, 1, 1, 1, 1, 1e-5, 16, 2000, 1, None)
+    assert rc == -2
+    assert L.nfx_flowbn_apply(None, None, None, 1, 1, 1, 1, 1e-5, 0, 2, 1, None) == 0
+    assert L.nfx_flowbn_workspace_bytes(1 << 20, 63) >= 8 * 63 * 2
 
 
 def test_product_raises_without_library(monkeypatch, tmp_path):

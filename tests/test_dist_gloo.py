@@ -4,13 +4,16 @@ broadcast replicates rank 0's parameters."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
+
+import nfs_amd
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from nfs_amd.distributed import shard_range
-from _dist_worker import _model, _train_worker, _worker
+from _dist_worker import _model, _syncbn_worker, _train_worker, _train_worker_weighted, _worker
 
 
 def _free_port():
@@ -83,3 +86,61 @@ def test_data_parallel_gradients_match_full_batch(kind):
         for r in range(world):
             assert torch.allclose(torch.from_numpy(res[r][1][k]), p.grad, rtol=1e-4, atol=1e-6), k
 
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_syncbn_merge_and_sums_match_full_batch():
+    """merge_bn_stats / allreduce_bn_sums (nfs_amd/distributed.py, used between the train-mode
+    coupling kernels' passes) called directly on CPU float64 tensors over 2 gloo ranks with
+    unequal shards: the merged (n, mean, M2) and the summed BatchNorm-backward blocks equal the
+    single-process full-batch values; and the between-layer BatchNorm of a train-mode forward
+    (normalizing_flow_model.py:74-79) updates the running statistics from the moments of the
+    whole batch, identical on every rank."""
+    n = 1001
+    res = _spawn(_syncbn_worker, 2, n)
+    X = torch.randn(n, 6, generator=torch.Generator().manual_seed(11), dtype=torch.float64) * 3 + 1
+    mean = X.mean(0)
+    for _, stats, sums, _ in res:
+        np.testing.assert_allclose(stats[:, 0], n)
+        np.testing.assert_allclose(stats[:, 1], mean.numpy(), rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(stats[:, 2], ((X - mean) ** 2).sum(0).numpy(), rtol=1e-12)
+        np.testing.assert_allclose(sums[0], X.sum(0).numpy(), rtol=1e-13)
+        np.testing.assert_allclose(sums[1], (X * X).sum(0).numpy(), rtol=1e-13)
+    torch.manual_seed(5)
+    m = nfs_amd.RealNVPSpline(2, 4, 16, batch_norm_between_layers=True).train()
+    z = torch.randn(n, 2, generator=torch.Generator().manual_seed(12))
+    with torch.no_grad():
+        m.forward(z)
+    ref = {k: v.numpy() for k, v in m.state_dict().items() if "batch_norms" in k and "running" in k}
+    assert ref
+    for k, v in ref.items():
+        assert np.array_equal(res[0][3][k], res[1][3][k]), k
+        np.testing.assert_allclose(res[0][3][k], v, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("kind", ["maf", "spline"])
+def test_unequal_shards_weighted_gradients_match_full_batch(kind):
+    """n % world != 0: average_gradients(local_count=...) weights each rank's mean-loss
+    gradient by its shard size, giving exactly the full-batch gradient."""
+    n = 801
+    res = _spawn(_train_worker_weighted, 2, kind, n)
+    m = _model(1000, kind).train()
+    d = 2 if kind != "maf" else 5
+    x = torch.randn(n, d, generator=torch.Generator().manual_seed(9))
+    (-m.log_prob(x).mean()).backward()
+    for k, p in m.named_parameters():
+        for r in range(2):
+            assert torch.allclose(torch.from_numpy(res[r][1][k]), p.grad, rtol=1e-4, atol=1e-6), k

@@ -229,3 +229,45 @@ def test_small_and_streaming_kernels_agree(cuda_device, d, H, B):
         f(prev)
     for a, b in zip(out["small"], out["streaming"]):
         assert ((a - b).abs() <= 2e-6 * (1 + b.abs())).all(), (a - b).abs().max().item()
+
+
+@pytest.mark.parametrize("B", [1_000_037, 999_999])
+def test_streaming_half_chunk_tail_vs_oracle(cuda_device, B):
+    """Streaming kernel at a batch where every wave runs F >= 1 whole 64-sample chunks AND the
+    leftover chunks are split into 32-sample half chunks (2R <= nwaves): the tail region
+    [F*nwaves*64, B) lies inside the last 2^18 rows, which are checked per element against the
+    oracle in both directions, and the whole batch against the small-batch kernel, including
+    the fused log_prob (LOGP) variant."""
+    m, _ = realnvp_from_golden(cuda_device)
+    x = torch.randn(B, 2, generator=torch.Generator().manual_seed(B)) * 1.5
+    L = nfs_amd._lib
+    f = L.lib().nfx_affine_kernel_policy
+    prev = f(L.NFX_AFFINE_STREAMING)
+    try:
+        with torch.no_grad():
+            xs = x.to(cuda_device)
+            zi, ldi = m.inverse(xs)
+            xf, ldf = m.forward(xs)
+            lp = m.log_prob(xs)
+        f(L.NFX_AFFINE_SMALL)
+        with torch.no_grad():
+            zi2, ldi2 = m.inverse(xs)
+            xf2, ldf2 = m.forward(xs)
+            lp2 = m.log_prob(xs)
+    finally:
+        f(prev)
+    for a, b in ((zi, zi2), (xf, xf2)):
+        assert ((a - b).abs() <= 2e-6 * (1 + b.abs())).all(), (a - b).abs().max().item()
+    for a, b in ((ldi, ldi2), (ldf, ldf2), (lp, lp2)):
+        assert ((a - b).abs() <= 2e-5 + 2e-6 * b.abs()).all(), (a - b).abs().max().item()
+    tail = slice(B - (1 << 18), B)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        zr, ldr = oracle.flow_model(sd, oracle.realnvp_spec(8), x[tail], -1)
+        xr, lfr = oracle.flow_model(sd, oracle.realnvp_spec(8), x[tail], 1)
+        lpr = oracle.gauss_log_prob(zr, ldr)
+    assert_y(zi[tail].cpu(), zr)
+    assert_ld(ldi[tail].cpu(), ldr)
+    assert_y(xf[tail].cpu(), xr)
+    assert_ld(ldf[tail].cpu(), lfr)
+    assert_lp(lp[tail].cpu(), lpr)

@@ -175,6 +175,44 @@ def test_full_scale_nll_cfg4(cuda_device):
     assert abs(nll - meta["nll_f64"]) <= 1e-6 * abs(meta["nll_f64"]), (nll, meta["nll_f64"])
 
 
+def _iaf784(dev):
+    g = load_golden("g6_iaf784.npz")
+    f = nfs_amd.InverseAutoregressiveFlow(784, 64)
+    f.load_state_dict(state_dict_from(g, "", f))
+    return nfs_amd.NormalizingFlowModel([f]).to(dev).eval()
+
+
+def test_full_scale_nll_cfg5i(cuda_device):
+    """BASELINE cfg5 density direction at full size: IAF(784,64) log_prob through the sequential
+    inverse (inverse_autoregressive_flow.py:65-103), B = 8192, NLL vs the reference (G8)."""
+    meta = golden_json("g8_full_nll.json")["cfg5i_iaf_d784_B8192"]
+    x = torch.randn(meta["B"], meta["d"], generator=torch.Generator().manual_seed(meta["seed"]))
+    assert abs(float(x.double().sum()) - meta["input_sum_f64"]) < 1e-3
+    m = _iaf784(cuda_device)
+    nfs_amd.reset_stats()
+    nll = m.nll(x.to(cuda_device))
+    assert nfs_amd.STATS["torch"] == 0
+    assert abs(nll - meta["nll_f64"]) <= 1e-6 * abs(meta["nll_f64"]), (nll, meta["nll_f64"])
+
+
+def test_full_scale_forward_cfg5f(cuda_device):
+    """BASELINE cfg5 sampling direction at full size: IAF(784,64).forward (parallel,
+    inverse_autoregressive_flow.py:30-63), B = 524,288, vs the reference's checksums (G8): the
+    float64 sums of x, |x| and log-det, and the first rows element by element."""
+    meta = golden_json("g8_full_nll.json")["cfg5f_iaf_d784_B524288"]
+    z = torch.randn(meta["B"], meta["d"], generator=torch.Generator().manual_seed(meta["seed"]))
+    assert abs(float(z.double().sum()) - meta["input_sum_f64"]) < 1e-3
+    m = _iaf784(cuda_device)
+    with torch.no_grad():
+        x, ld = m.forward(z.to(cuda_device))
+        sx, sax, sld = (float(v) for v in (x.double().sum(), x.double().abs().sum(), ld.double().sum()))
+    assert abs(sax - meta["out_abs_sum_f64"]) <= 1e-6 * meta["out_abs_sum_f64"], (sax, meta["out_abs_sum_f64"])
+    assert abs(sx - meta["out_sum_f64"]) <= 1e-6 * meta["out_abs_sum_f64"], (sx, meta["out_sum_f64"])
+    assert abs(sld - meta["ld_sum_f64"]) <= 1e-6 * meta["B"], (sld, meta["ld_sum_f64"])
+    assert_y(x[:4].reshape(-1).cpu(), np.asarray(meta["out_head_rows4"]))
+    assert_ld(ld[:64].cpu(), np.asarray(meta["ld_head64"]), 1e-3)
+
+
 def _made_tables(packed, d, H):
     """nk extents + tsafe of the packed MADE image (mirror of MadeLayout, nfx_made_kernel.h)."""
     up4 = lambda v: (v + 3) & ~3

@@ -168,3 +168,37 @@ def test_full_scale_nll_cfg3(cuda_device):
     m, _ = load_model("k8.", cuda_device)
     nll = m.nll(x.to(cuda_device))
     assert abs(nll - meta["nll_f64"]) <= 1e-5, (nll, meta["nll_f64"])
+
+
+@pytest.mark.parametrize("K", [8, 10])
+def test_spline_extreme_logits_vs_oracle(cuda_device, K):
+    """Spline logits the reference handles without NaN: a -inf width/height/derivative logit
+    (softmax weight 0, softplus 0), a spread of ~95 (exp of the minimum is subnormal in torch
+    and flushed by the kernel's exp; min_bin_width/min_derivative absorb it) and a spread of
+    ~300 (exp underflows to 0 in both). The kernel's exp_safe must reproduce all of them."""
+    torch.manual_seed(K)
+    mask = torch.tensor([1.0, 0.0])
+    layer = nfs_amd.SplineCouplingLayer(2, 32, mask, num_bins=K)
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(0.2 * torch.randn_like(p))
+        P = 3 * K - 1
+        b = layer.param_net[4].bias
+        b[P + 0] = float("-inf")        # width logit 0 of the transformed dim 1
+        b[P + 1] = 95.0                 # spread ~95 against the others
+        b[P + K + 2] = -300.0           # height logit far below the rest
+        b[P + K + 3] = float("-inf")
+        b[P + 2 * K] = float("-inf")    # derivative logit: softplus(-inf) = 0
+        b[P + 2 * K + 1] = -120.0       # softplus(-120) subnormal -> min_derivative
+    x = torch.randn(2000, 2) * 2.5
+    sd = {k: v.clone() for k, v in layer.state_dict().items()}
+    layer = layer.to(cuda_device).eval()
+    for direction in (1, -1):
+        with torch.no_grad():
+            yg, lg = (layer.forward if direction > 0 else layer.inverse)(x.to(cuda_device))
+            yr, lr = oracle.spline_coupling(sd, "", x, direction, K=K)
+            y64, l64 = oracle.spline_coupling(sd64(sd), "", x.double(), direction, K=K)
+        assert torch.isfinite(yr).all() and torch.isfinite(lr).all()
+        assert torch.isfinite(yg).all() and torch.isfinite(lg).all()
+        assert_fp32_parity(yg.cpu(), yr, y64, what=f"y dir={direction}")
+        assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}")

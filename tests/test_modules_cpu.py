@@ -150,3 +150,74 @@ def test_arqs_composite_matches_reference(name):
         yi, li = m.inverse(x)
     for got, key in ((yf, "fwd_y"), (lf, "fwd_ld"), (yi, "inv_y"), (li, "inv_ld")):
         np.testing.assert_allclose(got.numpy(), g[f"{name}.{key}"], rtol=1e-5, atol=1e-5, err_msg=key)
+
+
+def _g12_model(name):
+    if name == "rn":
+        return nfs_amd.RealNVP(2, 8, 64, batch_norm_between_layers=True)
+    if name == "rs":
+        return nfs_amd.RealNVPSpline(2, 8, 64, batch_norm_between_layers=True)
+    return nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(10, 16) for _ in range(3)],
+                                        batch_norm_between_layers=True)
+
+
+@pytest.mark.parametrize("name", ["rn", "rs", "maf"])
+def test_between_layer_batchnorm_composite_matches_reference(name):
+    """NormalizingFlowModel(batch_norm_between_layers=True) on the CPU composite path vs G12:
+    state_dict keys, eval both directions, and the train-mode forward's running statistics."""
+    g = load_golden("g12_flowbn.npz")
+    m = _g12_model(name)
+    keys = {k for k, v in m.state_dict().items() if v.dtype != torch.int64}
+    assert {name + "." + k for k in keys} == {k for k in g if k.startswith(name + ".") and
+                                              not k.startswith(name + ".after_train.") and
+                                              k.count(".") > 1 and not k.split(".", 1)[1] in
+                                              ("x", "z", "inv_z", "inv_ld", "fwd_x", "fwd_ld", "log_prob",
+                                               "nll_f64", "train_fwd_x", "train_fwd_ld")}
+    m.load_state_dict(state_dict_from(g, name + ".", m))
+    m.eval()
+    tol = dict(rtol=1e-6, atol=2e-6)
+    with torch.no_grad():
+        z, ld = m.inverse(torch.from_numpy(g[f"{name}.x"]))
+        x, ldf = m.forward(torch.from_numpy(g[f"{name}.z"]))
+    np.testing.assert_allclose(z.numpy(), g[f"{name}.inv_z"], **tol)
+    np.testing.assert_allclose(ld.numpy(), g[f"{name}.inv_ld"], **tol)
+    np.testing.assert_allclose(x.numpy(), g[f"{name}.fwd_x"], **tol)
+    np.testing.assert_allclose(ldf.numpy(), g[f"{name}.fwd_ld"], **tol)
+    m.train()
+    with torch.no_grad():
+        xt, ldt = m.forward(torch.from_numpy(g[f"{name}.z"]))
+    np.testing.assert_allclose(xt.numpy(), g[f"{name}.train_fwd_x"], **tol)
+    np.testing.assert_allclose(ldt.numpy(), g[f"{name}.train_fwd_ld"], **tol)
+    after = state_dict_from(g, f"{name}.after_train.", _g12_model(name))
+    for k, v in m.state_dict().items():
+        if v.is_floating_point():
+            np.testing.assert_allclose(v.numpy(), after[k].numpy(), **tol)
+
+
+def test_sequential_flow_composite_matches_reference():
+    """SequentialFlow (sequential_flow.py:5-34) of mixed layers on the CPU composite path vs G13."""
+    g = load_golden("g13_sequential.npz")
+
+    def alt(dim, even):
+        mask = torch.zeros(dim)
+        mask[(0 if even else 1)::2] = 1
+        return mask
+
+    models = {"s2": nfs_amd.SequentialFlow([nfs_amd.CouplingLayer(2, 32, alt(2, i % 2 == 0)) for i in range(4)]),
+              "s5": nfs_amd.SequentialFlow([nfs_amd.CouplingLayer(5, 32, alt(5, True)),
+                                            nfs_amd.SplineCouplingLayer(5, 32, alt(5, False), num_bins=8),
+                                            nfs_amd.MaskedAutoregressiveFlow(5, 16),
+                                            nfs_amd.InverseAutoregressiveFlow(5, 16)])}
+    with pytest.raises(ValueError):
+        nfs_amd.SequentialFlow(models["s2"].flows[0])
+    for name, m in models.items():
+        m.load_state_dict(state_dict_from(g, name + ".", m))
+        m.eval()
+        with torch.no_grad():
+            z, ld = m.inverse(torch.from_numpy(g[f"{name}.x"]))
+            x, ldf = m.forward(torch.from_numpy(g[f"{name}.z"]))
+        tol = dict(rtol=1e-6, atol=2e-6)
+        np.testing.assert_allclose(z.numpy(), g[f"{name}.inv_z"], **tol)
+        np.testing.assert_allclose(ld.numpy(), g[f"{name}.inv_ld"], **tol)
+        np.testing.assert_allclose(x.numpy(), g[f"{name}.fwd_x"], **tol)
+        np.testing.assert_allclose(ldf.numpy(), g[f"{name}.fwd_ld"], **tol)

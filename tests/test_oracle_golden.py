@@ -202,3 +202,62 @@ def test_train_mode_g11():
     for k in sd4:
         if k.endswith(("running_mean", "running_var")):
             close(sd4[k], g["c4.after." + k], rtol=1e-6, atol=1e-7)
+
+
+G12_CASES = {
+    "rn": (lambda tr: oracle.realnvp_spec(8, training=tr), "flow.batch_norms."),
+    "rs": (lambda tr: oracle.spline_model_spec(8), "flow.batch_norms."),
+    "maf": (lambda tr: oracle.maf_spec(3), "batch_norms."),
+}
+
+
+@pytest.mark.parametrize("name", sorted(G12_CASES))
+def test_between_layer_batchnorm_g12(name):
+    """NormalizingFlowModel(batch_norm_between_layers=True) (normalizing_flow_model.py:25-128):
+    eval both directions + log_prob, and the train-mode forward's running-stat update."""
+    g = load_golden("g12_flowbn.npz")
+    sd = oracle_sd(g, name + ".")
+    sd = {k: v for k, v in sd.items() if not k.startswith("after_train.")}
+    spec_fn, bnp = G12_CASES[name]
+    x, z = torch.from_numpy(g[f"{name}.x"]), torch.from_numpy(g[f"{name}.z"])
+    with torch.no_grad():
+        zi, ldi = oracle.flow_model(sd, spec_fn(False), x, -1, bn_prefix=bnp)
+        xf, ldf = oracle.flow_model(sd, spec_fn(False), z, 1, bn_prefix=bnp)
+        lp = oracle.gauss_log_prob(zi, ldi)
+    tol = dict(rtol=1e-6, atol=2e-6)
+    close(zi, g[f"{name}.inv_z"], **tol)
+    close(ldi, g[f"{name}.inv_ld"], **tol)
+    close(xf, g[f"{name}.fwd_x"], **tol)
+    close(ldf, g[f"{name}.fwd_ld"], **tol)
+    close(lp, g[f"{name}.log_prob"], **tol)
+    sdt = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        xt, ldt = oracle.flow_model(sdt, spec_fn(True), z, 1, bn_prefix=bnp, training=True)
+    close(xt, g[f"{name}.train_fwd_x"], **tol)
+    close(ldt, g[f"{name}.train_fwd_ld"], **tol)
+    after = oracle_sd(g, f"{name}.after_train.")
+    for k, v in after.items():
+        close(sdt[k], v, **tol)
+
+
+G13_SPECS = {
+    "s2": [("coupling", f"flows.{i}.", {}) for i in range(4)],
+    "s5": [("coupling", "flows.0.", {}), ("spline", "flows.1.", {"K": 8}), ("maf", "flows.2.", {}),
+           ("iaf", "flows.3.", {})],
+}
+
+
+@pytest.mark.parametrize("name", sorted(G13_SPECS))
+def test_sequential_flow_g13(name):
+    """SequentialFlow (sequential_flow.py:15-34): zeros(B) accumulator."""
+    g = load_golden("g13_sequential.npz")
+    sd = oracle_sd(g, name + ".")
+    x, z = torch.from_numpy(g[f"{name}.x"]), torch.from_numpy(g[f"{name}.z"])
+    with torch.no_grad():
+        zi, ldi = oracle.sequential_flow(sd, G13_SPECS[name], x, -1)
+        xf, ldf = oracle.sequential_flow(sd, G13_SPECS[name], z, 1)
+    tol = dict(rtol=1e-6, atol=2e-6)
+    close(zi, g[f"{name}.inv_z"], **tol)
+    close(ldi, g[f"{name}.inv_ld"], **tol)
+    close(xf, g[f"{name}.fwd_x"], **tol)
+    close(ldf, g[f"{name}.fwd_ld"], **tol)

@@ -93,7 +93,7 @@ def main():
             for p in glob.glob(os.path.join(d, cfg, "trace", "*", "*_kernel_stats.csv")):
                 shutil.copy(p, f"{dest}_{cfg}_kernel_stats.csv")
             dom = {"affine_coupling_kernel": "cfg2", "spline_coupling_kernel": "cfg3", "made_tile_kernel": "cfg4",
-                   "made_wide_kernel": "cfg5f", "made_seqg_kernel": "cfg5i"}
+                   "made_wide_kernel": "cfg5f", "made_seqs_kernel": "cfg5i"}
             for tag, c in dom.items():
                 # every template instance of the dominant kernel (the last layer runs the fused
                 # log_prob variant), weighted by dispatch count = the per-launch mean bench.py times
@@ -102,8 +102,18 @@ def main():
                     continue
                 n = sum(s.get("pmc_dispatches", 1) for _, s in inst)
                 avg = lambda f: sum(s[f] * s.get("pmc_dispatches", 1) for _, s in inst) / n
+                spl = None
+                for logname in ("fetch.log", "trace.log"):  # bench's JSON line: samples per launch
+                    try:
+                        with open(os.path.join(d, cfg, logname)) as lf:
+                            lines = [ln for ln in lf if ln.startswith("{")]
+                        spl = json.loads(lines[-1])["roofline"]["samples_per_launch"]
+                        break
+                    except (OSError, IndexError, KeyError, ValueError):
+                        continue
                 with open(os.path.join(root, "profiles", f"pmc_traffic_{cfg}.json"), "w") as f:
                     json.dump({"kernel": [k for k, _ in inst], "hbm_bytes_per_launch": avg("hbm_bytes_per_launch"),
+                               "samples_per_launch": spl,
                                "fetch_bytes_raw": avg("fetch_bytes_raw"), "write_bytes": avg("write_bytes"),
                                "source": os.path.basename(dest) + f"_{cfg}.json",
                                "note": "dispatch-weighted over the kernel's template instances; FETCH_SIZE "

@@ -15,12 +15,12 @@ for c in $cfgs; do
   d="$out/$c"
   mkdir -p "$d"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/trace" -- \
-    python3 "$root/bench.py" --config "$c" --steps 10 --warmup 3 --no-cpu > "$d/trace.log" 2>&1 || exit $?
+    python3 "$root/bench.py" --config "$c" --steps 10 --warmup 3 --no-cpu --no-secondary > "$d/trace.log" 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$d/fetch" -- \
-    python3 "$root/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu > "$d/fetch.log" 2>&1 || exit $?
+    python3 "$root/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu --no-secondary > "$d/fetch.log" 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$d/write" -- \
-    python3 "$root/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu > "$d/write.log" 2>&1 || exit $?
+    python3 "$root/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu --no-secondary > "$d/write.log" 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d "$d/sq" -- \
-    python3 "$root/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu > "$d/sq.log" 2>&1 || exit $?
+    python3 "$root/bench.py" --config "$c" --steps 3 --warmup 1 --no-cpu --no-secondary > "$d/sq.log" 2>&1 || exit $?
   echo "profiled $c"
 done
