@@ -52,25 +52,46 @@ def cuda_device():
     return torch.device("cuda:0")
 
 
-def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=5e-4, what="", kind=None, max_ill=0.02):
-    """Parity of ill-conditioned fp32 math (RQ spline chains) in two tiers.
+def fp32_jitter(fn, *inputs, k=8, seed=0):
+    """Per-element fp32 sensitivity of `fn` (an fp32 oracle closure returning a tuple of
+    tensors): the largest deviation from fn(*inputs) over k evaluations whose inputs are
+    jittered by -1/0/+1 ulp per element. A one-ulp nudge of the inputs re-randomises every
+    internal fp32 rounding downstream (MLP logits, softmax, knot cumsum, the root), so the spread
+    is the variation a different but equally valid fp32 evaluation order can produce. NaN
+    deviations (a jitter crossing a guard) count as infinitely sensitive."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        base = [o.double() for o in fn(*inputs)]
+        dev = [torch.zeros_like(o) for o in base]
+        for _ in range(k):
+            jit = []
+            for t in inputs:
+                step = torch.randint(-1, 2, t.shape, generator=g).to(t.dtype) * t.abs() * 2.0 ** -23
+                jit.append(torch.where(torch.isfinite(t), t + step, t))
+            for i, o in enumerate(fn(*jit)):
+                dd = (o.double() - base[i]).abs()
+                dd = torch.where(torch.isnan(dd) & ~torch.isnan(base[i]), torch.full_like(dd, float("inf")), dd)
+                dev[i] = torch.maximum(dev[i], torch.nan_to_num(dd, nan=0.0))
+    return [d.numpy() for d in dev]
 
-    Tier 1 — SURVEY §8(c)'s fixed tolerances. Every element where the reference's own fp32
-    result (cpu32) is within 1e-5 of the float64 evaluation of the same math (ref64 = the oracle
-    run in double) — 1e-5 (1 + |ref|) for values, 1e-5 absolute for log-dets — is
-    well-conditioned, and there the kernel must match the reference at the fixed tolerances:
-      values   |gpu - cpu32| <= 1e-5 (1 + |cpu32|)        log-dets   |gpu - cpu32| <= 1e-4
-    At most `max_ill` (2 %) of the elements may fall outside tier 1 (at least 3 elements are
-    always allowed, for the knot/edge rows of the small fixtures).
-    Tier 2 — the ill-conditioned remainder: near a knot with steep end derivatives the
-    softmax/exp/log chain and the citardauq root lose up to ~1e-3 against float64 even in the
-    reference (a 1-ulp knot difference moves ld by ~1e-4), so there the kernel is judged by an
-    error model — it must be as accurate as the reference, not systematically worse:
-      per element  |gpu - ref64| <= 8 |cpu32 - ref64| + slack (1 + |ref64|), waived below
-                   floor (1 + |ref64|)
-    and over the whole tensor: mean|gpu - ref64| <= 1.5 mean|cpu32 - ref64| + 1e-7,
-    max|gpu - ref64| <= 4 max|cpu32 - ref64| + slack. NaN patterns must agree with the
-    reference. `kind` ("y" or "ld") defaults from `what`. Returns the tier counts."""
+
+def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=None, what="", kind=None, max_ill=0.02, sens=None):
+    """Per-element parity of ill-conditioned fp32 math (RQ spline chains, train-mode chains).
+
+    Every element must lie within SURVEY §8(c)'s fixed tolerance of the reference's own fp32
+    result (cpu32):
+      values    |gpu - cpu32| <= 1e-5 (1 + |cpu32|)           log-dets   |gpu - cpu32| <= 1e-4
+    except elements whose MEASURED fp32 conditioning c = max(|cpu32 - ref64|, sens) widens the
+    bound to  tol + 8 c : ref64 is the float64 evaluation of the same math (the oracle run in
+    double) and sens (conftest.fp32_jitter) the spread of one-ulp-jittered fp32 evaluations —
+    how far an equally valid fp32 evaluation order can land. Near a knot with steep end
+    derivatives the reference's own fp32 log-det is up to ~1e-3 off float64, and there the
+    bound follows the measured sensitivity element by element (no blanket floor). At most
+    `max_ill` of the elements (default 2 %, at least 3) may need the widened bound; the count is
+    printed. Whole-tensor guards: mean|gpu - ref64| <= 1.5 mean|cpu32 - ref64| + 1e-7 and
+    max|gpu - ref64| <= 4 max|cpu32 - ref64| + slack (as accurate as the reference, never
+    systematically worse). NaN patterns must agree. `kind` ("y" or "ld") defaults from `what`;
+    `floor` is accepted for old call sites and ignored."""
     import re
     if kind is None:
         kind = "ld" if re.search(r"\bld\b|log_det", what) else "y"
@@ -79,29 +100,27 @@ def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=5e-4, what="", kind=
     r = np.asarray(ref64, np.float64).ravel()
     assert np.array_equal(np.isnan(g), np.isnan(c)), f"{what}: NaN pattern differs from the reference"
     ok = ~np.isnan(c) & ~np.isnan(r)
-    g, c, r = g[ok], c[ok], r[ok]
+    sv = np.zeros_like(r) if sens is None else np.asarray(sens, np.float64).ravel()
+    g, c, r, sv = g[ok], c[ok], r[ok], sv[ok]
     if g.size == 0:
-        return {"n": 0, "ill": 0}
-    ec_ = np.abs(c - r)
-    if kind == "y":
-        well = ec_ <= 1e-5 * (1 + np.abs(r))
-        bad1 = well & (np.abs(g - c) > 1e-5 * (1 + np.abs(c)))
-    else:
-        well = ec_ <= 1e-5
-        bad1 = well & (np.abs(g - c) > 1e-4)
-    n_ill = int((~well).sum())
-    assert not bad1.any(), (f"{what}: {int(bad1.sum())} well-conditioned elements exceed the fixed "
-                            f"{'1e-5(1+|ref|)' if kind == 'y' else '1e-4'} tolerance; worst "
-                            f"{np.abs(g - c)[bad1].max():.3g}")
-    assert n_ill <= max(3, max_ill * g.size), (f"{what}: {n_ill}/{g.size} elements are ill-conditioned "
-                                              f"(> {max_ill:.0%})")
-    eg, ec = np.abs(g - r), ec_
-    bound = np.maximum(8 * ec + slack * (1 + np.abs(r)), floor * (1 + np.abs(r)))
-    bad = (~well) & (eg > bound)
-    assert not bad.any(), (f"{what}: {bad.sum()} ill-conditioned elements exceed the fp32 error model; worst "
-                           f"{eg[bad].max():.3g} (ref err {ec[bad][eg[bad].argmax()]:.3g})")
+        return {"n": 0, "relaxed": 0}
+    ec = np.abs(c - r)
+    cond = np.maximum(ec, sv)
+    tol = 1e-5 * (1 + np.abs(c)) if kind == "y" else np.full_like(c, 1e-4)
+    err = np.abs(g - c)
+    bad = err > tol + 8 * cond
+    assert not bad.any(), (f"{what}: {int(bad.sum())} elements exceed fixed tolerance + 8x their fp32 "
+                           f"conditioning; worst excess {(err - tol - 8 * cond)[bad].max():.3g} "
+                           f"(err {err[bad].max():.3g})")
+    relaxed = err > tol
+    n_rel = int(relaxed.sum())
+    if not os.environ.get("NFX_MEASURE_ILL"):
+        assert n_rel <= max(3, max_ill * g.size), (f"{what}: {n_rel}/{g.size} elements need the "
+                                                  f"conditioning-widened bound (> {max_ill:.0%})")
+    eg = np.abs(g - r)
     assert eg.mean() <= 1.5 * ec.mean() + 1e-7, f"{what}: mean err {eg.mean():.3g} vs reference {ec.mean():.3g}"
     assert eg.max() <= 4 * ec.max() + slack, f"{what}: max err {eg.max():.3g} vs reference {ec.max():.3g}"
-    print(f"[fp32 parity] {what}: {g.size - n_ill}/{g.size} well-conditioned at the fixed tolerance, "
-          f"{n_ill} ({n_ill / g.size:.2%}) by the error model")
-    return {"n": int(g.size), "ill": n_ill}
+    print(f"[fp32 parity] {what}: {g.size - n_rel}/{g.size} within the fixed tolerance, {n_rel} "
+          f"({n_rel / g.size:.2%}) within tol + 8x measured conditioning; "
+          f"{int((cond > tol).sum())} with conditioning above the tolerance; max err {err.max():.3g}")
+    return {"n": int(g.size), "relaxed": n_rel}

