@@ -79,7 +79,7 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) {
         f32x16 a0, a1;
-        a0 = a1 = load_bias16(P + L.b1 + ht * 32, h);
+        load_bias16_x2(P + L.b1 + ht * 32, h, a0, a1);
 #pragma unroll
         for (int ks = 0; ks < KS1; ++ks) {
             const float w = P[L.w1 + (ht * KS1 + ks) * 64 + lane];
@@ -104,7 +104,7 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
 #pragma unroll
     for (int hto = 0; hto < HT; ++hto) {
         f32x16 a0, a1;
-        a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
+        load_bias16_x2(P + L.b2 + hto * 32, h, a0, a1);
 #pragma unroll
         for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll

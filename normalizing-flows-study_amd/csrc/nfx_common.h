@@ -68,6 +68,15 @@ __device__ __forceinline__ f32x16 load_bias16(const float* __restrict__ tile, in
     return f32x16{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], c[0], c[1], c[2], c[3], e[0], e[1], e[2], e[3]};
 }
 
+// The same bias tile into two accumulators (the two sample tiles of a 64-sample chunk) with two
+// LDS reads instead of one read + 16 v_mov: LDS bandwidth is idle here, while the fp32 vector
+// pipe is the bound (the copies cost as much as 16 VALU ops per tile). The opaque zero keeps the
+// compiler from merging the two reads.
+__device__ __forceinline__ int opaque_zero();
+__device__ __forceinline__ void load_bias16_x2(const float* __restrict__ tile, int h, f32x16& a0, f32x16& a1) {
+    a0 = load_bias16(tile, h);
+    a1 = load_bias16(tile + opaque_zero(), h);
+}
 
 // A zero the compiler cannot see through. Offsetting the LDS weight pointer by it inside a
 // grid-stride loop stops LICM from hoisting every (loop-invariant) weight read out of the

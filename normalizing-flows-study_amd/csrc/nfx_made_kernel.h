@@ -163,7 +163,7 @@ __device__ __forceinline__ void made_hidden(const float* __restrict__ W, int wof
 #pragma unroll
     for (int hto = 0; hto < HT; ++hto) {
         f32x16 a0, a1;
-        a0 = a1 = load_bias16(W + boff + hto * 32, h);
+        load_bias16_x2(W + boff + hto * 32, h, a0, a1);
 #pragma unroll
         for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
         // ---- layer 1: h1 = relu(W1m x + b1), K streamed in 32-dim chunks through LDS ----
         f32x16 h1[HT][2];
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) h1[ht][0] = h1[ht][1] = load_bias16(W + L.b1 + ht * 32, h);
+        for (int ht = 0; ht < HT; ++ht) load_bias16_x2(W + L.b1 + ht * 32, h, h1[ht][0], h1[ht][1]);
         for (int kc = 0; kc < L.NKC; ++kc) {
             stage_in(in, base, d, B, 32 * kc, stg);
             wave_lds_sync();
@@ -256,8 +256,8 @@ __global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
         float acc0 = 0.f, acc1 = 0.f;
         for (int j = 0; j < L.NJ; ++j) {
             f32x16 mu0, mu1, al0, al1;
-            mu0 = mu1 = load_bias16(W + L.b4 + (j * 2 + 0) * 32, h);
-            al0 = al1 = load_bias16(W + L.b4 + (j * 2 + 1) * 32, h);
+            load_bias16_x2(W + L.b4 + (j * 2 + 0) * 32, h, mu0, mu1);
+            load_bias16_x2(W + L.b4 + (j * 2 + 1) * 32, h, al0, al1);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll

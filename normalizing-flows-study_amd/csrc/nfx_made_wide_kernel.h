@@ -55,7 +55,7 @@ __device__ __forceinline__ void hidden_tile2(const float* __restrict__ W, int wo
                                              const f32x16 (&hin)[HT][2], f32x16& o0, f32x16& o1) {
     const int lane = lane_id(), h = lane >> 5;
     f32x16 a0, a1;
-    a0 = a1 = load_bias16(W + boff + hto * 32, h);
+    load_bias16_x2(W + boff + hto * 32, h, a0, a1);
 #pragma unroll
     for (int kt = 0; kt < NK; ++kt) {
 #pragma unroll
@@ -98,8 +98,8 @@ __device__ __forceinline__ void out_pair2(const float* __restrict__ wb, const fl
                                           const f32x16 (&hin)[HT][2], f32x16& mu0, f32x16& mu1,
                                           f32x16& al0, f32x16& al1) {
     const int lane = lane_id(), h = lane >> 5;
-    mu0 = mu1 = load_bias16(b4 + (j * 2 + 0) * 32, h);
-    al0 = al1 = load_bias16(b4 + (j * 2 + 1) * 32, h);
+    load_bias16_x2(b4 + (j * 2 + 0) * 32, h, mu0, mu1);
+    load_bias16_x2(b4 + (j * 2 + 1) * 32, h, al0, al1);
 #pragma unroll
     for (int kt = 0; kt < NK; ++kt) {
 #pragma unroll
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
 
         f32x16 h1[HT][2];
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) h1[ht][0] = h1[ht][1] = load_bias16(B1 + ht * 32, h);
+        for (int ht = 0; ht < HT; ++ht) load_bias16_x2(B1 + ht * 32, h, h1[ht][0], h1[ht][1]);
 
         int kc = 0;
         auto l1_step = [&](auto seg) {

@@ -66,12 +66,21 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
     }
 }
 
-static spline_kernel_t pick_spline(int HT, int K, int dir, bool logp) {
+static spline_kernel_t pick_spline(int HT, int K, int dir, bool logp, int d) {
+    if (d == 2) {
+        switch (HT) {
+            case 1: return spline_pick_ht<1, 2>(K, dir, logp);
+            case 2: return spline_pick_ht<2, 2>(K, dir, logp);
+            case 3: return spline_pick_ht<3, 2>(K, dir, logp);
+            case 4: return spline_pick_ht<4, 2>(K, dir, logp);
+            default: return nullptr;
+        }
+    }
     switch (HT) {
-        case 1: return spline_pick_ht<1>(K, dir, logp);
-        case 2: return spline_pick_ht<2>(K, dir, logp);
-        case 3: return spline_pick_ht<3>(K, dir, logp);
-        case 4: return spline_pick_ht<4>(K, dir, logp);
+        case 1: return spline_pick_ht<1, 0>(K, dir, logp);
+        case 2: return spline_pick_ht<2, 0>(K, dir, logp);
+        case 3: return spline_pick_ht<3, 0>(K, dir, logp);
+        case 4: return spline_pick_ht<4, 0>(K, dir, logp);
         default: return nullptr;
     }
 }
@@ -115,7 +124,7 @@ static int spline_launch(const float* packed, const float* in, float* out, float
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "spline_coupling: null pointer");
     if (in == out) return set_error(NFX_EINVAL, "spline_coupling: in and out must not alias");
     const int HT = (H + 31) / 32;
-    spline_kernel_t k = pick_spline(HT, K, direction, fused);
+    spline_kernel_t k = pick_spline(HT, K, direction, fused, d);
     if (!k) return set_error(NFX_EUNSUPPORTED, "spline_coupling: no kernel for H=%d K=%d", H, K);
     // Scalars exactly as the reference's Python-float expressions round them into fp32 ops.
     SplineConsts C;

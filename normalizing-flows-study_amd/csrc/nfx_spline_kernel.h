@@ -76,9 +76,57 @@ __device__ __forceinline__ float tsoftplus(float x) {
     return x > 20.f ? x : l;
 }
 
+// ---- VALU-lean helpers of the forward spline (the fp32 pipe is shared with the fp32 MFMAs, so
+// every vector instruction here adds to the layer's time; DESIGN.md "roofline") ----
+// a / b for b > 0 finite and a/b in the normal range (the spline's divisors are all clamped to
+// >= eps): the hardware reciprocal plus one Newton correction of the quotient (Markstein),
+// within 1 ulp of the correctly rounded quotient and usually equal to it — 4 instructions
+// instead of the 10 of the IEEE division sequence (div_scale/div_fmas/div_fixup).
+__device__ __forceinline__ float div_fast(float a, float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    const float q = a * r;
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+// log(x) for normal x > 0 (the callers clamp to >= 1e-8 or pass 1 + u): hardware log2 * ln2,
+// ~2 ulp.
+__device__ __forceinline__ float log_fast(float x) { return __builtin_amdgcn_logf(x) * 0.693147182f; }
+
+// exp_safe on a pair (widths, heights): the compensated exp2 of exp_fast with the arithmetic
+// as packed fp32 (v_pk_mul/v_pk_fma), the two v_exp_f32 and the -inf clamp per element.
+__device__ __forceinline__ f32x2 exp_safe2(f32x2 x) {
+#ifdef NFX_SPLINE_SCALAR
+    return f32x2{exp_safe(x.x), exp_safe(x.y)};
+#else
+    x = __builtin_elementwise_maximum(x, f32x2{-128.f, -128.f});
+    const f32x2 c = {1.44269502f, 1.44269502f};
+    const f32x2 t = x * c;
+    const f32x2 e = __builtin_elementwise_fma(x, f32x2{1.9259629e-8f, 1.9259629e-8f},
+                                              __builtin_elementwise_fma(x, c, -t));
+    const f32x2 r = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    return __builtin_elementwise_fma(r, e * f32x2{0.693147182f, 0.693147182f}, r);
+#endif
+}
+
+// torch softplus (threshold 20) on a pair, log1p as in tsoftplus with the hardware log.
+__device__ __forceinline__ f32x2 tsoftplus2(f32x2 x) {
+#pragma clang fp contract(off)
+    const f32x2 u = exp_safe2(x);
+    const f32x2 w = u + f32x2{1.f, 1.f};
+    const f32x2 wm1 = w - f32x2{1.f, 1.f};
+    f32x2 l;
+    l.x = wm1.x == 0.f ? u.x : log_fast(w.x) * (u.x * __builtin_amdgcn_rcpf(wm1.x));
+    l.y = wm1.y == 0.f ? u.y : log_fast(w.y) * (u.y * __builtin_amdgcn_rcpf(wm1.y));
+    return f32x2{x.x > 20.f ? x.x : l.x, x.y > 20.f ? x.y : l.y};
+}
+
 // One RQ spline evaluation of SplineCouplingLayer._rational_quadratic_spline for a single
 // input v with its 3K-1 unnormalised parameters p[] (:182-309, per element).
 // Returns the spline-level guarded output (NaN/Inf -> input, :306) and log|det| (-> 0, :307).
+// Same operation order as the reference (contraction off); work the reference spends on bins
+// the sample is not in is skipped: the widths/heights of every bin are needed for the knots,
+// but only the selected bin's two derivatives go through softplus (the reference evaluates
+// all K-1), and the knots of the bin (not the width array) are gathered by a select chain on
+// the monotone comparisons `knot_k <= v` (= searchsorted(right=True) - 1, clamped).
 template <int K, bool INV>
 __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], const SplineConsts& C,
                                                float& out, float& lad) {
@@ -88,72 +136,76 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
     out = v;
     lad = 0.f;
     if (v >= -B && v <= B) {
-        float w[K], h[K], cwk[K + 1], chk[K + 1], dk[K + 1];
-        // softmax (max-subtracted exp, times the reciprocal of the sum) then min-width affine
-        {
-            float m = p[0];
+        // softmax of widths (.x) and heights (.y) together: max-subtracted exp, times the
+        // reciprocal of the sum (ATen's vectorised softmax), then the min-width affine (:204-219)
+        f32x2 m = {p[0], p[K]};
 #pragma unroll
-            for (int k = 1; k < K; ++k) m = tmax(m, p[k]);
-            float s = 0.f;
+        for (int k = 1; k < K; ++k) m = __builtin_elementwise_maximum(m, f32x2{p[k], p[K + k]});
+        f32x2 e[K];
+        f32x2 s = {0.f, 0.f};
 #pragma unroll
-            for (int k = 0; k < K; ++k) { w[k] = exp_safe(p[k] - m); s = s + w[k]; }
-            const float inv = 1.f / s;
-#pragma unroll
-            for (int k = 0; k < K; ++k) w[k] = tclamp_min(C.min_w + C.cw * (w[k] * inv), eps);
+        for (int k = 0; k < K; ++k) {
+#ifdef NFX_SPLINE_SCALAR
+            e[k] = f32x2{exp_safe(p[k] - m.x), exp_safe(p[K + k] - m.y)};
+            s.x = s.x + e[k].x;
+            s.y = s.y + e[k].y;
+#else
+            e[k] = exp_safe2(f32x2{p[k], p[K + k]} - m);
+            s = s + e[k];
+#endif
         }
-        {
-            float m = p[K];
-#pragma unroll
-            for (int k = 1; k < K; ++k) m = tmax(m, p[K + k]);
-            float s = 0.f;
-#pragma unroll
-            for (int k = 0; k < K; ++k) { h[k] = exp_safe(p[K + k] - m); s = s + h[k]; }
-            const float inv = 1.f / s;
-#pragma unroll
-            for (int k = 0; k < K; ++k) h[k] = tclamp_min(C.min_h + C.ch * (h[k] * inv), eps);
-        }
+        const f32x2 inv = {div_fast(1.f, s.x), div_fast(1.f, s.y)};
+        const f32x2 mins = {C.min_w, C.min_h}, scl = {C.cw, C.ch};
         // knots: ATen's CPU cumsum accumulates float in double and rounds each prefix (:208-213)
+        float cwk[K + 1], chk[K + 1];
         {
             double aw = 0.0, ah = 0.0;
+            const f32x2 tb = {C.two_bound, C.two_bound}, nb = {-B, -B};
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                aw += (double)w[k];
-                ah += (double)h[k];
+#ifdef NFX_SPLINE_SCALAR
+                const float wx = tclamp_min(C.min_w + C.cw * (e[k].x * inv.x), eps);
+                const float wy = tclamp_min(C.min_h + C.ch * (e[k].y * inv.y), eps);
+                aw += (double)wx;
+                ah += (double)wy;
                 cwk[k + 1] = C.two_bound * (float)aw + (-B);
                 chk[k + 1] = C.two_bound * (float)ah + (-B);
+#else
+                const f32x2 wv = __builtin_elementwise_maximum(mins + scl * (e[k] * inv), f32x2{eps, eps});
+                aw += (double)wv.x;
+                ah += (double)wv.y;
+                const f32x2 kn = tb * f32x2{(float)aw, (float)ah} + nb;
+                cwk[k + 1] = kn.x;
+                chk[k + 1] = kn.y;
+#endif
             }
             cwk[0] = -B; cwk[K] = B;
             chk[0] = -B; chk[K] = B;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                w[k] = tclamp_min(cwk[k + 1] - cwk[k], eps);
-                h[k] = tclamp_min(chk[k + 1] - chk[k], eps);
-            }
         }
-        dk[0] = 1.f;
-        dk[K] = 1.f;
-#pragma unroll
-        for (int k = 0; k < K - 1; ++k) dk[k + 1] = tclamp_min(C.min_d + tsoftplus(p[2 * K + k]), eps);
-
-        // searchsorted(knots, v, right=True) - 1, clamped to [0, K-1]  (:241-244)
-        int cnt = 0;
-#pragma unroll
-        for (int k = 0; k <= K; ++k) cnt += ((INV ? chk[k] : cwk[k]) <= v) ? 1 : 0;
-        int bin = cnt - 1;
-        bin = bin < 0 ? 0 : (bin > K - 1 ? K - 1 : bin);
-        // gather by select (keeps every array in registers)
-        float w_k = w[0], x_k = cwk[0], h_k = h[0], y_k = chk[0], d_k = dk[0], d_k1 = dk[1];
+        // bin = last k in [0, K-1] with knot_k <= v (knots non-decreasing; the pinned knot_0 =
+        // -B <= v): gather the bin's knots and the raw logits of its two derivatives
+        float x_k = cwk[0], x_k1 = cwk[1], y_k = chk[0], y_k1 = chk[1];
+        float ua = 0.f, ub = p[2 * K];
+        bool in0 = true, inl = (K == 1);
 #pragma unroll
         for (int k = 1; k < K; ++k) {
-            const bool s = (k == bin);
-            w_k = s ? w[k] : w_k;
-            x_k = s ? cwk[k] : x_k;
-            h_k = s ? h[k] : h_k;
-            y_k = s ? chk[k] : y_k;
-            d_k = s ? dk[k] : d_k;
-            d_k1 = s ? dk[k + 1] : d_k1;
+            const bool c = (INV ? chk[k] : cwk[k]) <= v;
+            x_k = c ? cwk[k] : x_k;
+            x_k1 = c ? cwk[k + 1] : x_k1;
+            y_k = c ? chk[k] : y_k;
+            y_k1 = c ? chk[k + 1] : y_k1;
+            ua = c ? p[2 * K + k - 1] : ua;
+            if (k < K - 1) ub = c ? p[2 * K + k] : ub;
+            if (k == 1) in0 = !c;
+            if (k == K - 1) inl = c;
         }
-        const float s_k = h_k / tclamp_min(w_k, eps);
+        // derivatives d_k, d_{k+1}: clamp(min_d + softplus(u), eps), pinned to 1 at both ends
+        const f32x2 sp = tsoftplus2(f32x2{ua, ub});
+        const float d_k = in0 ? 1.f : tclamp_min(C.min_d + sp.x, eps);
+        const float d_k1 = inl ? 1.f : tclamp_min(C.min_d + sp.y, eps);
+        const float w_k = tclamp_min(x_k1 - x_k, eps);   // :214-215 (w = diff of pinned knots)
+        const float h_k = tclamp_min(y_k1 - y_k, eps);   // :227-228
+        const float s_k = div_fast(h_k, w_k);            // (w_k >= eps already: the clamp at :260 is a no-op)
         float o, l;
         if constexpr (INV) {
             // citardauq root (:266-281)
@@ -163,23 +215,23 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
             const float b = h_k * d_k - dy * t;
             const float c = -s_k * dy;
             const float disc = tclamp_min(b * b - 4.f * a * c, 0.f);
-            float den = -b - sqrtf(disc);
+            float den = -b - __builtin_amdgcn_sqrtf(disc);
             den = fabsf(den) < eps ? eps : den;
             const float xi = tclamp((2.f * c) / den, 0.f, 1.f);
             o = xi * w_k + x_k;
             const float omx = 1.f - xi;
             const float dld = s_k + (d_k1 + d_k - 2.f * s_k) * xi * omx;
             const float nld = (s_k * s_k) * (d_k1 * (xi * xi) + 2.f * s_k * xi * omx + d_k * (omx * omx));
-            l = -logf(tclamp_min(nld, eps)) + 2.f * logf(tclamp_min(dld, eps));
+            l = -log_fast(tclamp_min(nld, eps)) + 2.f * log_fast(tclamp_min(dld, eps));
         } else {
             // forward (:283-293)
-            const float xi = tclamp((v - x_k) / tclamp_min(w_k, eps), 0.f, 1.f);
+            const float xi = tclamp(div_fast(v - x_k, w_k), 0.f, 1.f);
             const float omx = 1.f - xi;
             const float den = tclamp_min(s_k + (d_k1 + d_k - 2.f * s_k) * xi * omx, eps);
             const float num = h_k * (s_k * (xi * xi) + d_k * xi * omx);
-            o = y_k + num / den;
+            o = y_k + div_fast(num, den);
             const float nd = (s_k * s_k) * (d_k1 * (xi * xi) + 2.f * s_k * xi * omx + d_k * (omx * omx));
-            l = logf(tclamp_min(nd / tclamp_min(den * den, eps), eps));
+            l = log_fast(tclamp_min(div_fast(nd, tclamp_min(den * den, eps)), eps));
         }
         out = o;
         lad = l;
@@ -188,12 +240,21 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
     if (nonfinite(lad)) lad = 0.f;    // :307
 }
 
-template <int HT, int K, int DIR, bool LOGP>
-__global__ __launch_bounds__(256) void spline_coupling_kernel(
+// DS = the data dimension when it is fixed at compile time (2: the two-moons-shaped BASELINE
+// cfg3 / RealNVPSpline path), 0 = runtime d <= 8. With DS = 2 a lane's sample row is one
+// 8-byte load and the layer-1 operands of the two sample tiles come out of one
+// v_permlane32_swap of that row (no per-element loads or 64-bit address arithmetic), and every
+// loop over the row is compile-time.
+// Occupancy: the d = 2 kernels at H <= 64 fit 168 VGPRs without spilling, i.e. 3 waves per SIMD
+// (3 workgroups per CU) instead of 2 — more MFMA/VALU interleaving across waves.
+template <int HT, int K, int DIR, bool LOGP, int DS>
+__global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coupling_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
-    float* __restrict__ logdet, int64_t B, int d, SplineConsts C, int accumulate,
+    float* __restrict__ logdet, int64_t B, int d_rt, SplineConsts C, int accumulate,
     int64_t nchunks, float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
 #pragma clang fp contract(off)
+    constexpr int DMAX = DS ? DS : 8;
+    const int d = DS ? DS : d_rt;
     const SplineLayout L = spline_layout(HT, d);
     extern __shared__ f32x4 lds4[];
     {
@@ -209,26 +270,32 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
 
     // Software pipeline: chunk c + nwaves's x rows and incoming log-det load while chunk c runs.
     struct Fetch {
-        float xb[2][4];  // raw layer-1 operands x[sample base+32st+col][2ks+h]
-        float xr[8];     // the lane's own sample row
+        float xb[2][4];   // raw layer-1 operands x[sample base+32st+col][2ks+h] (DS = 0)
+        float xr[DMAX];   // the lane's own sample row
         float ldin;
     };
     auto fetch = [&](int64_t c, Fetch& f) {
         const int64_t base = c * 64;
         const bool live = c < nchunks;
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            const int64_t s = base + 32 * st + col;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const int k = 2 * ks + h;
-                f.xb[st][ks] = (live && ks < KS1 && k < d && s < B) ? in[s * d + k] : 0.f;
-            }
-        }
         const int64_t so = base + lane;
         const bool row = live && so < B;
+        if constexpr (DS == 2) {
+            const f32x2 v = row ? *reinterpret_cast<const f32x2*>(in + so * 2) : f32x2{0.f, 0.f};
+            f.xr[0] = v.x;
+            f.xr[1] = v.y;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f.xr[j] = (row && j < d) ? in[so * d + j] : 0.f;
+            for (int st = 0; st < 2; ++st) {
+                const int64_t s = base + 32 * st + col;
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const int k = 2 * ks + h;
+                    f.xb[st][ks] = (live && ks < KS1 && k < d && s < B) ? in[s * d + k] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < DMAX; ++j) f.xr[j] = (row && j < d) ? in[so * d + j] : 0.f;
+        }
         f.ldin = (row && accumulate) ? logdet[so] : 0.f;
     };
     float mkb[4];
@@ -246,27 +313,42 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
         fetch(c + nwaves, nxt);
 
         // Layer-1 B operands (x rescaled, times mask), k-steps padded to 4.
+        float xraw[2][4];
+        if constexpr (DS == 2) {
+            // lanes 0..31 hold the rows of samples base+col, lanes 32..63 those of base+32+col;
+            // operand (st, k = h) of lane (col, h) is x[base+32st+col][h]: one row swap
+            const float other = halves_other(cur.xr[0], cur.xr[1]);
+            xraw[0][0] = h ? other : cur.xr[0];
+            xraw[1][0] = h ? cur.xr[1] : other;
+#pragma unroll
+            for (int ks = 1; ks < 4; ++ks) xraw[0][ks] = xraw[1][ks] = 0.f;
+        } else {
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) xraw[st][ks] = cur.xb[st][ks];
+        }
         float xb[2][4];
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
-                float xv = cur.xb[st][ks];
+                float xv = xraw[st][ks];
                 if (C.rescale) xv = C.rs_to_scale * (xv - C.rs_lo) - C.bound;
                 xb[st][ks] = xv * mkb[ks];
             }
         }
         const int64_t so = base + lane;
-        float xr[8];
+        float xr[DMAX];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xr[j] = cur.xr[j];
+        for (int j = 0; j < DMAX; ++j) xr[j] = cur.xr[j];
 
         // Layer 1 + ReLU
         f32x16 h1[HT][2];
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
             f32x16 a0, a1;
-            a0 = a1 = load_bias16(P + L.b1 + ht * 32, h);
+            load_bias16_x2(P + L.b1 + ht * 32, h, a0, a1);
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 if (ks < KS1) {
@@ -288,7 +370,7 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
 #pragma unroll
         for (int hto = 0; hto < HT; ++hto) {
             f32x16 a0, a1;
-            a0 = a1 = load_bias16(P + L.b2 + hto * 32, h);
+            load_bias16_x2(P + L.b2 + hto * 32, h, a0, a1);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -311,14 +393,14 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
             h2[hto][1] = a1;
         }
 
-        float y[8];
+        float y[DMAX];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = xr[j];
+        for (int j = 0; j < DMAX; ++j) y[j] = xr[j];
         float ld = 0.f;
         for (int t = 0; t < NT; ++t) {
             // Layer 3, tile t: the 3K-1 parameters of transformed dim tdim[t].
             f32x16 a0, a1;
-            a0 = a1 = load_bias16(P + L.b3 + t * 32, h);
+            load_bias16_x2(P + L.b3 + t * 32, h, a0, a1);
 #pragma unroll
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
@@ -344,24 +426,30 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
             const int dt = (int)P[L.tdim + t];
             float v = 0.f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v = (j == dt) ? xr[j] : v;
+            for (int j = 0; j < DMAX; ++j) v = (j == dt) ? xr[j] : v;
             if (C.rescale) v = C.rs_to_scale * (v - C.rs_lo) - C.bound;
             float o, l;
             rq_spline_elem<K, (DIR < 0)>(v, prm, C, o, l);
             if (C.rescale) o = (o + C.bound) * C.rs_from_scale + C.rs_lo;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) y[j] = (j == dt) ? o : y[j];
+            for (int j = 0; j < DMAX; ++j) y[j] = (j == dt) ? o : y[j];
             ld = (t == 0) ? l : ld + l;
         }
         if (so < B) {
             float m = 0.f;
+            float yo[DMAX];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < DMAX; ++j) {
                 const float v = nonfinite(y[j]) ? 0.f : y[j];
-                if (j < d) {
-                    out[so * d + j] = v;
-                    m = (j == 0) ? gauss_sq0(v) : gauss_sq(m, v);
-                }
+                yo[j] = v;
+                if (j < d) m = (j == 0) ? gauss_sq0(v) : gauss_sq(m, v);
+            }
+            if constexpr (DS == 2) {
+                *reinterpret_cast<f32x2*>(out + so * 2) = f32x2{yo[0], yo[1]};
+            } else {
+#pragma unroll
+                for (int j = 0; j < DMAX; ++j)
+                    if (j < d) out[so * d + j] = yo[j];
             }
             if (nonfinite(ld)) ld = 0.f;
             const float ldt = accumulate ? cur.ldin + ld : ld;
@@ -383,7 +471,8 @@ __global__ __launch_bounds__(256) void spline_coupling_kernel(
 typedef void (*spline_kernel_t)(const float*, const float*, float*, float*, int64_t, int,
                                 SplineConsts, int, int64_t, float*, double*, float);
 
-template <int HT>
+// DS = 0: runtime d <= 8; DS = 2: the d = 2 specialisation (nfx_spline_d2_h*.hip)
+template <int HT, int DS>
 spline_kernel_t spline_pick_ht(int K, int dir, bool logp);
 
 }  // namespace nfx
