@@ -435,6 +435,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         # on the launch stream. Kept out of the headline loop because each event record adds
         # ~5 us of GPU idle between kernels (measured, profiles/).
         eager_only[0] = True
+        aux_events = []
         if coupling_train:
             from nfs_amd.flows import coupling as _cp
             _cp.TRAIN_EVENTS = []
@@ -448,7 +449,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
             for _ in range(a.steps):
                 step()
             torch.cuda.synchronize()
-            events = bwd_mod.BACKWARD_EVENTS
+            events = [e for e in bwd_mod.BACKWARD_EVENTS if e[0] != "made_wgrad_kernel"]
+            aux_events = [e for e in bwd_mod.BACKWARD_EVENTS if e[0] == "made_wgrad_kernel"]
             bwd_mod.BACKWARD_EVENTS = None
         else:
             flow.layer_events = []
@@ -575,7 +577,16 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         result["nll_f64"] = None
         result["roofline"]["note"] = ("dominant kernel = the fused backward (forward recompute + "
                                       "data-gradient chain, 2x the layer's forward flops); the "
-                                      "weight gradients run as batched library GEMMs")
+                                      "weight gradients run as the MFMA sample-contraction kernel "
+                                      "(made_wgrad_kernel, HBM-bound: reads the factor rows once)")
+        if aux_events:
+            wd = [e0.elapsed_time(e1) for _, e0, e1 in aux_events]
+            wms = sum(wd) / len(wd)
+            fac_bytes = 4 * B * (2 * 63 + 3 * 64 + 3 * 64 + 63)  # δ + input rows the contraction reads
+            result["roofline"]["wgrad"] = {"kernel": "made_wgrad_kernel", "bound": "hbm", "mean_launch_ms": wms,
+                                           "bytes_per_launch": fac_bytes,
+                                           "achieved": fac_bytes / (wms * 1e-3) / 1e9, "peak": 8000.0,
+                                           "unit": "GB/s", "frac": fac_bytes / (wms * 1e-3) / 1e9 / 8000.0}
     if world == 1 and with_cpu and training:
         result["cpu_baseline"] = cpu_training_baseline(model, spec, x)
     elif world == 1 and with_cpu:

@@ -175,11 +175,11 @@ int nfx_made_affine_logprob(const float* packed, const float* in, float* out, fl
  * nfx_made_pack_backward adds the transposed weight tiles to a packed image built by
  * nfx_made_pack (same buffer). nfx_made_affine_backward recomputes the layer and writes
  *   grad_in [B, d]  = dL/dx
- *   factors [3d + 6H + 4][B], feature-major rows:
+ *   factors [3d + 6H + 4][P], feature-major rows (P = nfx_made_factor_pitch(B)):
  *     [δμ | δα] (2d) | δ3 | δ2 | δ1 (H each) | h3, 1 | h2, 1 | h1, 1 (H + 1 each) | x, 1 (d + 1)
  * from grad_out = dL/dz [B, d] and grad_log_det = dL/dlog_det [B]. The parameter gradients
- * are plain GEMMs over the sample dimension: [dW4 | db4] = [δμ;δα]·[h3;1]ᵀ, [dW3 | db3] =
- * δ3·[h2;1]ᵀ, [dW2 | db2] = δ2·[h1;1]ᵀ, [dW1 | db1] = δ1·[x;1]ᵀ (each dW ⊙ its MADE mask).
+ * are contractions over the sample dimension (nfx_made_backward_weights): dW4 = [δμ;δα]·h3ᵀ,
+ * dW3 = δ3·h2ᵀ, dW2 = δ2·h1ᵀ, dW1 = δ1·xᵀ (each ⊙ its MADE mask), db = row sums of δ.
  * `factors` holds nfx_made_backward_factor_floats(B, d, H) floats.
  * ------------------------------------------------------------------------------------- */
 int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
@@ -187,6 +187,22 @@ size_t nfx_made_backward_factor_floats(int64_t B, int d, int H);
 int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,
                              const float* grad_log_det, float* grad_in, float* factors, int64_t B,
                              int d, int H, int variant, void* stream);
+
+/* MADE parameter gradients from the factors above (both MAF and IAF backward kernels write this
+ * layout, rows of pitch nfx_made_factor_pitch(B) = B rounded up to 32): fp32 MFMA contractions
+ * over the sample dimension, reduced in float64 in a fixed order (deterministic), written to
+ * `grads` in MADE.parameters() order — net.0.weight [H,d], net.0.bias [H], net.2.weight [H,H],
+ * net.2.bias, net.4.weight, net.4.bias, net.6.weight [2d,H], net.6.bias [2d] — each weight
+ * gradient multiplied by its mask (masks[4]: the MaskedLinear `mask` buffers, device, row-major;
+ * the gradient of F.linear(a, W * mask, b), masked_linear.py:14-18). `grads` holds
+ * nfx_made_param_floats(d, H) floats, `workspace` nfx_made_wgrad_workspace_bytes(B, d, H) bytes.
+ * Replaces the autograd weight-gradient GEMMs of made.py:81-134. */
+int64_t nfx_made_factor_pitch(int64_t B);
+size_t nfx_made_param_floats(int d, int H);
+size_t nfx_made_wgrad_workspace_bytes(int64_t B, int d, int H);
+int nfx_made_backward_weights(const float* factors, int64_t B, int d, int H,
+                              const float* const* masks, float* grads, void* workspace,
+                              void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Training: backward of SplineCouplingLayer.forward/inverse
@@ -258,6 +274,15 @@ int nfx_affine_train_backward(const float* tpack, const float* in, const float* 
                               void* workspace, void* stream);
 int nfx_affine_train_assemble(const double* G, const double* stats1, const double* stats2, int d,
                               int H, float eps, float* grads, void* stream);
+/* Eval-mode CouplingLayer under autograd (coupling_layer.py:40-96 with model.eval(): BatchNorm
+ * normalises with its RUNNING statistics, which are buffers, so nothing couples the samples).
+ * Same kernels: nfx_affine_eval_stats writes triples (-1, running_mean, -running_var) for the 4
+ * BatchNorms (s_net.1, s_net.4, b_net.1, b_net.4); nfx_affine_train_pack(stats1, stats2) folds
+ * them exactly like eval BatchNorm; nfx_affine_train_backward(stage 1..3) and
+ * nfx_affine_train_assemble then give dL/dx and every parameter gradient (gamma/beta included)
+ * with the batch-statistics terms of the BatchNorm backward dropped (n < 0). */
+int nfx_affine_eval_stats(float* const* running_mean, float* const* running_var, int H,
+                          double* stats1, double* stats2, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Gaussian base log-density + NLL partial sums — the log_prob glue of the callers

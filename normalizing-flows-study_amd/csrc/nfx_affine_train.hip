@@ -33,14 +33,16 @@ namespace nfx {
 
 // BatchNorm fold of layer `layer` (0 or 1) of net P from float64 statistics triples
 // [Hp][3] = (n, mean, M2): r = 1/sqrt(var + eps), var = M2 / n (biased, as BatchNorm1d
-// normalises). stats == nullptr -> identity (mean 0, r 1).
+// normalises). stats == nullptr -> identity (mean 0, r 1). A triple with n < 0 carries RUNNING
+// statistics (eval-mode BatchNorm, nfx_affine_eval_stats): (-1, running_mean, -running_var), so
+// var = M2 / n = running_var exactly and the backward drops the batch-coupling terms.
 struct BnFold {
     double mean, r;
 };
 __device__ inline BnFold bn_fold(const double* stats, int Hp, int net, int row, double eps) {
     if (!stats) return {0.0, 1.0};
     const double* q = stats + ((size_t)net * Hp + row) * 3;
-    const double var = q[0] > 0.0 ? q[2] / q[0] : 0.0;
+    const double var = q[0] != 0.0 ? q[2] / q[0] : 0.0;
     return {q[1], 1.0 / sqrt(var + eps)};
 }
 
@@ -283,6 +285,19 @@ __global__ void affine_train_running_kernel(const double* stats1, const double* 
     if (p.rv[k]) p.rv[k][row] = (float)(momentum * var_u + (1.0 - momentum) * (double)p.rv[k][row]);
 }
 
+// Eval-mode statistics triples from the running statistics of the 4 BatchNorms
+// (s_net.1, s_net.4, b_net.1, b_net.4): stats{1,2}[net][row] = (-1, running_mean, -running_var).
+__global__ void affine_eval_stats_kernel(NfxBnPtrs p, int H, int Hp, double* stats1, double* stats2) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (net * 2 + layer) * Hp + row
+    if (i >= 4 * Hp) return;
+    const int k = i / Hp, row = i % Hp, net = k >> 1, layer = k & 1;
+    double* q = (layer ? stats2 : stats1) + ((size_t)net * Hp + row) * 3;
+    const bool live = row < H;
+    q[0] = -1.0;
+    q[1] = live ? (double)p.rm[k][row] : 0.0;
+    q[2] = live ? -(double)p.rv[k][row] : -1.0;
+}
+
 int train_sum_finish(const float* part, int nw, int len, double* out, hipStream_t s) {
     affine_train_sum_finish<<<(len + 15) / 16, 256, 0, s>>>(part, nw, len, out);
     return check_launch("affine_train_sum_finish");
@@ -418,6 +433,21 @@ extern "C" int nfx_affine_train_update_running(const double* stats1, const doubl
     const int Hp = 32 * ((H + 31) / 32);
     affine_train_running_kernel<<<(4 * H + 255) / 256, 256, 0, (hipStream_t)stream>>>(stats1, stats2, p, H, Hp, momentum);
     return check_launch("affine_train_running_kernel");
+}
+
+extern "C" int nfx_affine_eval_stats(float* const* running_mean, float* const* running_var, int H, double* stats1,
+                                     double* stats2, void* stream) {
+    if (!stats1 || !stats2 || !running_mean || !running_var || H <= 0)
+        return set_error(NFX_EINVAL, "affine_eval_stats: bad arguments");
+    NfxBnPtrs p;
+    for (int k = 0; k < 4; ++k) {
+        if (!running_mean[k] || !running_var[k]) return set_error(NFX_EINVAL, "affine_eval_stats: null running stats");
+        p.rm[k] = running_mean[k];
+        p.rv[k] = running_var[k];
+    }
+    const int Hp = 32 * ((H + 31) / 32);
+    affine_eval_stats_kernel<<<(4 * Hp + 255) / 256, 256, 0, (hipStream_t)stream>>>(p, H, Hp, stats1, stats2);
+    return check_launch("affine_eval_stats_kernel");
 }
 
 extern "C" int nfx_affine_train_backward(const float* tpack, const float* x, const float* gy, const float* gld,

@@ -145,14 +145,15 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
     }
     if constexpr (STAGE == TS_BWD2 || STAGE == TS_BWD3) {
         // k1 = sum g / N, k2 = sum g x^ / N in accumulator order, N = the batch the statistics
-        // were taken over (all ranks under SyncBN)
+        // were taken over (all ranks under SyncBN); N < 0 marks running statistics (eval-mode
+        // BatchNorm): the normalisation does not depend on the batch, k1 = k2 = 0
         const double N = stats2[0];
         const double* S = G + (STAGE == TS_BWD2 ? GL.g1s : GL.g2s);
         for (int i = threadIdx.x; i < 4 * Hp; i += 256) {
             const int n = i / (2 * Hp), q = (i / Hp) & 1, a = i % Hp;  // a: accumulator index
             const int ht = a >> 5, hh = (a >> 4) & 1, r = a & 15;
             const int row = 32 * ht + crow(r, hh);
-            kc[i] = (float)(S[(n * 2 + q) * Hp + row] / N);
+            kc[i] = N > 0.0 ? (float)(S[(n * 2 + q) * Hp + row] / N) : 0.f;  // N < 0: running stats
         }
     }
     __syncthreads();

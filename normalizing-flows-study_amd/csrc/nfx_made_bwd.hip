@@ -10,9 +10,9 @@
 // activations; gx = the epilogue's direct term + W1mᵀ δ1. The weight gradients are reductions
 // over the SAMPLE dimension (K = B), which the per-sample tile layout cannot contract without a
 // transpose per tile, so the kernel writes the per-sample factors feature-major (δ4ᵀ, δ3ᵀ, δ2ᵀ,
-// δ1ᵀ, h3ᵀ, h2ᵀ, h1ᵀ: coalesced 128-byte rows, one half-wave per feature row) and the weight
-// gradients are plain GEMMs over them (gW4 = δ4ᵀ·h3, …, gW1 = δ1ᵀ·x; hipBLASLt through torch),
-// masked like the reference's weight*mask.
+// δ1ᵀ, h3ᵀ, h2ᵀ, h1ᵀ: coalesced 128-byte rows, one half-wave per feature row, row pitch
+// P = B rounded up to 32) and the weight gradients are MFMA sample contractions over them
+// (nfx_made_wgrad.hip: gW4 = δ4·h3ᵀ, …, gW1 = δ1·xᵀ), masked like the reference's weight*mask.
 //
 // Epilogue backward, per element (torch semantics of the reference ops):
 //   a = clamp(alpha, -3, 3); e = exp(-a); zr = (x - mu) * e; z = finite(zr) ? zr : 0
@@ -58,15 +58,24 @@ __global__ void made_bwd_pack_kernel(NfxMlpRaw net, int d, int H, float* packed)
 // the scalar offset, and the descriptor's range check drops rows >= nrows; lanes past B get an
 // offset outside every range. No per-element branches or 64-bit address math.
 __device__ __forceinline__ void store_fm(float* __restrict__ dst, const f32x16& t, int row0, int nrows, int64_t B,
-                                         int64_t base) {
+                                         int64_t P, int64_t base) {
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, (int)(((int64_t)nrows * B - base) * 4),
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, (int)(((int64_t)nrows * P - base) * 4),
                                                       0x00020000);
-    const int vo = base + col < B ? (int)((col + 4 * h * B) * 4) : (int)0xFFFFFFF0;
+    const int vo = base + col < B ? (int)((col + 4 * h * P) * 4) : (int)0xFFFFFFF0;
+    if (row0 + 32 <= nrows) {  // uniform: the whole tile is inside the block
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rowu = row0 + (r & 3) + 8 * (r >> 2);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * B * 4), 0);
+        for (int r = 0; r < 16; ++r) {
+            const int rowu = row0 + (r & 3) + 8 * (r >> 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * P * 4), 0);
+        }
+    } else {  // last tile of a ragged block: rows past it belong to the next block
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int rowu = row0 + (r & 3) + 8 * (r >> 2);
+            if (rowu + 4 * h < nrows)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * P * 4), 0);
+        }
     }
 }
 
@@ -122,14 +131,15 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     // feature-major factors: [d4 (2d) | d3 | d2 | d1 (H each) | h3, 1 | h2, 1 | h1, 1 (H+1 each) |
     // x, 1 (d+1)] rows x B — the trailing ones rows turn each weight-gradient GEMM into the
     // bias gradient as well (its last column)
+    const int64_t P = (B + 31) & ~(int64_t)31;  // factor row pitch (nfx_made_factor_pitch)
     float* D4 = acts;
-    float* D3 = D4 + (int64_t)2 * d * B;
-    float* D2 = D3 + (int64_t)H * B;
-    float* D1 = D2 + (int64_t)H * B;
-    float* H3 = D1 + (int64_t)H * B;
-    float* H2 = H3 + (int64_t)(H + 1) * B;
-    float* H1 = H2 + (int64_t)(H + 1) * B;
-    float* X1 = H1 + (int64_t)(H + 1) * B;
+    float* D3 = D4 + (int64_t)2 * d * P;
+    float* D2 = D3 + (int64_t)H * P;
+    float* D1 = D2 + (int64_t)H * P;
+    float* H3 = D1 + (int64_t)H * P;
+    float* H2 = H3 + (int64_t)(H + 1) * P;
+    float* H1 = H2 + (int64_t)(H + 1) * P;
+    float* X1 = H1 + (int64_t)(H + 1) * P;
 
     for (int64_t t = (int64_t)blockIdx.x * kBwdWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kBwdWaves) {
         const int64_t base = t * 32;
@@ -150,19 +160,19 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         const float* Pt = packed + opaque_zero();
         {
             // x and the ones rows, feature-major: half-wave h writes dim row 2i+h of 32 samples
-            const auto rs = __builtin_amdgcn_make_buffer_rsrc(X1 + base, 0, (int)(((int64_t)(d + 1) * B - base) * 4),
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(X1 + base, 0, (int)(((int64_t)(d + 1) * P - base) * 4),
                                                               0x00020000);
-            const int vo = base + col < B ? (int)((col + h * B) * 4) : (int)0xFFFFFFF0;
+            const int vo = base + col < B ? (int)((col + h * P) * 4) : (int)0xFFFFFFF0;
 #pragma unroll
             for (int i = 0; i < 32; ++i)
                 if (2 * i < d)
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(2 * i + h < d ? xt[col * S + 2 * i + h] : 1.f), rs,
-                                                          vo, (int)(2 * i * B * 4), 0);
+                                                          vo, (int)(2 * i * P * 4), 0);
             if (h == 0 && base + col < B) {
-                if ((d & 1) == 0) X1[(int64_t)d * B + base + col] = 1.f;  // odd d: written above (row 2i+1 = d)
-                H3[(int64_t)H * B + base + col] = 1.f;
-                H2[(int64_t)H * B + base + col] = 1.f;
-                H1[(int64_t)H * B + base + col] = 1.f;
+                if ((d & 1) == 0) X1[(int64_t)d * P + base + col] = 1.f;  // odd d: written above (row 2i+1 = d)
+                H3[(int64_t)H * P + base + col] = 1.f;
+                H2[(int64_t)H * P + base + col] = 1.f;
+                H1[(int64_t)H * P + base + col] = 1.f;
             }
         }
 
@@ -188,11 +198,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         made_hidden1<HT>(Wf, L.w2, L.b2, h1, h2);
         const uint32_t m1 = relu_bits<HT>(h1);
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) store_fm(H1, h1[ht], 32 * ht, H, B, base);
+        for (int ht = 0; ht < HT; ++ht) store_fm(H1, h1[ht], 32 * ht, H, B, P, base);
         made_hidden1<HT>(Wf, L.w3, L.b3, h2, h3);
         const uint32_t m2 = relu_bits<HT>(h2);
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) store_fm(H2, h2[ht], 32 * ht, H, B, base);
+        for (int ht = 0; ht < HT; ++ht) store_fm(H2, h2[ht], 32 * ht, H, B, P, base);
 
         // layer 4 for every output block (kept for the log-det sum), then the epilogue backward.
         // d4[j*2 + 0] = mu / δmu rows of block j, d4[j*2 + 1] = alpha / δalpha rows (t4 k order).
@@ -225,7 +235,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         }
         const uint32_t m3 = relu_bits<HT>(h3);
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) store_fm(H3, h3[ht], 32 * ht, H, B, base);
+        for (int ht = 0; ht < HT; ++ht) store_fm(H3, h3[ht], 32 * ht, H, B, P, base);
 
         // ld_raw = -sum_i clamp(alpha_i, -3, 3) of the lane's sample, summed in the forward
         // kernel's order (rows past d: alpha = 0)
@@ -278,13 +288,13 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (j < NJ) {
-                store_fm(D4, d4[2 * j], 32 * j, d, B, base);                        // mu rows
-                store_fm(D4 + (int64_t)d * B, d4[2 * j + 1], 32 * j, d, B, base);   // alpha rows
+                store_fm(D4, d4[2 * j], 32 * j, d, B, P, base);                        // mu rows
+                store_fm(D4 + (int64_t)d * P, d4[2 * j + 1], 32 * j, d, B, P, base);   // alpha rows
             }
         }
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
-            store_fm(D3, g[ht], 32 * ht, H, B, base);
+            store_fm(D3, g[ht], 32 * ht, H, B, P, base);
         }
         f32x16 g2[HT];
 #pragma unroll
@@ -296,7 +306,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         }
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
-            store_fm(D2, g2[ht], 32 * ht, H, B, base);
+            store_fm(D2, g2[ht], 32 * ht, H, B, P, base);
         }
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
@@ -307,7 +317,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         }
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
-            store_fm(D1, g[ht], 32 * ht, H, B, base);
+            store_fm(D1, g[ht], 32 * ht, H, B, P, base);
         }
         // gx = direct term (in the tile) + W1mᵀ δ1, accumulator layout rows = dims
         wave_lds_sync();
@@ -352,7 +362,7 @@ extern "C" int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float*
 
 extern "C" size_t nfx_made_backward_factor_floats(int64_t B, int d, int H) {
     if (B < 0 || d <= 0 || H <= 0) return 0;
-    return (size_t)B * (size_t)(3 * d + 6 * H + 4);
+    return (size_t)((B + 31) & ~(int64_t)31) * (size_t)(3 * d + 6 * H + 4);
 }
 
 extern "C" int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,

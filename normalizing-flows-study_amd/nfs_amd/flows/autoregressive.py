@@ -15,6 +15,8 @@ ROCm device every direction runs as one gfx950 kernel (csrc/nfx_made*.hip):
     degree are known, and each output once — the same values (masked weights multiply exact
     zeros) at the cost of ONE MADE evaluation instead of d.
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -116,25 +118,6 @@ class MADE(nn.Module):
         return [m for m in self.net if isinstance(m, nn.BatchNorm1d)]
 
 
-def _sample_gemm(a, b, chunk=4096):
-    """a [M, B] · b [N, B]ᵀ for a long sample dimension B: split-K as one strided-batched GEMM
-    over B // chunk contiguous sample chunks (a library GEMM picks one tile column for such
-    shapes and leaves most CUs idle), plus the remainder, reduced over the chunks."""
-    M, Bn = a.shape
-    S = Bn // chunk
-    out = None
-    if S >= 2:
-        n = S * chunk
-        pa = a[:, :n].reshape(M, S, chunk).transpose(0, 1)               # [S, M, chunk]
-        pb = b[:, :n].reshape(b.shape[0], S, chunk).permute(1, 2, 0)     # [S, chunk, N]
-        out = torch.bmm(pa, pb).sum(dim=0)
-        a, b = a[:, n:], b[:, n:]
-    if a.shape[1] > 0:
-        r = a @ b.t()
-        out = r if out is None else out + r
-    return out
-
-
 class _MadeAffineFlow(HipFlow):
     """Shared HIP plumbing of MAF / IAF (conditioner = MADE(dim, H, 2))."""
 
@@ -195,24 +178,34 @@ class _MadeAffineFlow(HipFlow):
         if ev is not None:
             e1.record()
             ev.append(("made_bwd_kernel", e0, e1))
-        o = 0
+        return gx, self._weight_grads(fac, B)
 
-        def take(rows):
-            nonlocal o
-            t = fac[o:o + rows * B].view(rows, B)
-            o += rows * B
-            return t
-
-        d4, d3, d2, d1 = take(2 * d), take(H), take(H), take(H)
-        h3, h2, h1, x1 = take(H + 1), take(H + 1), take(H + 1), take(d + 1)
-        lins = self.conditioner.linears()
-        grads = {}
-        for lin, dl, act in zip(lins, (d1, d2, d3, d4), (x1, h1, h2, h3)):
-            g = _sample_gemm(dl, act)  # [out, in + 1]: weight gradient | bias gradient
-            grads[lin.weight] = g[:, :-1] * lin.mask.to(g.dtype)
-            if lin.bias is not None:
-                grads[lin.bias] = g[:, -1]
-        return gx, [grads.get(p) for p in self.parameters()]
+    def _weight_grads(self, fac, B):
+        """MADE parameter gradients (parameters() order) from the feature-major factors:
+        nfx_made_backward_weights (MFMA sample contractions, masks applied)."""
+        d, H = self.dim, self.conditioner.hidden_dim
+        L = _lib.lib()
+        dev = fac.device
+        grads = torch.empty(L.nfx_made_param_floats(d, H), device=dev, dtype=torch.float32)
+        ws = torch.empty(max(1, L.nfx_made_wgrad_workspace_bytes(B, d, H)), device=dev, dtype=torch.uint8)
+        masks = [lin.mask.to(device=dev, dtype=torch.float32).contiguous() for lin in self.conditioner.linears()]
+        mp = (ctypes.c_void_p * 4)(*[_lib.ptr(m) for m in masks])
+        ev = BACKWARD_EVENTS
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _lib.check(L.nfx_made_backward_weights(_lib.ptr(fac), B, d, H, mp, _lib.ptr(grads), _lib.ptr(ws),
+                                               _lib.stream_of(fac)), "nfx_made_backward_weights")
+        if ev is not None:
+            e1.record()
+            ev.append(("made_wgrad_kernel", e0, e1))
+        grads._nfx_keep = (masks, ws)
+        out, o = [], 0
+        for p in self.conditioner.parameters():
+            n = p.numel()
+            out.append(grads[o:o + n].view_as(p))
+            o += n
+        return out
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
         packed = self._packed(x.device, self._build_pack)

@@ -6,6 +6,10 @@ in eval mode the layer runs as ONE fused gfx950 kernel (csrc/nfx_affine*.hip): b
 MLPs on fp32 MFMA with BatchNorm folded from its running statistics, the affine transform,
 the NaN/Inf guards and the log-det.
 
+In eval mode under autograd (e.g. fine-tuning with frozen BatchNorm statistics) the same fused
+backward kernels run with the running statistics in place of the batch statistics
+(`_hip_backward`, nfx_affine_eval_stats), so gradients never recompute through ATen.
+
 In TRAIN mode (the reference's training loops, README.md:107-117 / plots/_common.py:194-211)
 the conditioner BatchNorm normalises with batch statistics; on a ROCm device that runs through
 the train-mode kernels (csrc/nfx_affine_train.hip, `_CouplingTrainFunction`): two statistics
@@ -199,8 +203,42 @@ class CouplingLayer(HipFlow):
         tpack._nfx_keep = (keep, mask, epack, ws)  # sources alive while the kernels are queued
         return y, ld, tpack, stats
 
-    def _train_backward(self, x, gy, gld, direction, tpack, stats):
-        """dL/dx and the parameter gradients (parameters() order) of one train-mode call."""
+    # -- eval mode under autograd (running-statistics BatchNorm) -----------------------------
+    def _hip_backward_ok(self, x, direction):
+        """Eval-mode call under autograd: the train-mode backward kernels with the BatchNorm
+        running statistics in place of batch statistics (nfx_affine_eval_stats)."""
+        bns = self._batchnorms()
+        if x.dtype != torch.float32 or x.dim() != 2 or len(bns) != 4:
+            return False
+        if any(bn.training or not bn.affine or bn.running_mean is None for bn in bns):
+            return False
+        return x.shape[1] == self.data_dim and self.data_dim <= MAX_D and self._hidden() <= MAX_H_TRAIN
+
+    def _build_eval_backward_pack(self, device):
+        L = _lib.lib()
+        d, H = self.data_dim, self._hidden()
+        s_raw, b_raw, keep = self._raw_nets()
+        mask = self.mask.detach().to(device=device, dtype=torch.float32).contiguous()
+        stats = torch.empty(2, L.nfx_affine_train_stats_doubles(H), device=device, dtype=torch.float64)
+        st = _lib.stream_of(stats)
+        bns = [self.s_net[1], self.s_net[4], self.b_net[1], self.b_net[4]]
+        rm = (ctypes_vp * 4)(*[bn.running_mean.data_ptr() for bn in bns])
+        rv = (ctypes_vp * 4)(*[bn.running_var.data_ptr() for bn in bns])
+        p = _lib.ptr
+        _lib.check(L.nfx_affine_eval_stats(rm, rv, H, p(stats[0]), p(stats[1]), st), "nfx_affine_eval_stats")
+        tpack = torch.empty(L.nfx_affine_train_pack_floats(d, H), device=device, dtype=torch.float32)
+        _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), p(stats[0]), p(stats[1]), d, H, p(tpack), None, st),
+                   "nfx_affine_train_pack")
+        tpack._nfx_keep = (keep, mask)
+        return tpack, stats
+
+    def _hip_backward(self, x, gy, gld, direction):
+        tpack, stats = self._packed(x.device, self._build_eval_backward_pack, slot="_nfx_evalbwd_pack_cache")
+        return self._train_backward(x, gy, gld, direction, tpack, stats, sync=False)
+
+    def _train_backward(self, x, gy, gld, direction, tpack, stats, sync=True):
+        """dL/dx and the parameter gradients (parameters() order) of one train-mode call
+        (sync=False: eval mode, the BatchNorm sums are plain parameter-gradient partials)."""
         L = _lib.lib()
         x = x.contiguous()
         B, d = x.shape
@@ -226,7 +264,7 @@ class CouplingLayer(HipFlow):
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
                 ev.append((f"affine_train_kernel<BWD{stage}>", e0, e1))
-            if stage in s_blocks:
+            if sync and stage in s_blocks:
                 _dist.allreduce_bn_sums(s_blocks[stage])
         grads = torch.empty(L.nfx_affine_train_param_floats(d, H), device=dev, dtype=torch.float32)
         _lib.check(L.nfx_affine_train_assemble(p(G), p(stats[0]), p(stats[1]), d, H, float(self.s_net[1].eps),

@@ -249,3 +249,60 @@ def test_eval_after_train_uses_running_stats(cuda_device):
         yr, _ = ref.inverse(x.double().cpu())
     _close(y1, yr, what="eval after train")
     assert (y1 - y0).abs().max().item() > 1e-4  # the running statistics did change
+
+
+@pytest.mark.parametrize("d,H,B,direction", [
+    (2, 64, 1, -1), (2, 64, 1000, 1), (2, 64, 65537, -1), (1, 32, 500, -1), (3, 16, 777, 1),
+    (5, 48, 4097, -1), (8, 64, 3000, 1), (2, 20, 129, -1),
+])
+def test_eval_mode_backward_vs_float64_autograd(cuda_device, d, H, B, direction):
+    """Eval-mode CouplingLayer under autograd (running-statistics BatchNorm, coupling_layer.py:
+    40-96 with model.eval()): the fused train-mode backward kernels with the running statistics
+    (nfx_affine_eval_stats, n < 0 triples), no recompute through ATen; gamma/beta gradients
+    included, running statistics untouched."""
+    layer = _perturbed_layer(d, H, 300 + d * 5 + H, mask_even=(B % 2 == 1))
+    ref = copy.deepcopy(layer).double().eval()
+    ref32 = copy.deepcopy(layer).eval()
+    gpu = layer.to(cuda_device).eval()
+    before = {k: v.clone() for k, v in gpu.named_buffers()}
+    gen = torch.Generator().manual_seed(B + 11)
+    x = (torch.randn(B, d, generator=gen) * 1.3 + 0.2)
+    wy = torch.randn(B, d, generator=gen)
+    wl = torch.randn(B, generator=gen)
+    xr = x.double().requires_grad_(True)
+    yr, ldr = ref.forward(xr) if direction > 0 else ref.inverse(xr)
+    ((yr * wy.double()).sum() + (ldr * wl.double()).sum()).backward()
+    y32, ld32 = ref32.forward(x) if direction > 0 else ref32.inverse(x)
+    ((y32 * wy).sum() + (ld32 * wl).sum()).backward()
+    nfs_amd.reset_stats()
+    xg = x.to(cuda_device).requires_grad_(True)
+    yg, ldg = gpu.forward(xg) if direction > 0 else gpu.inverse(xg)
+    ((yg * wy.to(cuda_device)).sum() + (ldg * wl.to(cuda_device)).sum()).backward()
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 2, nfs_amd.STATS
+    _close(yg, yr, what="y")
+    _close(ldg, ldr, what="log_det")
+    _gclose(xg.grad, xr.grad, what="dL/dx", ref32=None)
+    for (k, pg), (_, pr), (_, p32) in zip(gpu.named_parameters(), ref.named_parameters(), ref32.named_parameters()):
+        _gclose(pg.grad, pr.grad, what=k + " (eval)", ref32=p32.grad)
+    for k, v in gpu.named_buffers():
+        assert torch.equal(v, before[k]), f"eval backward changed buffer {k}"
+
+
+def test_eval_mode_realnvp_step_matches_float64(cuda_device):
+    """A full RealNVP(2,8,64) NLL step in eval mode: 8 HIP forwards + 8 fused eval backwards."""
+    g = load_golden("g11_train.npz")
+    m = _load(nfs_amd.RealNVP(2, 8, 64), g, "rn.init.")
+    ref = copy.deepcopy(m).double().eval()
+    gpu = m.to(cuda_device).eval()
+    x = torch.from_numpy(g["rn.x"])
+    zr, ldr = ref.inverse(x.double())
+    lr = -(-0.5 * (zr.pow(2).sum(1) + 2 * np.log(2 * np.pi)) + ldr).mean()
+    lr.backward()
+    nfs_amd.reset_stats()
+    z, ld = gpu.inverse(x.to(cuda_device))
+    loss = -(-0.5 * (z.pow(2).sum(1) + 2 * np.log(2 * np.pi)) + ld).mean()
+    loss.backward()
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 16, nfs_amd.STATS
+    assert abs(loss.item() - lr.item()) <= 1e-5
+    for (k, pg), (_, pr) in zip(gpu.named_parameters(), ref.named_parameters()):
+        _gclose(pg.grad, pr.grad, frac=5e-4, what=k + " (eval step)")
