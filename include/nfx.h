@@ -169,9 +169,11 @@ int nfx_made_affine_logprob(const float* packed, const float* in, float* out, fl
                             int variant, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * Training: backward of MaskedAutoregressiveFlow.inverse
- * (masked_autoregressive_flow.py:18-44) under autograd — the reference's density-training
- * direction — for d <= 64, H <= 64 and no BatchNorm (NFX_EUNSUPPORTED otherwise).
+ * Training: backward of the PARALLEL MADE directions under autograd —
+ * MaskedAutoregressiveFlow.inverse (masked_autoregressive_flow.py:18-44, the density-training
+ * direction; variant NFX_MAF_INVERSE) and InverseAutoregressiveFlow.forward
+ * (inverse_autoregressive_flow.py:30-63; NFX_IAF_FORWARD) — for d <= 64, H <= 64 and no
+ * BatchNorm (NFX_EUNSUPPORTED otherwise).
  * nfx_made_pack_backward adds the transposed weight tiles to a packed image built by
  * nfx_made_pack (same buffer). nfx_made_affine_backward recomputes the layer and writes
  *   grad_in [B, d]  = dL/dx
@@ -197,6 +199,15 @@ int nfx_made_affine_backward(const float* packed, const float* in, const float* 
  * the gradient of F.linear(a, W * mask, b), masked_linear.py:14-18). `grads` holds
  * nfx_made_param_floats(d, H) floats, `workspace` nfx_made_wgrad_workspace_bytes(B, d, H) bytes.
  * Replaces the autograd weight-gradient GEMMs of made.py:81-134. */
+/* Backward of the SEQUENTIAL directions (NFX_IAF_INVERSE: inverse_autoregressive_flow.py:65-103,
+ * the IAF density direction; NFX_MAF_FORWARD: masked_autoregressive_flow.py:46-78) for
+ * d <= 4096, H <= 128, no BatchNorm: the d MADE calls of the reference are differentiated as one
+ * forward recompute + one reverse sweep per sample (a triangular adjoint solve). Writes grad_in
+ * and the same factor layout (X1 = the MADE input zs), so the parameter gradients are again
+ * nfx_made_backward_weights. */
+int nfx_made_seq_backward(const float* packed, const float* in, const float* grad_out,
+                          const float* grad_log_det, float* grad_in, float* factors, int64_t B,
+                          int d, int H, int variant, void* stream);
 int64_t nfx_made_factor_pitch(int64_t B);
 size_t nfx_made_param_floats(int d, int H);
 size_t nfx_made_wgrad_workspace_bytes(int64_t B, int d, int H);

@@ -111,7 +111,7 @@ __device__ __forceinline__ f32x16 chain_gmem(const float* __restrict__ A, int ot
 
 constexpr int kBwdWaves = 8;  // 2 per SIMD; weights are read from L2, LDS holds the tiles
 
-template <int HT>
+template <int HT, int VAR>
 __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, const float* __restrict__ gout,
     const float* __restrict__ gld_in, float* __restrict__ gin, float* __restrict__ acts, int64_t B, int d,
@@ -237,18 +237,20 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) store_fm(H3, h3[ht], 32 * ht, H, B, P, base);
 
-        // ld_raw = -sum_i clamp(alpha_i, -3, 3) of the lane's sample, summed in the forward
-        // kernel's order (rows past d: alpha = 0)
+        // ld_raw = -sum_i clamp(alpha_i, -3, 3) (MAF inverse) / +sum_i clamp(alpha_i, -2, 2) (IAF
+        // forward) of the lane's sample, summed in the forward kernel's order (rows past d: 0)
+        constexpr bool IAF = VAR == NFX_IAF_FORWARD;
+        constexpr float ALO = IAF ? -2.f : -3.f, AHI = IAF ? 2.f : 3.f, LDLIM = IAF ? 50.f : 100.f;
         float asum0 = 0.f;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) asum0 = asum0 + tclamp(d4[2 * j + 1][r], -3.f, 3.f);
-        const float ldraw = -halves_sum(asum0, asum0);
+            for (int r = 0; r < 16; ++r) asum0 = asum0 + tclamp(d4[2 * j + 1][r], ALO, AHI);
+        const float ldraw = IAF ? halves_sum(asum0, asum0) : -halves_sum(asum0, asum0);
         const float gld = (lane < 32 && col < rows) ? gld_in[base + col] : 0.f;
         float gld1 = nonfinite(ldraw) ? 0.f : gld;
         const float ld1 = nonfinite(ldraw) ? 0.f : ldraw;
-        if (!(ld1 >= -100.f && ld1 <= 100.f)) gld1 = 0.f;
+        if (!(ld1 >= -LDLIM && ld1 <= LDLIM)) gld1 = 0.f;
         const float gld1s = __shfl(gld1, col, 64);  // both lane halves of sample col
 
         // epilogue backward; the direct dz/dx term replaces x in the tile (same lane, same slot)
@@ -261,16 +263,30 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
                 const float xv = *px;
                 const float gz = gt[col * S + dim];
                 const float alpha = d4[2 * j + 1][r];
-                const float a = tclamp(alpha, -3.f, 3.f);
-                const float e = exp_fast(-a);
-                const float xm = xv - d4[2 * j][r];
-                const float zr = xm * e;
-                const float gzr = nonfinite(zr) ? 0.f : gz;
-                const float ge = gzr * e;
-                *px = ge;
-                d4[2 * j][r] = -ge;                                          // δmu
-                const float ga = -(gzr * xm * e) - gld1s;
-                d4[2 * j + 1][r] = (alpha >= -3.f && alpha <= 3.f) ? ga : 0.f;  // δalpha
+                if constexpr (IAF) {
+                    // inverse_autoregressive_flow.py:39-54: y = x exp(clamp(a,-2,2)) + clamp(mu,-10,10),
+                    // y = finite ? y : x
+                    const float mu = d4[2 * j][r];
+                    const float a = tclamp(alpha, -2.f, 2.f);
+                    const float e = exp_fast(a);
+                    const float yr = xv * e + tclamp(mu, -10.f, 10.f);  // same expression as the forward kernel
+                    const bool bad = nonfinite(yr);
+                    const float gyr = bad ? 0.f : gz;
+                    *px = bad ? gz : gyr * e;
+                    d4[2 * j][r] = (mu >= -10.f && mu <= 10.f) ? gyr : 0.f;                    // δmu
+                    d4[2 * j + 1][r] = (alpha >= -2.f && alpha <= 2.f) ? gyr * xv * e + gld1s : 0.f;  // δalpha
+                } else {
+                    const float a = tclamp(alpha, -3.f, 3.f);
+                    const float e = exp_fast(-a);
+                    const float xm = xv - d4[2 * j][r];
+                    const float zr = xm * e;
+                    const float gzr = nonfinite(zr) ? 0.f : gz;
+                    const float ge = gzr * e;
+                    *px = ge;
+                    d4[2 * j][r] = -ge;                                          // δmu
+                    const float ga = -(gzr * xm * e) - gld1s;
+                    d4[2 * j + 1][r] = (alpha >= -3.f && alpha <= 3.f) ? ga : 0.f;  // δalpha
+                }
             }
         }
 
@@ -368,8 +384,9 @@ extern "C" size_t nfx_made_backward_factor_floats(int64_t B, int d, int H) {
 extern "C" int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,
                                         const float* grad_log_det, float* grad_in, float* factors,
                                         int64_t B, int d, int H, int variant, void* stream) {
-    if (variant != NFX_MAF_INVERSE)
-        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: only NFX_MAF_INVERSE (density training)");
+    if (variant != NFX_MAF_INVERSE && variant != NFX_IAF_FORWARD)
+        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: parallel directions only (NFX_MAF_INVERSE, "
+                                           "NFX_IAF_FORWARD); the sequential ones are nfx_made_seq_backward");
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine_backward: bad shape");
     if (d > 64 || H > 64)
         return set_error(NFX_EUNSUPPORTED, "made_affine_backward: d=%d H=%d outside d<=64, H<=64", d, H);
@@ -379,16 +396,18 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
     const size_t lds = (size_t)kBwdWaves * 2 * 32 * kTileStride * sizeof(float);
-    const void* k = HT == 1 ? (const void*)made_bwd_kernel<1> : (const void*)made_bwd_kernel<2>;
+    const bool iaf = variant == NFX_IAF_FORWARD;
+    const void* k = HT == 1 ? (iaf ? (const void*)made_bwd_kernel<1, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<1, NFX_MAF_INVERSE>)
+                            : (iaf ? (const void*)made_bwd_kernel<2, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<2, NFX_MAF_INVERSE>);
     int rc = prepare_lds(k, lds);
     if (rc) return rc;
     const int64_t ntiles = (B + 31) / 32;
     const int threads = 64 * kBwdWaves;
     const int grid = resident_grid(k, threads, lds, (ntiles + kBwdWaves - 1) / kBwdWaves);
     hipStream_t s = (hipStream_t)stream;
-    if (HT == 1)
-        made_bwd_kernel<1><<<grid, threads, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
-    else
-        made_bwd_kernel<2><<<grid, threads, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, ntiles);
+    typedef void (*bwd_t)(const float*, const float*, const float*, const float*, float*, float*, int64_t, int, int,
+                          int64_t);
+    reinterpret_cast<bwd_t>(const_cast<void*>(k))<<<grid, threads, lds, s>>>(packed, in, grad_out, grad_log_det, grad_in,
+                                                                          factors, B, d, H, ntiles);
     return check_launch("made_bwd_kernel");
 }

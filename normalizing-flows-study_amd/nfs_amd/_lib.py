@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
     "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_affine_backward",
-    "nfx_made_factor_pitch", "nfx_made_param_floats", "nfx_made_wgrad_workspace_bytes", "nfx_made_backward_weights",
+    "nfx_made_seq_backward", "nfx_made_factor_pitch", "nfx_made_param_floats", "nfx_made_wgrad_workspace_bytes", "nfx_made_backward_weights",
     "nfx_affine_train_pack_floats", "nfx_affine_train_stats_doubles", "nfx_affine_train_grad_doubles",
     "nfx_affine_train_param_floats", "nfx_affine_train_workspace_bytes", "nfx_affine_train_pack",
     "nfx_affine_train_stats", "nfx_affine_train_update_running", "nfx_affine_train_backward",
@@ -104,6 +104,7 @@ _SIGNATURES = {
     "nfx_made_pack_backward": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
     "nfx_made_backward_factor_floats": (_sz, [_i64, _int, _int]),
     "nfx_made_affine_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_made_seq_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_made_factor_pitch": (_i64, [_i64]),
     "nfx_made_param_floats": (_sz, [_int, _int]),
     "nfx_made_wgrad_workspace_bytes": (_sz, [_i64, _int, _int]),

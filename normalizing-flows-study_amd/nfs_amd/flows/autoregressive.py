@@ -151,14 +151,17 @@ class _MadeAffineFlow(HipFlow):
         packed._nfx_keep = keep
         return packed
 
-    # -- training: fused backward of the parallel density direction (§8(f) item 1) --------
+    # -- training: fused backward of every direction (§8(f) item 1) --------------------------
     def _hip_backward_ok(self, x, direction):
+        if x.dtype != torch.float32 or self.conditioner.batchnorms():
+            return False
         d, H = self.dim, self.conditioner.hidden_dim
-        return (self._variant(direction) == _lib.NFX_MAF_INVERSE and d <= 64 and H <= 64
-                and not self.conditioner.batchnorms() and x.dtype == torch.float32)
+        if self._variant(direction) in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD):
+            return d <= 64 and H <= 64  # made_bwd_kernel (parallel directions)
+        return d <= MAX_D and H <= MAX_H  # made_seq_bwd_kernel (sequential directions)
 
-    def _hip_backward(self, x, gz, gld, direction=-1):
-        """dL/dx and the parameter gradients (in self.parameters() order) of the inverse pass."""
+    def _hip_backward(self, x, gz, gld, direction):
+        """dL/dx and the parameter gradients (in self.parameters() order) of one call."""
         x = x.contiguous()
         B, d = x.shape
         H = self.conditioner.hidden_dim
@@ -168,16 +171,19 @@ class _MadeAffineFlow(HipFlow):
         L = _lib.lib()
         gx = torch.empty_like(x)
         fac = torch.empty(L.nfx_made_backward_factor_floats(B, d, H), device=x.device, dtype=torch.float32)
+        variant = self._variant(direction)
+        parallel = variant in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD)
         ev = BACKWARD_EVENTS
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        _lib.check(L.nfx_made_affine_backward(_lib.ptr(packed), _lib.ptr(x), _lib.ptr(gz), _lib.ptr(gld),
-                                              _lib.ptr(gx), _lib.ptr(fac), B, d, H, _lib.NFX_MAF_INVERSE,
-                                              _lib.stream_of(x)), "nfx_made_affine_backward")
+        fn = L.nfx_made_affine_backward if parallel else L.nfx_made_seq_backward
+        _lib.check(fn(_lib.ptr(packed), _lib.ptr(x), _lib.ptr(gz), _lib.ptr(gld), _lib.ptr(gx), _lib.ptr(fac),
+                      B, d, H, variant, _lib.stream_of(x)),
+                   "nfx_made_affine_backward" if parallel else "nfx_made_seq_backward")
         if ev is not None:
             e1.record()
-            ev.append(("made_bwd_kernel", e0, e1))
+            ev.append(("made_bwd_kernel" if parallel else "made_seq_bwd_kernel", e0, e1))
         return gx, self._weight_grads(fac, B)
 
     def _weight_grads(self, fac, B):
