@@ -191,7 +191,7 @@ int nfx_made_affine_backward(const float* packed, const float* in, const float* 
                              int d, int H, int variant, void* stream);
 
 /* MADE parameter gradients from the factors above (both MAF and IAF backward kernels write this
- * layout, rows of pitch nfx_made_factor_pitch(B) = B rounded up to 32): fp32 MFMA contractions
+ * layout, rows of pitch nfx_made_factor_pitch(B) = B): fp32 MFMA contractions
  * over the sample dimension, reduced in float64 in a fixed order (deterministic), written to
  * `grads` in MADE.parameters() order — net.0.weight [H,d], net.0.bias [H], net.2.weight [H,H],
  * net.2.bias, net.4.weight, net.4.bias, net.6.weight [2d,H], net.6.bias [2d] — each weight

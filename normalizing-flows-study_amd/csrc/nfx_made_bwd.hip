@@ -10,8 +10,8 @@
 // activations; gx = the epilogue's direct term + W1mᵀ δ1. The weight gradients are reductions
 // over the SAMPLE dimension (K = B), which the per-sample tile layout cannot contract without a
 // transpose per tile, so the kernel writes the per-sample factors feature-major (δ4ᵀ, δ3ᵀ, δ2ᵀ,
-// δ1ᵀ, h3ᵀ, h2ᵀ, h1ᵀ: coalesced 128-byte rows, one half-wave per feature row, row pitch
-// P = B rounded up to 32) and the weight gradients are MFMA sample contractions over them
+// δ1ᵀ, h3ᵀ, h2ᵀ, h1ᵀ: coalesced 128-byte rows, one half-wave per feature row, row pitch B)
+// and the weight gradients are MFMA sample contractions over them
 // (nfx_made_wgrad.hip: gW4 = δ4·h3ᵀ, …, gW1 = δ1·xᵀ), masked like the reference's weight*mask.
 //
 // Epilogue backward, per element (torch semantics of the reference ops):
@@ -63,19 +63,10 @@ __device__ __forceinline__ void store_fm(float* __restrict__ dst, const f32x16& 
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, (int)(((int64_t)nrows * P - base) * 4),
                                                       0x00020000);
     const int vo = base + col < B ? (int)((col + 4 * h * P) * 4) : (int)0xFFFFFFF0;
-    if (row0 + 32 <= nrows) {  // uniform: the whole tile is inside the block
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int rowu = row0 + (r & 3) + 8 * (r >> 2);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * P * 4), 0);
-        }
-    } else {  // last tile of a ragged block: rows past it belong to the next block
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int rowu = row0 + (r & 3) + 8 * (r >> 2);
-            if (rowu + 4 * h < nrows)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * P * 4), 0);
-        }
+    for (int r = 0; r < 16; ++r) {
+        const int rowu = row0 + (r & 3) + 8 * (r >> 2);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t[r]), rs, vo, (int)(rowu * P * 4), 0);
     }
 }
 
@@ -131,7 +122,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     // feature-major factors: [d4 (2d) | d3 | d2 | d1 (H each) | h3, 1 | h2, 1 | h1, 1 (H+1 each) |
     // x, 1 (d+1)] rows x B — the trailing ones rows turn each weight-gradient GEMM into the
     // bias gradient as well (its last column)
-    const int64_t P = (B + 31) & ~(int64_t)31;  // factor row pitch (nfx_made_factor_pitch)
+    const int64_t P = B;  // factor row pitch (nfx_made_factor_pitch)
     float* D4 = acts;
     float* D3 = D4 + (int64_t)2 * d * P;
     float* D2 = D3 + (int64_t)H * P;
@@ -361,6 +352,257 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     }
 }
 
+
+// ---- general shapes: any d (<= 4096), H <= 128 (made_bwdw_kernel) ---------------------------
+// Same math as made_bwd_kernel, for the shapes whose [32 x d] x tile does not fit a wave's LDS
+// (e.g. the IAF(784, 64) sampling direction under autograd): the input layer streams x through a
+// [32 x 32] LDS stage per 32-dimension chunk; the output layer runs per (mu, alpha) block pair j
+// in two passes — pass A only sums clamp(alpha) (the log-det clamp decides every block's
+// gradient), pass B recomputes the block, runs the epilogue backward on the staged x / gz chunk,
+// writes the direct dL/dx term of the chunk, the block's δ rows, and folds δ into the layer-3
+// adjoint at once (gh3 += W4mᵀ δ_j, MFMA); after the hidden chain, gx += W1mᵀ δ1 is added per
+// input chunk (read-modify-write of the wave's own gx rows).
+constexpr int kBwdwWaves = 4;
+constexpr int kS32 = 33;  // [32 samples][33] stage stride (conflict-free column reads)
+
+__device__ __forceinline__ void stage32_in(const float* __restrict__ src, int64_t base, int d, int64_t B, int dim0,
+                                           float* st) {
+    const int lane = lane_id();
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int idx = i * 64 + lane, sm = idx >> 5, dd = idx & 31;
+        const int64_t row = base + sm;
+        const int dim = dim0 + dd;
+        st[sm * kS32 + dd] = (row < B && dim < d) ? src[row * d + dim] : 0.f;
+    }
+}
+
+__device__ __forceinline__ void stage32_out(float* __restrict__ dst, int64_t base, int d, int64_t B, int dim0,
+                                            const float* st) {
+    const int lane = lane_id();
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+        const int idx = i * 64 + lane, sm = idx >> 5, dd = idx & 31;
+        const int64_t row = base + sm;
+        const int dim = dim0 + dd;
+        if (row < B && dim < d) dst[row * d + dim] = st[sm * kS32 + dd];
+    }
+}
+
+template <int HT, int VAR>
+__global__ __launch_bounds__(64 * kBwdwWaves) void made_bwdw_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, const float* __restrict__ gout,
+    const float* __restrict__ gld_in, float* __restrict__ gin, float* __restrict__ acts, int64_t B, int d,
+    int H, int64_t ntiles) {
+    const MadeLayout L = made_layout(d, HT);
+    constexpr bool IAF = VAR == NFX_IAF_FORWARD;
+    constexpr float ALO = IAF ? -2.f : -3.f, AHI = IAF ? 2.f : 3.f, LDLIM = IAF ? 50.f : 100.f;
+    extern __shared__ f32x4 lds4[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* xt = reinterpret_cast<float*>(lds4) + wave * 2 * 32 * kS32;
+    float* gt = xt + 32 * kS32;
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int NKC = L.NKC, NJ = L.NJ;
+    const int64_t P = B;  // factor row pitch (nfx_made_factor_pitch)
+    float* D4 = acts;
+    float* D3 = D4 + (int64_t)2 * d * P;
+    float* D2 = D3 + (int64_t)H * P;
+    float* D1 = D2 + (int64_t)H * P;
+    float* H3 = D1 + (int64_t)H * P;
+    float* H2 = H3 + (int64_t)(H + 1) * P;
+    float* H1 = H2 + (int64_t)(H + 1) * P;
+    float* X1 = H1 + (int64_t)(H + 1) * P;
+
+    for (int64_t t = (int64_t)blockIdx.x * kBwdwWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kBwdwWaves) {
+        const int64_t base = t * 32;
+        const float* Wf = packed + opaque_zero();
+        const bool live = base + col < B;
+        // ---- layer 1 over 32-dimension chunks of x (x rows also written feature-major) ----
+        f32x16 h1[HT];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(Wf + L.b1 + ht * 32, h);
+        for (int kc = 0; kc < NKC; ++kc) {
+            wave_lds_sync();
+            stage32_in(in, base, d, B, 32 * kc, xt);
+            wave_lds_sync();
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+#pragma unroll
+                for (int ht = 0; ht < HT; ++ht) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(Wf + L.w1 + ((ht * 4 * NKC + kc * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) h1[ht] = mfma32(w[rr], xt[col * kS32 + 8 * g + 2 * rr + h], h1[ht]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int dim = 32 * kc + 2 * i + h;
+                if (live && dim < d) X1[(int64_t)dim * P + base + col] = xt[col * kS32 + 2 * i + h];
+            }
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
+        f32x16 h2[HT], h3[HT];
+        made_hidden1<HT>(Wf, L.w2, L.b2, h1, h2);
+        uint32_t m1[HT], m2[HT], m3[HT];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            m1[ht] = 0u;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) m1[ht] |= (h1[ht][r] > 0.f ? 1u : 0u) << r;
+            store_fm(H1, h1[ht], 32 * ht, H, B, P, base);
+        }
+        made_hidden1<HT>(Wf, L.w3, L.b3, h2, h3);
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            m2[ht] = m3[ht] = 0u;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                m2[ht] |= (h2[ht][r] > 0.f ? 1u : 0u) << r;
+                m3[ht] |= (h3[ht][r] > 0.f ? 1u : 0u) << r;
+            }
+            store_fm(H2, h2[ht], 32 * ht, H, B, P, base);
+            store_fm(H3, h3[ht], 32 * ht, H, B, P, base);
+        }
+
+        // ---- pass A: the log-det sum (alpha rows only) ----
+        float asum0 = 0.f;
+        for (int j = 0; j < NJ; ++j) {
+            f32x16 al = load_bias16(Wf + L.b4 + (j * 2 + 1) * 32, h);
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 wa = *reinterpret_cast<const f32x4*>(Wf + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) al = mfma32(wa[rr], h3[kt][4 * rq + rr], al);
+                }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) asum0 = asum0 + tclamp(al[r], ALO, AHI);
+        }
+        const float ssum = halves_sum(asum0, asum0);
+        const float ldraw = IAF ? ssum : -ssum;
+        const float gld = (lane < 32 && live) ? gld_in[base + col] : 0.f;
+        float gld1 = nonfinite(ldraw) ? 0.f : gld;
+        const float ld1 = nonfinite(ldraw) ? 0.f : ldraw;
+        if (!(ld1 >= -LDLIM && ld1 <= LDLIM)) gld1 = 0.f;
+        const float gld1s = __shfl(gld1, col, 64);
+
+        // ---- pass B: per output block, epilogue backward + gh3 accumulation ----
+        f32x16 g3[HT];
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) g3[ot] = f32x16{};
+        for (int j = 0; j < NJ; ++j) {
+            f32x16 mu = load_bias16(Wf + L.b4 + (j * 2 + 0) * 32, h);
+            f32x16 al = load_bias16(Wf + L.b4 + (j * 2 + 1) * 32, h);
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 wm = *reinterpret_cast<const f32x4*>(Wf + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                    const f32x4 wa = *reinterpret_cast<const f32x4*>(Wf + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        mu = mfma32(wm[rr], h3[kt][4 * rq + rr], mu);
+                        al = mfma32(wa[rr], h3[kt][4 * rq + rr], al);
+                    }
+                }
+            wave_lds_sync();
+            stage32_in(in, base, d, B, 32 * j, xt);
+            stage32_in(gout, base, d, B, 32 * j, gt);
+            wave_lds_sync();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int dd = crow(r, h);
+                float* px = xt + col * kS32 + dd;
+                const float xv = *px;
+                const float gz = gt[col * kS32 + dd];
+                const float alpha = al[r];
+                if constexpr (IAF) {
+                    const float m = mu[r];
+                    const float a = tclamp(alpha, -2.f, 2.f);
+                    const float e = exp_fast(a);
+                    const float yr = xv * e + tclamp(m, -10.f, 10.f);
+                    const bool bad = nonfinite(yr);
+                    const float gyr = bad ? 0.f : gz;
+                    *px = bad ? gz : gyr * e;
+                    mu[r] = (m >= -10.f && m <= 10.f) ? gyr : 0.f;
+                    al[r] = (alpha >= -2.f && alpha <= 2.f) ? gyr * xv * e + gld1s : 0.f;
+                } else {
+                    const float a = tclamp(alpha, -3.f, 3.f);
+                    const float e = exp_fast(-a);
+                    const float xm = xv - mu[r];
+                    const float zr = xm * e;
+                    const float gzr = nonfinite(zr) ? 0.f : gz;
+                    const float ge = gzr * e;
+                    *px = ge;
+                    mu[r] = -ge;
+                    al[r] = (alpha >= -3.f && alpha <= 3.f) ? -(gzr * xm * e) - gld1s : 0.f;
+                }
+            }
+            wave_lds_sync();
+            stage32_out(gin, base, d, B, 32 * j, xt);  // direct dL/dx term of the chunk
+            store_fm(D4, mu, 32 * j, d, B, P, base);
+            store_fm(D4 + (int64_t)d * P, al, 32 * j, d, B, P, base);
+#pragma unroll
+            for (int ot = 0; ot < HT; ++ot) {
+#pragma unroll
+                for (int which = 0; which < 2; ++which) {
+                    const f32x16& dl = which ? al : mu;
+#pragma unroll
+                    for (int rq = 0; rq < 4; ++rq) {
+                        const f32x4 w = *reinterpret_cast<const f32x4*>(
+                            Wf + L.t4 + (((ot * 2 * NJ + 2 * j + which) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) g3[ot] = mfma32(w[rr], dl[4 * rq + rr], g3[ot]);
+                    }
+                }
+            }
+        }
+        // ---- hidden chain ----
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) g3[ot][r] = ((m3[ot] >> r) & 1u) ? g3[ot][r] : 0.f;
+            store_fm(D3, g3[ot], 32 * ot, H, B, P, base);
+        }
+        f32x16 g2[HT];
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) {
+            f32x16 acc = chain_gmem<HT>(Wf + L.t3, ot, HT, g3, f32x16{});
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = ((m2[ot] >> r) & 1u) ? acc[r] : 0.f;
+            g2[ot] = acc;
+            store_fm(D2, acc, 32 * ot, H, B, P, base);
+        }
+#pragma unroll
+        for (int ot = 0; ot < HT; ++ot) {
+            f32x16 acc = chain_gmem<HT>(Wf + L.t2, ot, HT, g2, f32x16{});
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = ((m1[ot] >> r) & 1u) ? acc[r] : 0.f;
+            g3[ot] = acc;  // δ1
+            store_fm(D1, acc, 32 * ot, H, B, P, base);
+        }
+        // ---- gx += W1mᵀ δ1 per input chunk ----
+        for (int kc = 0; kc < NKC; ++kc) {
+            const f32x16 gx = chain_gmem<HT>(Wf + L.t1, kc, HT, g3, f32x16{});
+            wave_lds_sync();
+            stage32_in(gin, base, d, B, 32 * kc, xt);
+            wave_lds_sync();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float* px = xt + col * kS32 + crow(r, h);
+                *px = *px + gx[r];
+            }
+            wave_lds_sync();
+            stage32_out(gin, base, d, B, 32 * kc, xt);
+        }
+        wave_lds_sync();
+    }
+}
+
 }  // namespace nfx
 
 using namespace nfx;
@@ -378,7 +620,7 @@ extern "C" int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float*
 
 extern "C" size_t nfx_made_backward_factor_floats(int64_t B, int d, int H) {
     if (B < 0 || d <= 0 || H <= 0) return 0;
-    return (size_t)((B + 31) & ~(int64_t)31) * (size_t)(3 * d + 6 * H + 4);
+    return (size_t)B * (size_t)(3 * d + 6 * H + 4);
 }
 
 extern "C" int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,
@@ -388,12 +630,30 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
         return set_error(NFX_EUNSUPPORTED, "made_affine_backward: parallel directions only (NFX_MAF_INVERSE, "
                                            "NFX_IAF_FORWARD); the sequential ones are nfx_made_seq_backward");
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine_backward: bad shape");
-    if (d > 64 || H > 64)
-        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: d=%d H=%d outside d<=64, H<=64", d, H);
+    if (d > 4096 || H > 128)
+        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: d=%d H=%d outside d<=4096, H<=128", d, H);
     if (B == 0) return NFX_OK;
     if (!packed || !in || !grad_out || !grad_log_det || !grad_in || !factors)
         return set_error(NFX_EINVAL, "made_affine_backward: null pointer");
     const int HT = (H + 31) / 32;
+    if (d > 64 || H > 64) {  // general shapes: x streamed in 32-dimension chunks
+        typedef void (*bwdw_t)(const float*, const float*, const float*, const float*, float*, float*, int64_t, int,
+                               int, int64_t);
+        const bool iaf = variant == NFX_IAF_FORWARD;
+        bwdw_t kw = nullptr;
+        switch (HT) {
+            case 1: kw = iaf ? made_bwdw_kernel<1, NFX_IAF_FORWARD> : made_bwdw_kernel<1, NFX_MAF_INVERSE>; break;
+            case 2: kw = iaf ? made_bwdw_kernel<2, NFX_IAF_FORWARD> : made_bwdw_kernel<2, NFX_MAF_INVERSE>; break;
+            case 3: kw = iaf ? made_bwdw_kernel<3, NFX_IAF_FORWARD> : made_bwdw_kernel<3, NFX_MAF_INVERSE>; break;
+            default: kw = iaf ? made_bwdw_kernel<4, NFX_IAF_FORWARD> : made_bwdw_kernel<4, NFX_MAF_INVERSE>; break;
+        }
+        const size_t ldsw = (size_t)kBwdwWaves * 2 * 32 * kS32 * sizeof(float);
+        const int64_t nt = (B + 31) / 32;
+        const int gw = resident_grid((const void*)kw, 64 * kBwdwWaves, ldsw, (nt + kBwdwWaves - 1) / kBwdwWaves);
+        kw<<<gw, 64 * kBwdwWaves, ldsw, (hipStream_t)stream>>>(packed, in, grad_out, grad_log_det, grad_in, factors, B,
+                                                                d, H, nt);
+        return check_launch("made_bwdw_kernel");
+    }
     const MadeLayout L = made_layout(d, HT);
     const size_t lds = (size_t)kBwdWaves * 2 * 32 * kTileStride * sizeof(float);
     const bool iaf = variant == NFX_IAF_FORWARD;

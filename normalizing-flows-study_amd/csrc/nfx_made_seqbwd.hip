@@ -20,7 +20,7 @@
 // adjoints in wave-private LDS rows.
 //
 // Outputs: grad_in [B, d] and the feature-major factors of nfx_made_backward_weights (rows of
-// pitch P = nfx_made_factor_pitch(B)): D4 = (δμ | δα), D3/D2/D1 = the ReLU'-gated hidden
+// pitch nfx_made_factor_pitch(B) = B): D4 = (δμ | δα), D3/D2/D1 = the ReLU'-gated hidden
 // adjoints, H3/H2/H1 = the hidden activations at zs, X1 = zs (the MADE input). The D4 rows hold
 // the raw (μ, α) of the forward sweep until the reverse sweep overwrites them.
 //
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64) void made_seq_bwd_kernel(const float* __restric
     const bool valid = s < B;
     const int64_t sv = valid ? s : 0;
     const float* P = packed;
-    const int64_t Pt = (B + 31) & ~(int64_t)31;
+    const int64_t Pt = B;  // factor row pitch (nfx_made_factor_pitch)
     float* D4 = fac;
     float* D3 = D4 + (int64_t)2 * d * Pt;
     float* D2 = D3 + (int64_t)H * Pt;

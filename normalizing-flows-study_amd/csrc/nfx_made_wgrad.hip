@@ -3,15 +3,15 @@
 //   dW = (δ · aᵀ) ⊙ mask,  db = Σ_samples δ
 // (the gradient of F.linear(a, W * mask, b), masked_linear.py:14-18, made.py:81-134), with δ the
 // layer's output gradient and a its input, both per sample. The backward kernels
-// (nfx_made_bwd.hip, nfx_made_iaf_bwd.hip) write δ and a FEATURE-MAJOR, [rows x P] with a
-// sample pitch P = nfx_made_factor_pitch(B) (a multiple of 32, so every 32-sample step of a row
-// is one aligned 128-byte segment):
+// (nfx_made_bwd.hip, nfx_made_seqbwd.hip) write δ and a FEATURE-MAJOR, [rows x P] with a
+// sample pitch P = nfx_made_factor_pitch(B) = B:
 //   D4 (2d) | D3 (H) | D2 (H) | D1 (H) | H3 (H+1) | H2 (H+1) | H1 (H+1) | X1 (d+1)
 // (the +1 rows are unused here; the bias gradients are row sums of δ).
 //
 // Contraction kernel: the sample dimension is the MFMA k dimension. A task = (sample chunk,
 // 32x32 output tile of one layer); lane (i, kh) of the wave loads 16 consecutive samples of
-// δ row i and of a row i (two 64-byte reads that, with the other lane half, cover the step's
+// δ row i and of a row i (four 16-byte reads when the pitch keeps rows 16-byte aligned, i.e.
+// B % 4 == 0, else sixteen 4-byte reads; with the other lane half they cover the step's
 // 128-byte segment) and feeds them as 16 v_mfma_f32_32x32x2_f32 k-steps — the k index of an
 // MFMA is a sample, and both operands agree on which, so no transpose is ever needed. The bias
 // sums ride along as lane-local adds of the δ values the tile already holds (column tile 0).
@@ -47,6 +47,7 @@ __device__ __forceinline__ int wg_layer_of(const WgArgs& a, int t) {
     return k;
 }
 
+template <bool VEC4>
 __global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int64_t B, int64_t P, int64_t chunk,
                                                                    int64_t ntasks, int blocks_per_xcd, float* part) {
     // undo the hardware's round robin of consecutive workgroups over the 8 XCDs
@@ -82,10 +83,16 @@ __global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int
     float bsum = 0.f;
     int64_t s = s0;
     // full 32-sample steps, two per iteration with the next pair's loads in flight
-#define load16(r, st, v)                                                                             \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                  \
-        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, vo, (int)((st) * 4) + 16 * q, 0);    \
-        v[q] = f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3])}; \
+#define load16(r, st, v)                                                                                   \
+    if constexpr (VEC4) {                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                    \
+            const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, vo, (int)((st) * 4) + 16 * q, 0);      \
+            v[q] = f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),             \
+                         __uint_as_float(u[3])};                                                           \
+        }                                                                                                  \
+    } else {                                                                                               \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) _Pragma("unroll") for (int e = 0; e < 4; ++e)        \
+            v[q][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, (int)((st) * 4) + 16 * q + 4 * e, 0)); \
     }
     const int64_t full_end = s0 + ((s1 - s0) / 32) * 32;
     if (s < full_end) {
@@ -228,7 +235,7 @@ static WgArgs wg_args(const float* factors, int64_t P, int d, int H, const float
 
 using namespace nfx;
 
-extern "C" int64_t nfx_made_factor_pitch(int64_t B) { return B <= 0 ? 0 : (B + 31) & ~(int64_t)31; }
+extern "C" int64_t nfx_made_factor_pitch(int64_t B) { return B <= 0 ? 0 : B; }
 
 extern "C" size_t nfx_made_wgrad_workspace_bytes(int64_t B, int d, int H) {
     if (B <= 0 || d <= 0 || H <= 0) return 0;
@@ -269,7 +276,10 @@ extern "C" int nfx_made_backward_weights(const float* factors, int64_t B, int d,
     float* part = reinterpret_cast<float*>(workspace);
     double* sums = reinterpret_cast<double*>(
         reinterpret_cast<char*>(workspace) + ((nch * len * sizeof(float) + 255) & ~(size_t)255));
-    made_wgrad_kernel<<<8 * bpx, 64 * kWgWaves, 0, s>>>(a, B, P, chunk, ntasks, bpx, part);
+    if (P % 4 == 0)
+        made_wgrad_kernel<true><<<8 * bpx, 64 * kWgWaves, 0, s>>>(a, B, P, chunk, ntasks, bpx, part);
+    else
+        made_wgrad_kernel<false><<<8 * bpx, 64 * kWgWaves, 0, s>>>(a, B, P, chunk, ntasks, bpx, part);
     int rc = check_launch("made_wgrad_kernel");
     if (rc) return rc;
     if ((rc = train_sum_finish(part, (int)nch, (int)len, sums, s))) return rc;

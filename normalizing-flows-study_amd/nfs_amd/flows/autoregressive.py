@@ -156,9 +156,9 @@ class _MadeAffineFlow(HipFlow):
         if x.dtype != torch.float32 or self.conditioner.batchnorms():
             return False
         d, H = self.dim, self.conditioner.hidden_dim
-        if self._variant(direction) in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD):
-            return d <= 64 and H <= 64  # made_bwd_kernel (parallel directions)
-        return d <= MAX_D and H <= MAX_H  # made_seq_bwd_kernel (sequential directions)
+        # parallel directions: made_bwd_kernel (d, H <= 64) / made_bwdw_kernel; sequential
+        # directions: made_seq_bwd_kernel
+        return d <= MAX_D and H <= MAX_H
 
     def _hip_backward(self, x, gz, gld, direction):
         """dL/dx and the parameter gradients (in self.parameters() order) of one call."""

@@ -128,6 +128,9 @@ def _close_or_ref(g, g64, g32, tol, what):
     ("iaf", -1, 7, 128, 100), ("iaf", -1, 784, 64, 6),
     ("maf", 1, 5, 16, 77), ("maf", 1, 20, 64, 300), ("maf", 1, 9, 128, 65),
     ("iaf", 1, 5, 16, 1), ("iaf", 1, 33, 32, 1000), ("iaf", 1, 63, 64, 2048), ("iaf", 1, 2, 64, 500),
+    # general-shape parallel kernel (made_bwdw_kernel): d > 64 or H > 64
+    ("maf", -1, 100, 64, 300), ("maf", -1, 20, 128, 257), ("maf", -1, 63, 96, 513), ("iaf", 1, 784, 64, 100),
+    ("iaf", 1, 65, 32, 31), ("maf", -1, 130, 128, 64),
 ])
 def test_all_directions_backward_vs_float64_autograd(cuda_device, kind, direction, d, H, B):
     """Fused backward of each MADE direction (nfx_made_affine_backward for the parallel ones,
