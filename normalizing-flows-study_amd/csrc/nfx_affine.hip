@@ -59,10 +59,19 @@ __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float
                 int t = o - L.b2, r = t & 15, h = (t >> 4) & 1, ht = t >> 5;
                 int row = 32 * ht + crow(r, h);
                 v = row < H ? mlp_bias(P, 1, row) : 0.f;
+            } else if (o < L.b3 && d > 8) {  // MFMA A-operand tiles of the output layer
+                int t = o - L.w3, rr = t & 3, lane = (t >> 2) & 63, rq = (t >> 8) & 3;
+                int kt = (t >> 10) % HT, j = (t >> 10) / HT;
+                int row = 32 * j + (lane & 31), col = 32 * kt + crow(4 * rq + rr, lane >> 5);
+                v = (row < d && col < H) ? mlp_weight(P, 2, H, row, col) : 0.f;
             } else if (o < L.b3) {
                 int t = o - L.w3, r = t & 15, h = (t >> 4) & 1, ht = (t >> 5) % HT, j = (t >> 5) / HT;
                 int col = 32 * ht + crow(r, h);
                 v = col < H ? mlp_weight(P, 2, H, j, col) : 0.f;
+            } else if (d > 8) {  // output bias in accumulator order
+                int t = o - L.b3, r = t & 15, h = (t >> 4) & 1, j = t >> 5;
+                int row = 32 * j + crow(r, h);
+                v = row < d ? mlp_bias(P, 2, row) : 0.f;
             } else {
                 int j = o - L.b3;
                 v = j < d ? mlp_bias(P, 2, j) : 0.f;
@@ -105,6 +114,40 @@ static std::atomic<int>& affine_policy() {
     return v;
 }
 
+typedef void (*affine_wide_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t, float*,
+                              double*, float);
+
+template <int HT>
+static affine_wide_t wide_pick(int dir, bool logp) {
+    if (dir > 0) return affine_wide_kernel<HT, 1, false>;
+    return logp ? affine_wide_kernel<HT, -1, true> : affine_wide_kernel<HT, -1, false>;
+}
+
+static int affine_wide_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d,
+                              int H, int direction, int accumulate, float* logp, double* sums, void* workspace,
+                              hipStream_t stream) {
+    const bool fused = sums != nullptr;
+    const int HT = (H + 31) / 32;
+    if (d > 64 || HT > 4)
+        return set_error(NFX_EUNSUPPORTED, "affine_coupling: d=%d H=%d outside the compiled family (d<=64, H<=128)", d, H);
+    affine_wide_t k = HT == 1 ? wide_pick<1>(direction, fused)
+                      : HT == 2 ? wide_pick<2>(direction, fused)
+                      : HT == 3 ? wide_pick<3>(direction, fused) : wide_pick<4>(direction, fused);
+    if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, stream) : NFX_OK;
+    if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "affine_coupling: null pointer");
+    if (in == out) return set_error(NFX_EINVAL, "affine_coupling: in and out must not alias");
+    const size_t lds = (size_t)kWideWaves * 32 * (d | 1) * sizeof(float);
+    const int64_t ntiles = (B + 31) / 32;
+    int grid = resident_grid((const void*)k, 64 * kWideWaves, lds, (ntiles + kWideWaves - 1) / kWideWaves);
+    if (grid > kMaxPartials) grid = kMaxPartials;
+    double* partials = reinterpret_cast<double*>(workspace);
+    k<<<grid, 64 * kWideWaves, lds, stream>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials,
+                                              gauss_const(d));
+    int rc = check_launch("affine_wide_kernel");
+    if (rc || !fused) return rc;
+    return gauss_finish(partials, grid, sums, B, stream);
+}
+
 static int affine_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
                          int d, int H, int direction, int accumulate, float* logp, double* sums,
                          void* workspace, hipStream_t stream) {
@@ -114,8 +157,10 @@ static int affine_launch(const float* packed, const float* in, float* out, float
         return set_error(NFX_EINVAL, "affine_coupling: direction must be +1 or -1");
     if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "affine_coupling_logprob: null logp/workspace");
     const int HT = (H + 31) / 32;
+    if (d > 8) return affine_wide_launch(packed, in, out, log_det, B, d, H, direction, accumulate, logp, sums,
+                                         workspace, stream);
     affine_kernel_t k = pick_affine(HT, d, direction, fused);
-    if (!k) return set_error(NFX_EUNSUPPORTED, "affine_coupling: d=%d H=%d outside the compiled family (d<=8, H<=128)", d, H);
+    if (!k) return set_error(NFX_EUNSUPPORTED, "affine_coupling: d=%d H=%d outside the compiled family (d<=64, H<=128)", d, H);
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, stream) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "affine_coupling: null pointer");
     if (in == out) return set_error(NFX_EINVAL, "affine_coupling: in and out must not alias");

@@ -13,8 +13,10 @@ __host__ __device__ constexpr int up4(int v) { return (v + 3) & ~3; }
 //   b1 [HT][2][16]          bias of layer 1 at accumulator register r of half h (BN folded)
 //   w2 [HT][HT][4][64][4]   A operand of layer 2: [out tile][k tile][r/4][lane][r%4]
 //   b2 [HT][2][16]
-//   w3 [d][HT][2][16]       output layer, by (j, k tile, half, r) for the VALU dot
+//   w3 [d][HT][2][16]       output layer, by (j, k tile, half, r) for the VALU dot    (d <= 8)
 //   b3 [up4(d)]
+//   w3 [NJ][HT][4][64][4]   output layer as MFMA A-operand tiles, NJ = ceil(d/32)     (d > 8)
+//   b3 [NJ][2][16]          its bias in accumulator order
 // then mask [up4(d)].
 struct AffineLayout {
     int d, HT, KS1;
@@ -31,8 +33,14 @@ __host__ __device__ constexpr AffineLayout affine_layout(int d, int HT) {
     L.b1 = o; o += HT * 32;
     L.w2 = o; o += HT * HT * 16 * 64;
     L.b2 = o; o += HT * 32;
-    L.w3 = o; o += d * HT * 32;
-    L.b3 = o; o += up4(d);
+    if (d <= 8) {  // VALU output layer (affine_coupling_kernel)
+        L.w3 = o; o += d * HT * 32;
+        L.b3 = o; o += up4(d);
+    } else {       // MFMA output layer (affine_wide_kernel): A-operand tiles + accumulator-order bias
+        const int NJ = (d + 31) / 32;
+        L.w3 = o; o += NJ * HT * 1024;
+        L.b3 = o; o += NJ * 32;
+    }
     L.net = o;
     L.mask = 2 * o;
     L.total = 2 * o + up4(d);
@@ -265,6 +273,149 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
     if constexpr (LOGP) {
         const double t = block_sum_f64<256>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
+    }
+}
+
+
+// ---- wide coupling layers (8 < d <= 64, e.g. UCI-shaped RealNVP d = 43 / 63) -------------------
+// A wave owns a 32-sample tile whose [32 x d] x block sits in a wave-private LDS tile (odd row
+// stride, conflict-free column reads), loaded and stored row by row with coalesced accesses.
+// Layer 1 (K = d) reads its B operands (x * mask) from the tile, layers 2 and 3 (H -> d, one
+// 32-row MFMA tile per 32 output dims) keep activations in accumulator registers, and the
+// affine epilogue runs in accumulator layout on the tile in place. Weights (both nets) are
+// read from L2 (up to ~260 KB at H = 128, beyond LDS).
+constexpr int kWideWaves = 4;
+
+template <int HT>
+__device__ __forceinline__ void wide_net(const float* __restrict__ P, const AffineLayout& L, const float* xt, int S,
+                                         const float* __restrict__ mask, int d, f32x16 (&res)[2]) {
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    f32x16 h1[HT];
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(P + L.b1 + ht * 32, h);
+    for (int ks = 0; ks < L.KS1; ++ks) {
+        const int k = 2 * ks + h;
+        const float xb = k < d ? xt[col * S + k] * mask[k] : 0.f;
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) h1[ht] = mfma32(P[L.w1 + (ht * L.KS1 + ks) * 64 + lane], xb, h1[ht]);
+    }
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
+    f32x16 h2[HT];
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a = load_bias16(P + L.b2 + hto * 32, h);
+#pragma unroll
+        for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h1[kt][4 * rq + rr], a);
+            }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+        h2[hto] = a;
+    }
+    const int NJ = (d + 31) / 32;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (j < NJ) {
+            f32x16 a = load_bias16(P + L.b3 + j * 32, h);
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(P + L.w3 + (((j * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h2[kt][4 * rq + rr], a);
+                }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = tclamp(a[r], -10.f, 10.f);
+            res[j] = a;
+        } else {
+            res[j] = f32x16{};
+        }
+    }
+}
+
+template <int HT, int DIR, bool LOGP>
+__global__ __launch_bounds__(64 * kWideWaves) void affine_wide_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles,
+    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    const AffineLayout L = affine_layout(d, HT);
+    const int S = d | 1;
+    extern __shared__ f32x4 lds4[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* xt = reinterpret_cast<float*>(lds4) + wave * 32 * S;
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const float* mask = packed + L.mask;
+    double lpacc = 0.0;
+    for (int64_t t = (int64_t)blockIdx.x * kWideWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kWideWaves) {
+        const int64_t base = t * 32;
+        const int rows = (int)(B - base < 32 ? B - base : 32);
+        const float* src = in + base * d;
+        for (int i = lane; i < 32 * d; i += 64) {
+            const int r = i / d, c = i - r * d;
+            xt[r * S + c] = r < rows ? src[i] : 0.f;
+        }
+        const float ldin = (accumulate && lane < rows) ? logdet[base + lane] : 0.f;
+        wave_lds_sync();
+        const float* Pw = packed + opaque_zero();
+        f32x16 sv[2], bv[2];
+        wide_net<HT>(Pw, L, xt, S, mask, d, sv);
+        wide_net<HT>(Pw + L.net, L, xt, S, mask, d, bv);
+        float ldp = 0.f;
+        {
+#pragma clang fp contract(off)  // separate mul/add roundings, as the reference's torch ops
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int dim = 32 * j + crow(r, h);
+                    if (dim < d) {
+                        float* px = xt + col * S + dim;
+                        const float xv = *px, m = mask[dim], om = 1.f - m;
+                        float tv;
+                        if constexpr (DIR < 0) {
+                            tv = (xv - bv[j][r]) * exp_fast(-sv[j][r]);
+                            ldp = ldp + om * (-sv[j][r]);
+                        } else {
+                            tv = xv * exp_fast(sv[j][r]) + bv[j][r];
+                            ldp = ldp + om * sv[j][r];
+                        }
+                        const float v = xv * m + om * tv;
+                        *px = nonfinite(v) ? 0.f : v;
+                    }
+                }
+        }
+        float ld = halves_sum(ldp, ldp);  // lanes 0..31: sample col
+        if (nonfinite(ld)) ld = 0.f;
+        wave_lds_sync();
+        float* dst = out + base * d;
+        for (int i = lane; i < rows * d; i += 64) {
+            const int r = i / d, c = i - r * d;
+            dst[i] = xt[r * S + c];
+        }
+        if (lane < rows) {
+            const float ldt = accumulate ? ldin + ld : ld;
+            logdet[base + lane] = ldt;
+            if constexpr (LOGP) {
+                float m = gauss_sq0(xt[lane * S]);
+                for (int c = 1; c < d; ++c) m = gauss_sq(m, xt[lane * S + c]);
+                const float lp = gauss_lp(m, cgauss, ldt);
+                logp[base + lane] = lp;
+                lpacc += (double)lp;
+            }
+        }
+        wave_lds_sync();
+    }
+    if constexpr (LOGP) {
+        const double tsum = block_sum_f64<64 * kWideWaves>(lpacc);
+        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
     }
 }
 

@@ -87,6 +87,14 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
+__device__ __forceinline__ void wave_lds_sync() {
+    // A wave's DS operations execute in order; this only stops the compiler from moving LDS
+    // accesses across the point (the tile is wave-private, no workgroup barrier needed).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Workgroup sum of a float64 (NT threads, wave64 shuffles then one LDS hop). Result valid in
 // thread 0. Deterministic order.
 template <int NT>

@@ -148,13 +148,6 @@ __device__ __forceinline__ void stage_out(float* __restrict__ out, int64_t base,
     }
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-    // A wave's DS operations execute in order; this only stops the compiler from moving LDS
-    // accesses across the point (the tile is wave-private, no workgroup barrier needed).
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int HT>
 __device__ __forceinline__ void made_hidden(const float* __restrict__ W, int woff, int boff,

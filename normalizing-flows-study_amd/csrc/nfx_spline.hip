@@ -25,7 +25,8 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
         float v = 0.f;
         if (i < L.b1) {
-            int t = i - L.w1, lane = t & 63, ks = (t >> 6) & 3, ht = t >> 8;
+            const int KS = spline_ks1(d);
+            int t = i - L.w1, lane = t & 63, ks = (t >> 6) % KS, ht = (t >> 6) / KS;
             int row = 32 * ht + (lane & 31), col = 2 * ks + (lane >> 5);
             v = (row < H && col < d) ? mlp_weight(net, 0, d, row, col) : 0.f;
         } else if (i < L.w2) {
@@ -67,6 +68,15 @@ __global__ void spline_pack_kernel(NfxMlpRaw net, const float* mask, int d, int 
 }
 
 static spline_kernel_t pick_spline(int HT, int K, int dir, bool logp, int d) {
+    if (d > 8) {
+        switch (HT) {
+            case 1: return spline_wide_pick_ht<1>(K, dir, logp);
+            case 2: return spline_wide_pick_ht<2>(K, dir, logp);
+            case 3: return spline_wide_pick_ht<3>(K, dir, logp);
+            case 4: return spline_wide_pick_ht<4>(K, dir, logp);
+            default: return nullptr;
+        }
+    }
     if (d == 2) {
         switch (HT) {
             case 1: return spline_pick_ht<1, 2>(K, dir, logp);
@@ -97,8 +107,8 @@ extern "C" size_t nfx_spline_packed_floats(int d, int H, int K) {
 extern "C" int nfx_spline_pack(const NfxMlpRaw* net, const float* mask, int d, int H, int K,
                                float* packed, void* stream) {
     if (!net || !mask || !packed) return set_error(NFX_EINVAL, "spline_pack: null pointer");
-    if (d <= 0 || d > 8 || H <= 0 || H > 128 || K < 2 || K > 11)
-        return set_error(NFX_EUNSUPPORTED, "spline_pack: d=%d H=%d K=%d outside d<=8, H<=128, 2<=K<=11", d, H, K);
+    if (d <= 0 || d > 64 || H <= 0 || H > 128 || K < 2 || K > 11)
+        return set_error(NFX_EUNSUPPORTED, "spline_pack: d=%d H=%d K=%d outside d<=64, H<=128, 2<=K<=11", d, H, K);
     for (int l = 0; l < 3; ++l)
         if (!net->w[l]) return set_error(NFX_EINVAL, "spline_pack: layer %d weight is null", l);
     const int total = (int)nfx_spline_packed_floats(d, H, K);
@@ -117,8 +127,8 @@ static int spline_launch(const float* packed, const float* in, float* out, float
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "spline_coupling: bad shape");
     if (direction != NFX_FORWARD && direction != NFX_INVERSE)
         return set_error(NFX_EINVAL, "spline_coupling: direction must be +1 or -1");
-    if (d > 8 || H > 128 || K < 2 || K > 11)
-        return set_error(NFX_EUNSUPPORTED, "spline_coupling: d=%d H=%d K=%d outside d<=8, H<=128, 2<=K<=11", d, H, K);
+    if (d > 64 || H > 128 || K < 2 || K > 11)
+        return set_error(NFX_EUNSUPPORTED, "spline_coupling: d=%d H=%d K=%d outside d<=64, H<=128, 2<=K<=11", d, H, K);
     if (fused && B > 0 && (!logp || !workspace)) return set_error(NFX_EINVAL, "spline_coupling_logprob: null logp/workspace");
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, stream) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "spline_coupling: null pointer");
@@ -139,6 +149,19 @@ static int spline_launch(const float* packed, const float* in, float* out, float
     C.rs_lo = data_min;
     C.rs_to_scale = rescale ? (float)((2.0 * bound) / ((double)data_max - (double)data_min)) : 1.f;
     C.rs_from_scale = rescale ? (float)(((double)data_max - (double)data_min) / (2.0 * bound)) : 1.f;
+    if (d > 8) {  // wide kernel: 32-sample tiles, weights from L2
+        const size_t ldsw = (size_t)kSplineWideWaves * 32 * (d | 1) * sizeof(float);
+        const int64_t ntiles = (B + 31) / 32;
+        int gw = resident_grid((const void*)k, 64 * kSplineWideWaves, ldsw,
+                               (ntiles + kSplineWideWaves - 1) / kSplineWideWaves);
+        if (gw > kMaxPartials) gw = kMaxPartials;
+        double* pw = reinterpret_cast<double*>(workspace);
+        k<<<gw, 64 * kSplineWideWaves, ldsw, stream>>>(packed, in, out, log_det, B, d, C, accumulate, ntiles, logp, pw,
+                                                        gauss_const(d));
+        int rcw = check_launch("spline_wide_kernel");
+        if (rcw || !fused) return rcw;
+        return gauss_finish(pw, gw, sums, B, stream);
+    }
     const size_t lds = (size_t)spline_layout(HT, d).total * sizeof(float);
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;

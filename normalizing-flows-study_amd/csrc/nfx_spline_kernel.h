@@ -21,17 +21,21 @@ namespace nfx {
 __host__ __device__ constexpr int sp_up4(int v) { return (v + 3) & ~3; }
 
 // Packed image (floats):
-//   w1 [HT][4][64]         layer-1 A operand, k-steps padded to 4 (d <= 8)
+//   w1 [HT][KS][64]        layer-1 A operand, KS = spline_ks1(d) k-steps (4, padded, for d <= 8)
 //   b1 [HT][2][16]         (bias of accumulator register r, lane-half h)
 //   w2 [HT][HT][4][64][4]
 //   b2 [HT][2][16]
 //   w3 [d][HT][4][64][4]   output tile t = t-th transformed dim: row i = parameter i
 //   b3 [d][2][16]
-//   mask [8], tdim [8] (indices of the transformed dims, as floats), meta [4] (meta[0] = NT)
+//   mask [max(8,d)], tdim [max(8,d)] (indices of the transformed dims, as floats), meta [4]
+//   (meta[0] = NT)
 struct SplineLayout {
     int HT, NT;  // NT here = capacity (d); the live count is meta[0]
     int w1, b1, w2, b2, w3, b3, mask, tdim, meta, total;
 };
+
+// layer-1 k-steps of the packed image: 4 (d <= 8, padded) or ceil(d/2) (wide kernel)
+__host__ __device__ constexpr int spline_ks1(int d) { return d <= 8 ? 4 : (d + 1) / 2; }
 
 __host__ __device__ constexpr SplineLayout spline_layout(int HT, int d) {
     SplineLayout L{};
@@ -39,14 +43,14 @@ __host__ __device__ constexpr SplineLayout spline_layout(int HT, int d) {
     L.HT = HT;
     L.NT = NT;
     int o = 0;
-    L.w1 = o; o += HT * 4 * 64;
+    L.w1 = o; o += HT * spline_ks1(d) * 64;
     L.b1 = o; o += HT * 32;
     L.w2 = o; o += HT * HT * 16 * 64;
     L.b2 = o; o += HT * 32;
     L.w3 = o; o += NT * HT * 16 * 64;
     L.b3 = o; o += NT * 32;
-    L.mask = o; o += 8;
-    L.tdim = o; o += 8;
+    L.mask = o; o += sp_up4(d > 8 ? d : 8);
+    L.tdim = o; o += sp_up4(d > 8 ? d : 8);
     L.meta = o; o += 4;
     L.total = o;
     return L;
@@ -474,5 +478,152 @@ typedef void (*spline_kernel_t)(const float*, const float*, float*, float*, int6
 // DS = 0: runtime d <= 8; DS = 2: the d = 2 specialisation (nfx_spline_d2_h*.hip)
 template <int HT, int DS>
 spline_kernel_t spline_pick_ht(int K, int dir, bool logp);
+
+
+// ---- wide spline coupling layers (8 < d <= 64) -----------------------------------------------
+// A wave owns a 32-sample tile whose [32 x d] x block sits in a wave-private LDS tile (odd row
+// stride), loaded/stored with coalesced row accesses. The param MLP runs as in the narrow kernel
+// (weights from L2: the d(3K-1)-row output layer outgrows LDS); the output layer produces the
+// tiles of two transformed dims (t, t+1) for the same 32 samples, and one v_permlane32_swap per
+// register leaves lanes 0..31 holding all parameters of dim t and lanes 32..63 those of dim t+1
+// for sample `col` — both lane halves run a spline, none is duplicated. Outputs go back into the
+// tile in place (each spline reads only its own dimension).
+constexpr int kSplineWideWaves = 4;
+
+template <int HT, int K, int DIR, bool LOGP>
+__global__ __launch_bounds__(64 * kSplineWideWaves) void spline_wide_kernel(
+    const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
+    float* __restrict__ logdet, int64_t B, int d, SplineConsts C, int accumulate, int64_t ntiles,
+    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+#pragma clang fp contract(off)
+    const SplineLayout L = spline_layout(HT, d);
+    const int KS = spline_ks1(d);
+    const int S = d | 1;
+    extern __shared__ f32x4 lds4[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* xt = reinterpret_cast<float*>(lds4) + wave * 32 * S;
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int NT = (int)packed[L.meta];
+    double lpacc = 0.0;
+    for (int64_t t = (int64_t)blockIdx.x * kSplineWideWaves + wave; t < ntiles;
+         t += (int64_t)gridDim.x * kSplineWideWaves) {
+        const int64_t base = t * 32;
+        const int rows = (int)(B - base < 32 ? B - base : 32);
+        const float* src = in + base * d;
+        for (int i = lane; i < 32 * d; i += 64) {
+            const int r = i / d, c = i - r * d;
+            xt[r * S + c] = r < rows ? src[i] : 0.f;
+        }
+        const float ldin = (accumulate && lane < rows) ? logdet[base + lane] : 0.f;
+        wave_lds_sync();
+        const float* P = packed + opaque_zero();
+        // layer 1 (x rescaled, times mask) + ReLU
+        f32x16 h1[HT];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(P + L.b1 + ht * 32, h);
+        for (int ks = 0; ks < KS; ++ks) {
+            const int k = 2 * ks + h;
+            float xv = 0.f;
+            if (k < d) {
+                xv = xt[col * S + k];
+                if (C.rescale) xv = C.rs_to_scale * (xv - C.rs_lo) - C.bound;
+                xv = xv * P[L.mask + k];
+            }
+#pragma unroll
+            for (int ht = 0; ht < HT; ++ht) h1[ht] = mfma32(P[L.w1 + (ht * KS + ks) * 64 + lane], xv, h1[ht]);
+        }
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
+        f32x16 h2[HT];
+#pragma unroll
+        for (int hto = 0; hto < HT; ++hto) {
+            f32x16 a = load_bias16(P + L.b2 + hto * 32, h);
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h1[kt][4 * rq + rr], a);
+                }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+            h2[hto] = a;
+        }
+        float ldp = 0.f;
+        for (int tt = 0; tt < NT; tt += 2) {
+            const bool two = tt + 1 < NT;
+            f32x16 a0 = load_bias16(P + L.b3 + tt * 32, h);
+            f32x16 a1 = two ? load_bias16(P + L.b3 + (tt + 1) * 32, h) : f32x16{};
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt)
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 w0 = *reinterpret_cast<const f32x4*>(P + L.w3 + (((tt * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                    const f32x4 w1 = two ? *reinterpret_cast<const f32x4*>(
+                                               P + L.w3 + ((((tt + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4)
+                                         : f32x4{};
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        a0 = mfma32(w0[rr], h2[kt][4 * rq + rr], a0);
+                        a1 = mfma32(w1[rr], h2[kt][4 * rq + rr], a1);
+                    }
+                }
+            float prm[32];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0[r]), __float_as_uint(a1[r]), false, false);
+                prm[crow(r, 0)] = __uint_as_float(sw[0]);
+                prm[crow(r, 1)] = __uint_as_float(sw[1]);
+            }
+            if (h == 0 || two) {
+                const int dt = (int)P[L.tdim + tt + h];
+                float* px = xt + col * S + dt;
+                float v = *px;
+                if (C.rescale) v = C.rs_to_scale * (v - C.rs_lo) - C.bound;
+                float o, l;
+                rq_spline_elem<K, (DIR < 0)>(v, prm, C, o, l);
+                if (C.rescale) o = (o + C.bound) * C.rs_from_scale + C.rs_lo;
+                *px = o;
+                ldp = ldp + l;
+            }
+        }
+        float ld = halves_sum(ldp, ldp);
+        if (nonfinite(ld)) ld = 0.f;
+        wave_lds_sync();
+        float* dst = out + base * d;
+        for (int i = lane; i < rows * d; i += 64) {
+            const int r = i / d, c = i - r * d;
+            const float v = xt[r * S + c];
+            dst[i] = nonfinite(v) ? 0.f : v;
+        }
+        if (lane < rows) {
+            const float ldt = accumulate ? ldin + ld : ld;
+            logdet[base + lane] = ldt;
+            if constexpr (LOGP) {
+                float m = 0.f;
+                for (int c = 0; c < d; ++c) {
+                    float v = xt[lane * S + c];
+                    v = nonfinite(v) ? 0.f : v;
+                    m = c == 0 ? gauss_sq0(v) : gauss_sq(m, v);
+                }
+                const float lp = gauss_lp(m, cgauss, ldt);
+                logp[base + lane] = lp;
+                lpacc += (double)lp;
+            }
+        }
+        wave_lds_sync();
+    }
+    if constexpr (LOGP) {
+        const double tsum = block_sum_f64<64 * kSplineWideWaves>(lpacc);
+        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    }
+}
+
+// wide kernels (8 < d <= 64), one TU per HT (nfx_spline_w_h*.hip)
+template <int HT>
+spline_kernel_t spline_wide_pick_ht(int K, int dir, bool logp);
 
 }  // namespace nfx

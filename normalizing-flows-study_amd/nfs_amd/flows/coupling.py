@@ -27,7 +27,8 @@ from .. import _lib
 from .. import distributed as _dist
 from .flow import HipFlow, STATS
 
-MAX_D = 8
+MAX_D = 64          # eval kernels: affine_coupling_kernel (d <= 8) / affine_wide_kernel (d <= 64)
+MAX_D_TRAIN = 8     # train-mode / backward kernels
 MAX_H = 128
 MAX_H_TRAIN = 64
 ctypes_vp = ctypes.c_void_p
@@ -130,7 +131,7 @@ class CouplingLayer(HipFlow):
                for bn in bns):
             return False
         d, H = self.data_dim, self._hidden()
-        return x.shape[1] == d and d <= MAX_D and H <= MAX_H_TRAIN and x.shape[0] >= 2
+        return x.shape[1] == d and d <= MAX_D_TRAIN and H <= MAX_H_TRAIN and x.shape[0] >= 2
 
     def _dispatch(self, x, direction):
         if self._train_ok(x):
@@ -212,7 +213,7 @@ class CouplingLayer(HipFlow):
             return False
         if any(bn.training or not bn.affine or bn.running_mean is None for bn in bns):
             return False
-        return x.shape[1] == self.data_dim and self.data_dim <= MAX_D and self._hidden() <= MAX_H_TRAIN
+        return x.shape[1] == self.data_dim and self.data_dim <= MAX_D_TRAIN and self._hidden() <= MAX_H_TRAIN
 
     def _build_eval_backward_pack(self, device):
         L = _lib.lib()

@@ -17,7 +17,8 @@ from .. import _lib
 from .flow import HipFlow, STATS
 
 MAX_K = 11        # 3K-1 <= 32: one MFMA row tile of spline parameters per transformed dim
-MAX_D = 8
+MAX_D = 64        # spline_coupling_kernel (d <= 8) / spline_wide_kernel (d <= 64)
+MAX_D_BWD = 8     # fused backward
 MAX_H = 128
 MAX_H_BWD = 64    # fused backward: dW accumulators of <= 2 (H <= 32) / 1 (H <= 64) transformed dims
 # (kernel-name, start-event, end-event) of every fused backward while a list is installed here
@@ -210,7 +211,7 @@ class SplineCouplingLayer(HipFlow):
         d, H, K = self.data_dim, self._hidden(), self.num_bins
         nt = self._n_transformed()
         ntmax = 2 if H <= 32 else 1
-        return (x.dtype == torch.float32 and d <= MAX_D and H <= MAX_H_BWD and 2 <= K <= MAX_K
+        return (x.dtype == torch.float32 and d <= MAX_D_BWD and H <= MAX_H_BWD and 2 <= K <= MAX_K
                 and nt <= ntmax and (self.data_min is None or self.data_max is None))
 
     def _n_transformed(self):
