@@ -14,6 +14,8 @@
 // citardauq inverse, and the reference's three guard stages. HBM traffic per sample is the
 // x row in, the y row out and the log-det read-modify-write (8d + 8 bytes).
 #pragma once
+#include <type_traits>
+
 #include "nfx_common.h"
 
 namespace nfx {
@@ -278,11 +280,22 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
         float xr[DMAX];   // the lane's own sample row
         float ldin;
     };
-    auto fetch = [&](int64_t c, Fetch& f) {
-        const int64_t base = c * 64;
-        const bool live = c < nchunks;
+    // Work split (as affine_coupling_kernel): every wave takes F = nchunks / nwaves whole 64-sample
+    // chunks; the R leftover chunks go out as 2R 32-sample half chunks, one to each of the first
+    // 2R waves (when 2R <= nwaves), so a SIMD's last round is half a chunk (1M samples: 15.26 chunks
+    // per SIMD ran as 16 rounds, now 15.5).
+    const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t F = nchunks / nwaves, R = nchunks - F * nwaves;
+    const bool split = 2 * R <= nwaves;
+    const int64_t nfull = split ? F : F + (wv < R ? 1 : 0);
+    const bool half = split && wv < 2 * R;
+    const int64_t half_base = F * nwaves * 64 + wv * 32;
+    auto unit_base = [&](int64_t u) { return u < nfull ? (wv + u * nwaves) * 64 : half_base; };
+    auto fetch = [&](int64_t u, Fetch& f) {
+        const int64_t base = unit_base(u);
+        const int nsamp = u < nfull ? 64 : (u == nfull && half ? 32 : 0);
         const int64_t so = base + lane;
-        const bool row = live && so < B;
+        const bool row = lane < nsamp && so < B;
         if constexpr (DS == 2) {
             const f32x2 v = row ? *reinterpret_cast<const f32x2*>(in + so * 2) : f32x2{0.f, 0.f};
             f.xr[0] = v.x;
@@ -294,7 +307,7 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const int k = 2 * ks + h;
-                    f.xb[st][ks] = (live && ks < KS1 && k < d && s < B) ? in[s * d + k] : 0.f;
+                    f.xb[st][ks] = (32 * st + col < nsamp && ks < KS1 && k < d && s < B) ? in[s * d + k] : 0.f;
                 }
             }
 #pragma unroll
@@ -306,15 +319,12 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) mkb[ks] = (2 * ks + h < d) ? sm[L.mask + 2 * ks + h] : 0.f;
 
-    int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    Fetch cur;
-    fetch(c, cur);
     double lpacc = 0.0;
-    for (; c < nchunks; c += nwaves) {
-        const int64_t base = c * 64;
+    // one unit: 2 sample tiles (TILES = 2) or the half chunk (TILES = 1: tile 1's MFMAs skipped,
+    // lanes 32..63 compute unused values)
+    auto unit = [&](auto tiles_c, int64_t base, const Fetch& cur) {
+        constexpr int TILES = decltype(tiles_c)::value;
         const float* P = sm + opaque_zero();
-        Fetch nxt;
-        fetch(c + nwaves, nxt);
 
         // Layer-1 B operands (x rescaled, times mask), k-steps padded to 4.
         float xraw[2][4];
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
                 if (ks < KS1) {
                     const float w = P[L.w1 + (ht * 4 + ks) * 64 + lane];
                     a0 = mfma32(w, xb[0][ks], a0);
-                    a1 = mfma32(w, xb[1][ks], a1);
+                    if constexpr (TILES == 2) a1 = mfma32(w, xb[1][ks], a1);
                 }
             }
 #pragma unroll
@@ -384,7 +394,7 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) {
                         a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
-                        a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
+                        if constexpr (TILES == 2) a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
                     }
                 }
             }
@@ -414,7 +424,7 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) {
                         a0 = mfma32(w[rr], h2[kt][0][4 * rq + rr], a0);
-                        a1 = mfma32(w[rr], h2[kt][1][4 * rq + rr], a1);
+                        if constexpr (TILES == 2) a1 = mfma32(w[rr], h2[kt][1][4 * rq + rr], a1);
                     }
                 }
             }
@@ -439,7 +449,7 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
             for (int j = 0; j < DMAX; ++j) y[j] = (j == dt) ? o : y[j];
             ld = (t == 0) ? l : ld + l;
         }
-        if (so < B) {
+        if (lane < 32 * TILES && so < B) {
             float m = 0.f;
             float yo[DMAX];
 #pragma unroll
@@ -464,8 +474,17 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
                 lpacc += (double)lp;
             }
         }
+    };
+
+    Fetch cur;
+    fetch(0, cur);
+    for (int64_t u = 0; u < nfull; ++u) {
+        Fetch nxt;
+        fetch(u + 1, nxt);
+        unit(std::integral_constant<int, 2>{}, unit_base(u), cur);
         cur = nxt;
     }
+    if (half) unit(std::integral_constant<int, 1>{}, half_base, cur);
     if constexpr (LOGP) {
         const double t = block_sum_f64<256>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
