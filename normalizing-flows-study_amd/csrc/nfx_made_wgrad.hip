@@ -31,13 +31,13 @@ struct WgLayer {
     float* gw;        // weight gradient [M x N] (row-major, nn.Linear layout)
     float* gb;        // bias gradient [M] (nullptr: no bias)
     int M, N, tm, tn, tile0, btile0;  // tiles: tm x tn starting at tile0; row blocks at btile0
-    int nrs, ncs, task0;              // workgroup tasks: super blocks of <= 4 x 4 tiles
 };
 struct WgArgs {
     WgLayer l[4];
-    int nl, T, NBT, TPC;  // layers, total tiles, total bias row blocks, workgroup tasks per chunk
+    int nl, T, NBT;  // layers, total tiles, total bias row blocks
 };
 
+constexpr int kWgWaves = 4;
 
 __device__ __forceinline__ int wg_layer_of(const WgArgs& a, int t) {
     int k = 0;
@@ -47,146 +47,117 @@ __device__ __forceinline__ int wg_layer_of(const WgArgs& a, int t) {
     return k;
 }
 
-// One workgroup = (sample chunk, layer, super block of <= 4 x 4 output tiles). Per 32-sample step
-// the rows its tiles need — <= 128 δ rows and <= 128 input rows, 128 bytes each — are read from
-// HBM ONCE (coalesced 16-byte loads, 8 per row segment) into a double-buffered LDS stage (row
-// stride 36 floats: the 16-byte operand reads of 32 different rows are conflict-free), the next
-// step's loads in flight while the 4 waves run their tiles' MFMAs from LDS (each wave <= 4 tiles,
-// 16 MFMAs per tile per step: lane (i, kh) feeds samples 16 kh .. 16 kh + 15 of row i).
-constexpr int kWgRS = 36;              // LDS row stride (floats)
-constexpr int kWgStage = 256 * kWgRS;  // one buffer: <= 128 δ rows + <= 128 input rows
-
 template <bool VEC4>
-__global__ __launch_bounds__(256) void made_wgrad_kernel(WgArgs a, int64_t B, int64_t P, int64_t chunk,
-                                                         int64_t ntasks, float* part) {
-    extern __shared__ f32x4 lds4[];
-    float* lds = reinterpret_cast<float*>(lds4);
-    const int64_t task = blockIdx.x;
+__global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int64_t B, int64_t P, int64_t chunk,
+                                                                   int64_t ntasks, int blocks_per_xcd, float* part) {
+    // undo the hardware's round robin of consecutive workgroups over the 8 XCDs
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: descriptors stay scalar
+    const int64_t task = ((int64_t)xcd * blocks_per_xcd + slot) * kWgWaves + wave;
     if (task >= ntasks) return;
     const int T = a.T;
-    const int64_t c = task / a.TPC;
-    const int tk = (int)(task % a.TPC);
-    int k = 0;
-#pragma unroll
-    for (int j = 1; j < 4; ++j)
-        if (j < a.nl && tk >= a.l[j].task0) k = j;
+    const int64_t c = task / T;
+    const int t = (int)(task % T);
+    const int k = wg_layer_of(a, t);
+    // field by field with constant kernarg indices: a dynamic index would copy the struct to
+    // scratch and turn every descriptor below into a VGPR (waterfall loops around each load)
 #define WGF(f) (k == 0 ? a.l[0].f : (k == 1 ? a.l[1].f : (k == 2 ? a.l[2].f : a.l[3].f)))
     const float* Ldm = WGF(dm);
     const float* Lam = WGF(am);
     const bool has_b = WGF(gb) != nullptr;
-    const int LM = WGF(M), LN = WGF(N), Ltn = WGF(tn), Ltm = WGF(tm), Ltile0 = WGF(tile0), Lbt0 = WGF(btile0);
-    const int Lncs = WGF(ncs), Ltask0 = WGF(task0);
+    const int LM = WGF(M), LN = WGF(N), Ltn = WGF(tn), Ltile0 = WGF(tile0), Lbt0 = WGF(btile0);
 #undef WGF
-    const int lt = tk - Ltask0, rs = lt / Lncs, cs = lt % Lncs;
-    const int rb0 = 4 * rs, cb0 = 4 * cs;
-    const int nrb = Ltm - rb0 < 4 ? Ltm - rb0 : 4, ncb = Ltn - cb0 < 4 ? Ltn - cb0 : 4;
-    const int R = 32 * nrb, NR = R + 32 * ncb;  // staged rows: δ rows [0, R), input rows [R, NR)
-    const int64_t s0 = c * chunk, s1 = (s0 + chunk < B) ? s0 + chunk : B;
-    const int nsteps = (int)((s1 - s0 + 31) / 32);
+    const int lt = t - Ltile0, tmi = lt / Ltn, tni = lt % Ltn;
     const int lane = lane_id(), i = lane & 31, kh = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nt = nrb * ncb;
-
-    // staging: item = (row, 16-byte piece q) for items threadIdx.x + 256 j
-    // two register sets: step s + 2 is loaded while step s computes and step s + 1 waits in
-    // registers for its LDS buffer (HBM latency covered by two steps of MFMA work)
-    auto load = [&](int step, f32x4 (&st)[8]) {
-        const int64_t sb = s0 + 32 * (int64_t)step;
-        const bool tail = sb + 32 > s1;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int item = threadIdx.x + 256 * j, row = item >> 3, q = item & 7;
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (row < NR) {
-                const bool dside = row < R;
-                const int grow = dside ? 32 * rb0 + row : 32 * cb0 + row - R;
-                if (grow < (dside ? LM : LN)) {
-                    const float* src = (dside ? Ldm : Lam) + (int64_t)grow * P + sb + 4 * q;
-                    if (VEC4 && !tail) {
-                        v = *reinterpret_cast<const f32x4*>(src);
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = sb + 4 * q + e < s1 ? src[e] : 0.f;
-                    }
-                }
-            }
-            st[j] = v;
-        }
-    };
-    auto stash = [&](int buf, const f32x4 (&st)[8]) {
-        float* dst = lds + buf * kWgStage;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int item = threadIdx.x + 256 * j, row = item >> 3, q = item & 7;
-            if (row < NR) *reinterpret_cast<f32x4*>(dst + row * kWgRS + 4 * q) = st[j];
-        }
-    };
-
-    f32x16 acc[4];
-    float bsum[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        acc[u] = f32x16{};
-        bsum[u] = 0.f;
+    const int64_t s0 = c * chunk, s1 = (s0 + chunk < B) ? s0 + chunk : B;
+    // descriptors based at the tile's first row: rows past M / N read as 0 (range check)
+    const int rowsD = LM - 32 * tmi < 32 ? LM - 32 * tmi : 32;
+    const int rowsA = LN - 32 * tni < 32 ? LN - 32 * tni : 32;
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Ldm) + (int64_t)32 * tmi * P, 0,
+                                                      (int)(rowsD * P * 4), 0x00020000);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Lam) + (int64_t)32 * tni * P, 0,
+                                                      (int)(rowsA * P * 4), 0x00020000);
+    const int vo = (int)((i * P + 16 * kh) * 4);
+    const bool bias = tni == 0 && has_b;
+    f32x16 acc{};
+    float bsum = 0.f;
+    int64_t s = s0;
+    // full 32-sample steps, two per iteration with the next pair's loads in flight
+#define load16(r, st, v)                                                                                   \
+    if constexpr (VEC4) {                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                    \
+            const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, vo, (int)((st) * 4) + 16 * q, 0);      \
+            v[q] = f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),             \
+                         __uint_as_float(u[3])};                                                           \
+        }                                                                                                  \
+    } else {                                                                                               \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) _Pragma("unroll") for (int e = 0; e < 4; ++e)        \
+            v[q][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, (int)((st) * 4) + 16 * q + 4 * e, 0)); \
     }
-    auto compute = [&](int step) {
-        const float* buf = lds + (step & 1) * kWgStage;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int ti = wave + 4 * u;
-            if (ti < nt) {
-                const int ta = ti / ncb, tb = ti % ncb;
-                const float* ar = buf + (32 * ta + i) * kWgRS + 16 * kh;
-                const float* br = buf + (R + 32 * tb + i) * kWgRS + 16 * kh;
-                const bool bias = has_b && cs == 0 && tb == 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const f32x4 av = *reinterpret_cast<const f32x4*>(ar + 4 * q);
-                    const f32x4 bv = *reinterpret_cast<const f32x4*>(br + 4 * q);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        acc[u] = mfma32(av[e], bv[e], acc[u]);
-                        if (bias) bsum[u] += av[e];
-                    }
-                }
-            }
-        }
-    };
-    f32x4 sa[8], sb2[8];
-    load(0, sa);
-    stash(0, sa);
-    if (nsteps > 1) load(1, sa);
-    __syncthreads();
-    for (int step = 0; step < nsteps; step += 2) {
-        // even step: sa holds step + 1
-        if (step + 2 < nsteps) load(step + 2, sb2);
-        compute(step);
-        if (step + 1 < nsteps) stash((step + 1) & 1, sa);
-        __syncthreads();
-        if (step + 1 >= nsteps) break;
-        // odd step: sb2 holds step + 2
-        if (step + 3 < nsteps) load(step + 3, sa);
-        compute(step + 1);
-        if (step + 2 < nsteps) stash((step + 2) & 1, sb2);
-        __syncthreads();
-    }
-    const int64_t len = (int64_t)T * 1024 + (int64_t)a.NBT * 32;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int ti = wave + 4 * u;
-        if (ti < nt) {
-            const int ta = ti / ncb, tb = ti % ncb;
-            const int gt = Ltile0 + (rb0 + ta) * Ltn + cb0 + tb;
-            float* o = part + c * len + (int64_t)gt * 1024 + lane * 16;
+    const int64_t full_end = s0 + ((s1 - s0) / 32) * 32;
+    if (s < full_end) {
+        // software pipeline over two register sets: the next step's rows are in flight while this
+        // step's 16 MFMAs run; the sched barriers keep the loads ahead of the MFMAs (the last
+        // step's prefetch re-reads itself instead of branching around the loads)
+        f32x4 dA[4], aA[4], dB[4], aB[4];
+        load16(rd, s, dA);
+        load16(ra, s, aA);
+        for (;;) {
+            int64_t sn = s + 32 < full_end ? s + 32 : s;
+            load16(rd, sn, dB);
+            load16(ra, sn, aB);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<f32x4*>(o + 4 * q) = f32x4{acc[u][4 * q], acc[u][4 * q + 1], acc[u][4 * q + 2], acc[u][4 * q + 3]};
-            if (has_b && cs == 0 && tb == 0) {
-                const float other = __shfl_xor(bsum[u], 32, 64);
-                if (kh == 0) part[c * len + (int64_t)T * 1024 + (int64_t)(Lbt0 + rb0 + ta) * 32 + i] = bsum[u] + other;
-            }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc = mfma32(dA[q][e], aA[q][e], acc);
+                    if (bias) bsum += dA[q][e];
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            s += 32;
+            if (s >= full_end) break;
+            sn = s + 32 < full_end ? s + 32 : s;
+            load16(rd, sn, dA);
+            load16(ra, sn, aA);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc = mfma32(dB[q][e], aB[q][e], acc);
+                    if (bias) bsum += dB[q][e];
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            s += 32;
+            if (s >= full_end) break;
         }
     }
+    if (s < s1) {  // ragged tail of the batch: samples >= B hold pitch padding -> select 0
+        f32x4 dv[4], av[4];
+        load16(rd, s, dv);
+        load16(ra, s, av);
+        const int64_t nval = s1 - s - 16 * kh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = 4 * q + e < nval;
+                const float dvv = ok ? dv[q][e] : 0.f, avv = ok ? av[q][e] : 0.f;
+                acc = mfma32(dvv, avv, acc);
+                if (bias) bsum += dvv;
+            }
+    }
+    const int64_t len = (int64_t)T * 1024 + (int64_t)a.NBT * 32;
+    float* out = part + c * len + (int64_t)t * 1024 + lane * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(out + 4 * q) = f32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+    if (bias) {
+        const float other = __shfl_xor(bsum, 32, 64);
+        if (kh == 0) part[c * len + (int64_t)T * 1024 + (int64_t)(Lbt0 + tmi) * 32 + i] = bsum + other;
+    }
+#undef load16
 }
 
 // sums[T*1024 + NBT*32] (float64, accumulator order) -> parameter gradients, masks applied.
@@ -214,11 +185,10 @@ __global__ void made_wgrad_assemble_kernel(WgArgs a, const double* sums) {
     }
 }
 
-static int64_t wg_chunk(int64_t B, int TPC) {
-    // about 1024 workgroups (4 per CU, one round at 2 resident per CU... 72 KB LDS each), chunks of
-    // >= 512 samples, 32-aligned
-    int64_t c = (B * TPC + 1023) / 1024;
-    if (c < 512) c = 512;
+static int64_t wg_chunk(int64_t B, int T) {
+    // about 4096 tasks (4 waves per SIMD in one round), chunks of >= 1024 samples, 32-aligned
+    int64_t c = (B * T + 4095) / 4096;
+    if (c < 1024) c = 1024;
     return (c + 31) & ~(int64_t)31;
 }
 
@@ -236,7 +206,7 @@ static WgArgs wg_args(const float* factors, int64_t P, int d, int H, const float
     const float* am[4] = {X1, H1, H2, H3};
     const int M[4] = {H, H, H, 2 * d}, N[4] = {d, H, H, H};
     // parameters() order: net.0.weight, net.0.bias, net.2.*, net.4.*, net.6.*
-    int64_t off = 0, tile = 0, bt = 0, task = 0;
+    int64_t off = 0, tile = 0, bt = 0;
     for (int k = 0; k < 4; ++k) {
         WgLayer& L = a.l[k];
         L.dm = dm[k];
@@ -250,10 +220,6 @@ static WgArgs wg_args(const float* factors, int64_t P, int d, int H, const float
         L.btile0 = (int)bt;
         tile += L.tm * L.tn;
         bt += L.tm;
-        L.nrs = (L.tm + 3) / 4;
-        L.ncs = (L.tn + 3) / 4;
-        L.task0 = (int)task;
-        task += L.nrs * L.ncs;
         L.gw = grads + off;
         off += (int64_t)M[k] * N[k];
         L.gb = grads + off;
@@ -262,7 +228,6 @@ static WgArgs wg_args(const float* factors, int64_t P, int d, int H, const float
     a.nl = 4;
     a.T = (int)tile;
     a.NBT = (int)bt;
-    a.TPC = (int)task;
     return a;
 }
 
@@ -274,11 +239,12 @@ extern "C" int64_t nfx_made_factor_pitch(int64_t B) { return B <= 0 ? 0 : B; }
 
 extern "C" size_t nfx_made_wgrad_workspace_bytes(int64_t B, int d, int H) {
     if (B <= 0 || d <= 0 || H <= 0) return 0;
-    const WgArgs a = wg_args(nullptr, B, d, H, nullptr, nullptr);
-    const int64_t len = (int64_t)a.T * 1024 + (int64_t)a.NBT * 32;
-    const int64_t chunk = wg_chunk(B, a.TPC);
+    const int64_t T = ((H + 31) / 32) * (((d + 31) / 32) + 2 * ((H + 31) / 32)) + ((2 * d + 31) / 32) * ((H + 31) / 32);
+    const int64_t NBT = 3 * ((H + 31) / 32) + (2 * d + 31) / 32;
+    const int64_t len = T * 1024 + NBT * 32;
+    const int64_t chunk = wg_chunk(B, (int)T);
     const int64_t nch = (B + chunk - 1) / chunk;
-    return (size_t)(((nch * len * sizeof(float) + 255) & ~(size_t)255) + len * sizeof(double));
+    return (size_t)(nch * len * sizeof(float) + len * sizeof(double) + 256);
 }
 
 extern "C" size_t nfx_made_param_floats(int d, int H) {
@@ -302,20 +268,18 @@ extern "C" int nfx_made_backward_weights(const float* factors, int64_t B, int d,
         return set_error(NFX_EUNSUPPORTED, "made_backward_weights: B=%lld too large for 32-bit row offsets", (long long)B);
     const WgArgs a = wg_args(factors, P, d, H, masks, grads);
     const int64_t len = (int64_t)a.T * 1024 + (int64_t)a.NBT * 32;
-    const int64_t chunk = wg_chunk(B, a.TPC);
+    const int64_t chunk = wg_chunk(B, a.T);
     const int64_t nch = (B + chunk - 1) / chunk;
-    const int64_t ntasks = nch * a.TPC;
+    const int64_t ntasks = nch * a.T;
+    const int64_t wgs = (ntasks + kWgWaves - 1) / kWgWaves;
+    const int bpx = (int)((wgs + 7) / 8);
     float* part = reinterpret_cast<float*>(workspace);
     double* sums = reinterpret_cast<double*>(
         reinterpret_cast<char*>(workspace) + ((nch * len * sizeof(float) + 255) & ~(size_t)255));
-    const size_t lds = 2 * (size_t)kWgStage * sizeof(float);
-    const void* kp = P % 4 == 0 ? (const void*)made_wgrad_kernel<true> : (const void*)made_wgrad_kernel<false>;
-    if (int rcl = prepare_lds(kp, lds)) return rcl;
-    if (ntasks > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "made_backward_weights: too many tasks");
     if (P % 4 == 0)
-        made_wgrad_kernel<true><<<(unsigned)ntasks, 256, lds, s>>>(a, B, P, chunk, ntasks, part);
+        made_wgrad_kernel<true><<<8 * bpx, 64 * kWgWaves, 0, s>>>(a, B, P, chunk, ntasks, bpx, part);
     else
-        made_wgrad_kernel<false><<<(unsigned)ntasks, 256, lds, s>>>(a, B, P, chunk, ntasks, part);
+        made_wgrad_kernel<false><<<8 * bpx, 64 * kWgWaves, 0, s>>>(a, B, P, chunk, ntasks, bpx, part);
     int rc = check_launch("made_wgrad_kernel");
     if (rc) return rc;
     if ((rc = train_sum_finish(part, (int)nch, (int)len, sums, s))) return rc;
