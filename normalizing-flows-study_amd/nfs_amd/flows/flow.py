@@ -6,8 +6,10 @@ src/flows/flow/sequential_flow.py:5-34): `forward(z) -> (x, log_det[B])`,
 
 Routing (HipFlow._route):
   * fp32 tensors on a ROCm device  -> the layer's fused gfx950 kernel through libnfx.so.
-    If autograd needs gradients, the kernel still computes the outputs and the backward pass
-    recomputes through the layer's torch composite (HipFlowFunction).
+    If autograd needs gradients, the kernel still computes the outputs and HipFlowFunction's
+    backward runs the layer's fused backward kernels (`_hip_backward`: MADE flows in every
+    direction, spline coupling, eval-mode affine coupling); shapes outside those kernel
+    families recompute through the layer's torch composite on the GPU.
   * CPU tensors or fp64 (gradcheck)  -> the layer's torch composite (same math as the reference).
   * train-mode BatchNorm in a conditioner (CouplingLayer) -> the train-mode kernels
     (batch statistics, running-stat update, fused backward; coupling._CouplingTrainFunction).
@@ -59,7 +61,8 @@ class Flow(nn.Module):
 
 
 class HipFlowFunction(torch.autograd.Function):
-    """HIP forward, torch-composite backward (recompute) for a HipFlow layer."""
+    """HIP forward; fused HIP backward where the layer has one (`_hip_backward_ok`), else a
+    recompute through the layer's torch composite."""
 
     @staticmethod
     def forward(ctx, layer, direction, x, *params):
