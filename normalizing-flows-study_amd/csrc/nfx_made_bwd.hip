@@ -100,6 +100,47 @@ __device__ __forceinline__ f32x16 chain_gmem(const float* __restrict__ A, int ot
     return acc;
 }
 
+// chain_gmem over k tiles [K0, NK) only: the leading k tiles of a transposed MADE weight tile
+// row are structurally zero (sorted degrees), so they are skipped whole; k0 is wave-uniform and
+// selects a straight-line variant (no branches around individual MFMAs).
+template <int NK, int K0>
+__device__ __forceinline__ f32x16 chain_gmem_k(const float* __restrict__ A, int ot, int nk_total, const f32x16* bt,
+                                               f32x16 acc) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int kt = K0; kt < NK; ++kt) {
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(A + (((ot * nk_total + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) acc = mfma32(w[rr], bt[kt][4 * rq + rr], acc);
+        }
+    }
+    return acc;
+}
+template <int NK, int K0 = 0>
+__device__ __forceinline__ f32x16 chain_gmem_from(int k0, const float* __restrict__ A, int ot, int nk_total,
+                                                  const f32x16* bt, f32x16 acc) {
+    if constexpr (K0 >= NK) {
+        return acc;
+    } else {
+        if (k0 <= K0) return chain_gmem_k<NK, K0>(A, ot, nk_total, bt, acc);
+        return chain_gmem_from<NK, K0 + 1>(k0, A, ot, nk_total, bt, acc);
+    }
+}
+
+// All 16 x HT values of a tile set finite (wave-wide): skipping structurally-zero weight blocks
+// is then exact (a zero weight times a finite operand adds an exact zero).
+template <int HT>
+__device__ __forceinline__ bool tiles_finite(const f32x16* t) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < HT; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ok = ok && !nonfinite(t[k][r]);
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
+}
+
 constexpr int kBwdWaves = 8;  // 2 per SIMD; weights are read from L2, LDS holds the tiles
 
 template <int HT, int VAR>
@@ -132,18 +173,49 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     float* H1 = H2 + (int64_t)(H + 1) * P;
     float* X1 = H1 + (int64_t)(H + 1) * P;
 
+    // Structural-zero extents of the forward image (made_live_kernel) and their transposed
+    // starts: W^T tile (ot, kt) of a layer is nonzero iff W block (kt, ot) is, i.e. iff
+    // ot < nk[kt]; nk is non-decreasing in kt (sorted degrees), so the nonzero kt form a suffix.
+    const int* nkp = reinterpret_cast<const int*>(packed);
+    int nk1[HT], nk2[HT], nk3[HT], nk4[2];
+    bool full2 = true, full3 = true;
+#pragma unroll
+    for (int i = 0; i < HT; ++i) {
+        nk1[i] = nkp[L.nk1 + i];
+        nk2[i] = nkp[L.nk2 + i];
+        nk3[i] = nkp[L.nk3 + i];
+        full2 = full2 && nk2[i] >= HT;
+        full3 = full3 && nk3[i] >= HT;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) nk4[j] = j < NJ ? nkp[L.nk4 + j] : HT;
+    auto kstart = [&](const int* nk, int n, int ot) {
+        int k0 = n;
+        for (int k = n - 1; k >= 0; --k)
+            if (nk[k] > ot) k0 = k;
+        return k0;
+    };
+    const float tsafe = packed[L.tsafe];
+
     for (int64_t t = (int64_t)blockIdx.x * kBwdWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kBwdWaves) {
         const int64_t base = t * 32;
         const int rows = (int)(B - base < 32 ? B - base : 32);
+        float xmax = 0.f;
         {
             const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + base * d, 0, rows * rowb, 0x00020000);
             const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gout) + base * d, 0, rows * rowb, 0x00020000);
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
-                xt[r * S + lane] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff, r * rowb, 0));
+                const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff, r * rowb, 0));
+                xt[r * S + lane] = xv;
+                xmax = tmax(xmax, fabsf(xv));  // NaN-propagating: a NaN fails the test
                 gt[r * S + lane] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, voff, r * rowb, 0));
             }
         }
+        // Skip structurally-zero blocks only when the tile's inputs are finite and within the
+        // overflow-safe bound (every forward activation finite: bit-identical to dense, as in
+        // made_tile_kernel); the backward chains additionally check their operand tiles.
+        const bool dense = __builtin_amdgcn_ballot_w64(!(xmax <= tsafe)) != 0;
         wave_lds_sync();
         // opaque offsets keep the compiler from hoisting every (loop-invariant) weight read out
         // of the tile loop into registers
@@ -167,30 +239,29 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
             }
         }
 
-        // ---- forward (dense) ----
+        // ---- forward recompute (structurally-zero blocks skipped unless dense) ----
         f32x16 h1[HT], h2[HT], h3[HT];
 #pragma unroll
-        for (int ht = 0; ht < HT; ++ht) h1[ht] = load_bias16(Wf + L.b1 + ht * 32, h);
-        for (int kc = 0; kc < NKC; ++kc) {
+        for (int ht = 0; ht < HT; ++ht) {
+            f32x16 a = load_bias16(Wf + L.b1 + ht * 32, h);
+            const int nkc = dense ? NKC : nk1[ht];
+            for (int kc = 0; kc < nkc; ++kc) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-#pragma unroll
-                for (int ht = 0; ht < HT; ++ht) {
+                for (int g = 0; g < 4; ++g) {
                     const f32x4 w = *reinterpret_cast<const f32x4*>(Wf + L.w1 + ((ht * 4 * NKC + kc * 4 + g) * 64 + lane) * 4);
 #pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) h1[ht] = mfma32(w[rr], xt[col * S + 32 * kc + 8 * g + 2 * rr + h], h1[ht]);
+                    for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], xt[col * S + 32 * kc + 8 * g + 2 * rr + h], a);
                 }
             }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+            h1[ht] = a;
         }
-#pragma unroll
-        for (int ht = 0; ht < HT; ++ht)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) h1[ht][r] = trelu(h1[ht][r]);
-        made_hidden1<HT>(Wf, L.w2, L.b2, h1, h2);
+        made_hidden_nk<HT>(Wf, L.w2, L.b2, h1, h2, nk2, dense || full2);
         const uint32_t m1 = relu_bits<HT>(h1);
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) store_fm(H1, h1[ht], 32 * ht, H, B, P, base);
-        made_hidden1<HT>(Wf, L.w3, L.b3, h2, h3);
+        made_hidden_nk<HT>(Wf, L.w3, L.b3, h2, h3, nk3, dense || full3);
         const uint32_t m2 = relu_bits<HT>(h2);
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) store_fm(H2, h2[ht], 32 * ht, H, B, P, base);
@@ -201,23 +272,8 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (j < NJ) {
-                f32x16 mu = load_bias16(Wf + L.b4 + (j * 2 + 0) * 32, h);
-                f32x16 al = load_bias16(Wf + L.b4 + (j * 2 + 1) * 32, h);
-#pragma unroll
-                for (int kt = 0; kt < HT; ++kt) {
-#pragma unroll
-                    for (int rq = 0; rq < 4; ++rq) {
-                        const f32x4 wm = *reinterpret_cast<const f32x4*>(
-                            Wf + L.w4 + ((((j * 2 + 0) * HT + kt) * 4 + rq) * 64 + lane) * 4);
-                        const f32x4 wa = *reinterpret_cast<const f32x4*>(
-                            Wf + L.w4 + ((((j * 2 + 1) * HT + kt) * 4 + rq) * 64 + lane) * 4);
-#pragma unroll
-                        for (int rr = 0; rr < 4; ++rr) {
-                            mu = mfma32(wm[rr], h3[kt][4 * rq + rr], mu);
-                            al = mfma32(wa[rr], h3[kt][4 * rq + rr], al);
-                        }
-                    }
-                }
+                f32x16 mu, al;
+                out_pair_n<HT, HT>(dense ? HT : nk4[j], Wf, L, j, h3, mu, al);
                 d4[2 * j] = mu;
                 d4[2 * j + 1] = al;
             } else {
@@ -283,11 +339,15 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 
         // ---- data-gradient chain on MFMA with the transposed weights (L2); every factor is
         // written feature-major as soon as it is final so it can die ----
+        // the structurally-zero leading k tiles of each transposed row are skipped when the
+        // chain's operand tiles are finite (0 * finite = exact 0), else the dense chain runs
+        const bool d4ok = !dense && tiles_finite<4>(d4);
         f32x16 g[HT];
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = NJ == 2 ? chain_gmem<4>(Pt + L.t4, ot, 4, d4, f32x16{})
-                                 : chain_gmem<2>(Pt + L.t4, ot, 2, d4, f32x16{});
+            const int k4 = d4ok ? 2 * kstart(nk4, NJ, ot) : 0;
+            f32x16 acc = NJ == 2 ? chain_gmem_from<4>(k4, Pt + L.t4, ot, 4, d4, f32x16{})
+                                 : chain_gmem_from<2>(k4, Pt + L.t4, ot, 2, d4, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = ((m3 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g[ot] = acc;
@@ -303,10 +363,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         for (int ht = 0; ht < HT; ++ht) {
             store_fm(D3, g[ht], 32 * ht, H, B, P, base);
         }
+        const bool g3ok = !dense && tiles_finite<HT>(g);
         f32x16 g2[HT];
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = chain_gmem<HT>(Pt + L.t3, ot, HT, g, f32x16{});
+            f32x16 acc = chain_gmem_from<HT>(g3ok ? kstart(nk3, HT, ot) : 0, Pt + L.t3, ot, HT, g, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = ((m2 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g2[ot] = acc;
@@ -315,9 +376,10 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         for (int ht = 0; ht < HT; ++ht) {
             store_fm(D2, g2[ht], 32 * ht, H, B, P, base);
         }
+        const bool g2ok = !dense && tiles_finite<HT>(g2);
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = chain_gmem<HT>(Pt + L.t2, ot, HT, g2, f32x16{});
+            f32x16 acc = chain_gmem_from<HT>(g2ok ? kstart(nk2, HT, ot) : 0, Pt + L.t2, ot, HT, g2, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = ((m1 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g[ot] = acc;
@@ -328,10 +390,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         }
         // gx = direct term (in the tile) + W1mᵀ δ1, accumulator layout rows = dims
         wave_lds_sync();
+        const bool g1ok = !dense && tiles_finite<HT>(g);
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
             if (ot < NKC) {
-                const f32x16 gx = chain_gmem<HT>(Pt + L.t1, ot, HT, g, f32x16{});
+                const f32x16 gx = chain_gmem_from<HT>(g1ok ? kstart(nk1, HT, ot) : 0, Pt + L.t1, ot, HT, g, f32x16{});
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     float* px = xt + col * S + 32 * ot + crow(r, h);
