@@ -70,6 +70,9 @@ typedef struct NfxMlpRaw {
 
 int nfx_abi_version(void);
 const char* nfx_last_error(void);
+/* Test hook: overwrite the LDS of every CU with the 32-bit pattern `bits` (tests poison LDS
+ * before a kernel to show it never reads LDS it did not write). */
+int nfx_debug_fill_lds(uint32_t bits, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Affine coupling — CouplingLayer (src/flows/coupling/coupling_layer.py:5-111).

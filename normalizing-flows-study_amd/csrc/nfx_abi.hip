@@ -40,3 +40,20 @@ int num_cus() {
 
 extern "C" int nfx_abi_version(void) { return NFX_ABI_VERSION; }
 extern "C" const char* nfx_last_error(void) { return nfx::g_err; }
+
+// Test hook: fill the whole LDS of every CU with the 32-bit pattern `bits` (one 160 KiB workgroup
+// per CU, several rounds), so a kernel that read LDS it never wrote would see that pattern
+// instead of whatever the previous kernel left behind. No effect on any later result.
+__global__ __launch_bounds__(256) void nfx_fill_lds_kernel(uint32_t bits, int nwords) {
+    extern __shared__ uint32_t fill[];
+    for (int i = threadIdx.x; i < nwords; i += 256) fill[i] = bits;
+    __syncthreads();
+}
+
+extern "C" int nfx_debug_fill_lds(uint32_t bits, void* stream) {
+    const int bytes = 160 * 1024;
+    int rc = nfx::prepare_lds((const void*)nfx_fill_lds_kernel, bytes);
+    if (rc) return rc;
+    nfx_fill_lds_kernel<<<8 * nfx::num_cus(), 256, bytes, (hipStream_t)stream>>>(bits, bytes / 4);
+    return nfx::check_launch("nfx_fill_lds_kernel");
+}

@@ -243,6 +243,15 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         while (q < H && ordD[q] == ordD[p]) ++q;
         lds[S.gend + p] = (float)q;
     }
+    // The 4 pad floats of every staged w4 row are never written by the staging, but step 3 reads
+    // w1t "rows" past the block end (multiplied by exact-zero chunk values) that land in the w4
+    // rows: zero the pads once so those products are exact zeros, not 0 * (stale LDS) = NaN.
+    if constexpr (RS4 > 2 * Hp) {
+        for (int e = threadIdx.x; e < 2 * kSeqsStep * (RS4 - 2 * Hp); e += 512) {
+            const int buf = e / (kSeqsStep * (RS4 - 2 * Hp)), t = e % (kSeqsStep * (RS4 - 2 * Hp));
+            lds[S.blk + buf * S.blkf + W4F + (t / (RS4 - 2 * Hp)) * RS4 + 2 * Hp + t % (RS4 - 2 * Hp)] = 0.f;
+        }
+    }
     __syncthreads();
     const float* degR = lds + S.deg;
     const float* gendR = lds + S.gend;

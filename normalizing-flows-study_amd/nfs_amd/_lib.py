@@ -28,7 +28,7 @@ NFX_AFFINE_SMALL = 2
 
 # Every symbol include/nfx.h declares (tests check the built library exports all of them).
 EXPORTED_SYMBOLS = (
-    "nfx_abi_version", "nfx_last_error",
+    "nfx_abi_version", "nfx_last_error", "nfx_debug_fill_lds",
     "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
     "nfx_affine_kernel_policy",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
@@ -81,6 +81,7 @@ _sz = ctypes.c_size_t
 _SIGNATURES = {
     "nfx_abi_version": (_int, []),
     "nfx_last_error": (ctypes.c_char_p, []),
+    "nfx_debug_fill_lds": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p]),
     "nfx_affine_packed_floats": (_sz, [_int, _int]),
     "nfx_affine_pack": (_int, [ctypes.POINTER(NfxMlpRaw), ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _vp, _vp]),
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
