@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
     // hidden-unit degrees (row sums of the input mask) and the stable by-degree completion
     // order of the sequential kernels: s_deg [unit degree | degrees in order | units in order]
     {
-        __shared__ int deg[128];
+        __shared__ int deg[256];
         const int Hp = L.Hp;
         for (int a = threadIdx.x; a < Hp; a += 256) deg[a] = a < H ? made_unit_degree(net, d, a) : 1000000000;
         __syncthreads();
@@ -188,6 +188,9 @@ static made_seq_kernel_t pick_seq(int HT, int variant) {
     }
 }
 
+int made_big_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d, int H,
+                    int variant, int accumulate, hipStream_t s);
+
 constexpr size_t kLdsBytes = 160 * 1024;
 constexpr int kTileMaxD = 64;  // made_tile_kernel: whole [32 x d] x tile per wave in LDS
 
@@ -202,8 +205,8 @@ extern "C" size_t nfx_made_packed_floats(int d, int H) {
 
 extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
     if (!net || !packed) return set_error(NFX_EINVAL, "made_pack: null pointer");
-    if (d <= 0 || d > 4096 || H <= 0 || H > 128)
-        return set_error(NFX_EUNSUPPORTED, "made_pack: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (d <= 0 || d > 4096 || H <= 0 || H > 256)
+        return set_error(NFX_EUNSUPPORTED, "made_pack: d=%d H=%d outside d<=4096, H<=256", d, H);
     if (net->n_layers != 4) return set_error(NFX_EINVAL, "made_pack: MADE has 4 masked layers (got %d)", net->n_layers);
     for (int l = 0; l < 4; ++l)
         if (!net->w[l]) return set_error(NFX_EINVAL, "made_pack: layer %d weight is null", l);
@@ -222,10 +225,17 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
                        void* workspace, hipStream_t s) {
     const bool fused = sums != nullptr;
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine: bad shape");
-    if (d > 4096 || H > 128) return set_error(NFX_EUNSUPPORTED, "made_affine: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (d > 4096 || H > 256) return set_error(NFX_EUNSUPPORTED, "made_affine: d=%d H=%d outside d<=4096, H<=256", d, H);
     if (variant < NFX_MAF_INVERSE || variant > NFX_IAF_INVERSE)
         return set_error(NFX_EINVAL, "made_affine: unknown variant %d", variant);
     const int HT = (H + 31) / 32;
+    if (HT > 4) {  // 128 < H <= 256: nfx_made_big.hip (no fused log_prob epilogue)
+        if (fused) return set_error(NFX_EUNSUPPORTED, "made_affine_logprob: no fused log_prob for H=%d > 128", H);
+        if (B == 0) return NFX_OK;
+        if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "made_affine: null pointer");
+        if (in == out) return set_error(NFX_EINVAL, "made_affine: in and out must not alias");
+        return made_big_launch(packed, in, out, log_det, B, d, H, variant, accumulate, s);
+    }
     const MadeLayout L = made_layout(d, HT);
     const bool parallel = variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD;
     const size_t wide_lds_bytes = (size_t)wide_lds(L, HT).total * sizeof(float);

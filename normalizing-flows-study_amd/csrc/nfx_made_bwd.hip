@@ -672,8 +672,8 @@ using namespace nfx;
 
 extern "C" int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
     if (!net || !packed) return set_error(NFX_EINVAL, "made_pack_backward: null pointer");
-    if (d <= 0 || d > 4096 || H <= 0 || H > 128)
-        return set_error(NFX_EUNSUPPORTED, "made_pack_backward: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (d <= 0 || d > 4096 || H <= 0 || H > 256)
+        return set_error(NFX_EUNSUPPORTED, "made_pack_backward: d=%d H=%d outside d<=4096, H<=256", d, H);
     const MadeLayout L = made_layout(d, (H + 31) / 32);
     int blocks = (L.total - L.t4 + 255) / 256;
     if (blocks > 1024) blocks = 1024;

@@ -25,7 +25,8 @@ import torch.nn.functional as F
 from .. import _lib
 from .flow import HipFlow
 
-MAX_H = 128
+MAX_H = 256       # eval kernels (H > 128: nfx_made_big.hip)
+MAX_H_BWD = 128   # fused backward kernels; wider layers differentiate through the composite
 MAX_D = 4096
 # Profiling hook (bench.py): when set to a list, every fused backward launch appends
 # (name, start, end) HIP events recorded on the launch stream around the kernel.
@@ -158,7 +159,7 @@ class _MadeAffineFlow(HipFlow):
         d, H = self.dim, self.conditioner.hidden_dim
         # parallel directions: made_bwd_kernel (d, H <= 64) / made_bwdw_kernel; sequential
         # directions: made_seq_bwd_kernel
-        return d <= MAX_D and H <= MAX_H
+        return d <= MAX_D and H <= MAX_H_BWD
 
     def _hip_backward(self, x, gz, gld, direction):
         """dL/dx and the parameter gradients (in self.parameters() order) of one call."""

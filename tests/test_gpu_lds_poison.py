@@ -66,11 +66,14 @@ def _model(kind):
         return _perturb(nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)]), 0.02, 10), 784
     if kind == "arqs":
         return _perturb(nfs_amd.NormalizingFlowModel([nfs_amd.ARQS(6, 64, num_bins=8) for _ in range(2)]), 0.05, 11), 6
+    if kind == "made_h256":
+        return _perturb(nfs_amd.NormalizingFlowModel(
+            [nfs_amd.MaskedAutoregressiveFlow(70, 256), nfs_amd.InverseAutoregressiveFlow(70, 256)]), 0.02, 12), 70
     raise ValueError(kind)
 
 
 KINDS = ["realnvp", "affine_d16", "spline", "maf63", "maf80_wide", "iaf150", "realnvp_bn_between",
-         "spline_d16", "maf100_h128", "iaf784", "arqs"]
+         "spline_d16", "maf100_h128", "iaf784", "arqs", "made_h256"]
 
 
 @pytest.mark.parametrize("kind", KINDS)

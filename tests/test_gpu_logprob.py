@@ -64,6 +64,12 @@ def _model(kind):
     if kind == "iaf150_sequential":
         fl = [nfs_amd.InverseAutoregressiveFlow(150, 64) for _ in range(2)]
         return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 9), 150, True
+    if kind == "maf40_h256":
+        fl = [nfs_amd.MaskedAutoregressiveFlow(40, 256) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 11), 40, False
+    if kind == "iaf90_h192_sequential":
+        fl = [nfs_amd.InverseAutoregressiveFlow(90, 192) for _ in range(2)]
+        return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 12), 90, False
     if kind == "iaf20_h96_sequential":
         fl = [nfs_amd.InverseAutoregressiveFlow(20, 96) for _ in range(2)]
         return _perturb(nfs_amd.NormalizingFlowModel(fl), 0.02, 10), 20, False
@@ -72,7 +78,7 @@ def _model(kind):
 
 KINDS = ["realnvp", "realnvp_bn_between", "affine_d5_h96", "spline_k5", "maf63",
          "maf80_wide", "maf100_h128_chunked", "iaf10_sequential", "iaf150_sequential",
-         "iaf20_h96_sequential"]
+         "iaf20_h96_sequential", "maf40_h256", "iaf90_h192_sequential"]
 
 
 @pytest.mark.parametrize("kind", KINDS)

@@ -92,7 +92,10 @@ def test_small_made_flows(cuda_device, name, kind):
 
 @pytest.mark.parametrize("d,H,B", [(5, 16, 1), (33, 32, 65), (63, 96, 130), (100, 128, 257), (7, 64, 1000),
                                    (65, 64, 129), (100, 32, 700), (200, 64, 1500), (784, 64, 77),
-                                   (300, 16, 33), (130, 48, 70), (129, 64, 35)])
+                                   (300, 16, 33), (130, 48, 70), (129, 64, 35),
+                                   # 128 < H <= 256: nfx_made_big.hip
+                                   (5, 256, 70), (63, 160, 100), (100, 256, 65), (300, 256, 33), (2, 200, 40),
+                                   (64, 129, 97)])
 def test_made_shapes_vs_oracle(cuda_device, d, H, B):
     torch.manual_seed(d * 31 + H)
     for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
@@ -111,7 +114,7 @@ def test_made_shapes_vs_oracle(cuda_device, d, H, B):
             assert_ld(lg.cpu(), lr, 5e-4)
 
 
-@pytest.mark.parametrize("d,H", [(6, 16), (100, 64)])
+@pytest.mark.parametrize("d,H", [(6, 16), (100, 64), (40, 224)])
 def test_made_nonfinite_inputs(cuda_device, d, H):
     """inf/NaN rows: parallel directions propagate 0*inf = NaN through the dense masked weights;
     sequential directions reproduce the reference's contamination of every later step."""

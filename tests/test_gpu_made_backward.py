@@ -178,3 +178,22 @@ def test_iaf_density_training_step(cuda_device):
     assert abs(loss.item() - l64.item()) <= 1e-5 * (1 + abs(l64.item()))
     for (k, p), (_, p64) in zip(mg.named_parameters(), m64.named_parameters()):
         _check(p.grad, p64.grad, 5e-5)
+
+
+@pytest.mark.parametrize("cls", [nfs_amd.MaskedAutoregressiveFlow, nfs_amd.InverseAutoregressiveFlow])
+def test_wide_hidden_training_step(cuda_device, cls):
+    """H = 256 (outside the fused backward kernels' H <= 128): the forward runs nfx_made_big.hip,
+    autograd recomputes through the layer's composite; loss and gradients match float64."""
+    torch.manual_seed(5)
+    flows = [_flow(cls, 10, 256, 70 + k) for k in range(2)]
+    model = nfs_amd.NormalizingFlowModel(flows)
+    m64 = copy.deepcopy(model).double()
+    x = torch.randn(300, 10, generator=torch.Generator().manual_seed(4))
+    l64 = -m64.log_prob(x.double()).mean()
+    l64.backward()
+    mg = model.to(cuda_device)
+    loss = -mg.log_prob(x.to(cuda_device)).mean()
+    loss.backward()
+    assert abs(loss.item() - l64.item()) <= 1e-5 * (1 + abs(l64.item()))
+    for (k, p), (_, p64) in zip(mg.named_parameters(), m64.named_parameters()):
+        _check(p.grad, p64.grad, 5e-5)
