@@ -159,13 +159,14 @@ int nfx_arqs(const float* packed, const float* in, float* out, float* log_det, i
  * (inverse_autoregressive_flow.py:30-103). net: 4 masked layers, output order [mu | alpha].
  * variant: NFX_MAF_INVERSE / NFX_IAF_FORWARD (parallel, MFMA) or
  *          NFX_MAF_FORWARD / NFX_IAF_INVERSE (sequential over d).
+ * Shapes: d <= 4096, H <= 256 (NFX_EUNSUPPORTED beyond).
  * ------------------------------------------------------------------------------------- */
 size_t nfx_made_packed_floats(int d, int H);
 int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
 int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
                     int64_t B, int d, int H, int variant, int accumulate, void* stream);
 /* Density direction + fused log_prob epilogue (see nfx_affine_coupling_logprob):
- * NFX_MAF_INVERSE with d <= 64 or H <= 64, NFX_IAF_INVERSE (sequential) with H <= 64;
+ * NFX_MAF_INVERSE with d <= 64 or H <= 64 (and H <= 128), NFX_IAF_INVERSE (sequential) with H <= 64;
  * NFX_EUNSUPPORTED otherwise (use nfx_gauss_logprob after nfx_made_affine). */
 int nfx_made_affine_logprob(const float* packed, const float* in, float* out, float* log_det,
                             float* logp, double* sums, void* workspace, int64_t B, int d, int H,
@@ -175,7 +176,7 @@ int nfx_made_affine_logprob(const float* packed, const float* in, float* out, fl
  * Training: backward of the PARALLEL MADE directions under autograd —
  * MaskedAutoregressiveFlow.inverse (masked_autoregressive_flow.py:18-44, the density-training
  * direction; variant NFX_MAF_INVERSE) and InverseAutoregressiveFlow.forward
- * (inverse_autoregressive_flow.py:30-63; NFX_IAF_FORWARD) — for d <= 64, H <= 64 and no
+ * (inverse_autoregressive_flow.py:30-63; NFX_IAF_FORWARD) — for d <= 4096, H <= 128 and no
  * BatchNorm (NFX_EUNSUPPORTED otherwise).
  * nfx_made_pack_backward adds the transposed weight tiles to a packed image built by
  * nfx_made_pack (same buffer). nfx_made_affine_backward recomputes the layer and writes
