@@ -104,6 +104,15 @@ __device__ __forceinline__ float dpp(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+// out[c] = v of lane c of this lane's 16-lane DPP row (row_newbcast:c, GFX90A+ encoding 0x150 + c).
+template <int C = 0>
+__device__ __forceinline__ void seqs_row_bcast16(float v, float (&out)[16]) {
+    if constexpr (C < 16) {
+        out[C] = dpp<0x150 + C>(v);
+        seqs_row_bcast16<C + 1>(v, out);
+    }
+}
+
 // Sum over the 16 lanes of a DPP row; every lane of the row ends with the total.
 __device__ __forceinline__ float row16_allsum(float v) {
     v = v + dpp<0xB1>(v);   // quad xor 1
@@ -258,7 +267,6 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     float* xin_t = lds + S.wv + wave * kSeqsTile;  // [4][64] inputs of the block
     float* zout_t = xin_t + 4 * kSeqsStep;         // [4][64] guarded outputs of the block
     float* at_t = zout_t + 4 * kSeqsStep;          // [4][64] clamped alphas of the block
-    float* cv_t = at_t + 4 * kSeqsStep;            // [4][16] chunk: raw values (MADE inputs)
     const int nblk = (d + kSeqsStep - 1) / kSeqsStep;
     // staged-row columns of this lane: w1t rows by position l % Hp; w4 rows interleave
     // (mu, alpha) per position, instruction `half` of a row covers positions 32 half + l / 2
@@ -410,19 +418,15 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 }
                 if constexpr (VAR == NFX_MAF_FORWARD) vo = nonfinite(vi) ? 0.f : vi;
                 else vo = nonfinite(vi) ? xin : vi;
-                cv_t[slot * 16 + sub] = vj ? vi : 0.f;
                 if (vj) {
                     zout_t[slot * kSeqsStep + rj] = vo;
                     at_t[slot * kSeqsStep + rj] = a;
                 }
-                seqs_lds_order();
+                // every lane of the row needs the chunk's 16 values: DPP row broadcasts
+                // (row_newbcast:c), no LDS round trip on the chunk's critical path
+                const float cvl = vj ? vi : 0.f;
                 float cv[16];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const f32x4 tv = *reinterpret_cast<const f32x4*>(cv_t + slot * 16 + 4 * q);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) cv[4 * q + c] = tv[c];
-                }
+                seqs_row_bcast16(cvl, cv);
                 // 3. rank-1 updates of the incomplete slots' layer-1 pre-activations, step order
                 const float* w1r = w1b + ii * Hp + sub * UPL;
                 const int kc3 = gi >> 4;
