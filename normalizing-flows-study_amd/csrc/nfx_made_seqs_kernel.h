@@ -196,16 +196,12 @@ __device__ __forceinline__ void seqs_dots(const float* w4r, const int (&offs)[16
 }
 
 // Step 3 for slots k >= K0 (the others are completed in every lane): pre1 += W1t[i] * v_i in
-// step order; w1r = this lane's slot 0 of step ii's row; pairs of slots as packed FMAs. Rows
-// read ahead of use as in seqs_dots.
+// step order, pairs of slots as packed FMAs. w = this lane's slots of the chunk's 16 W1t rows,
+// read before steps 1-2 finish (they depend only on the chunk position), so their LDS latency
+// hides behind the reduce-scatter and the affine map.
 template <int K0, int UPL>
-__device__ __forceinline__ void seqs_rank1(const float* w1r, int Hp, const float (&cv)[16],
+__device__ __forceinline__ void seqs_rank1(const float (&w)[16][UPL], const float (&cv)[16],
                                            f32x2 (&pre1)[UPL / 2]) {
-    constexpr int NW = UPL - K0;
-    float w[16][UPL];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) seqs_slots<K0, NW, UPL>(w1r + j * Hp, w[j]);
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         if constexpr (K0 % 2 == 1) pre1[K0 / 2][1] = fmaf(w[j][K0], cv[j], pre1[K0 / 2][1]);
@@ -383,6 +379,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                     case 3: if constexpr (UPL >= 3) seqs_dots<(UPL >= 3 ? 3 : 1), UPL>(w4r, offs, h3v, pm, pa); break;
                     default: seqs_dots<UPL, UPL>(w4r, offs, h3v, pm, pa); break;
                 }
+                // step-3 rows now: their LDS latency overlaps the reductions and step 2
+                float w1v[16][UPL];
+                {
+                    const float* w1r = w1b + ii * Hp + sub * UPL;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) seqs_slots<0, UPL, UPL>(w1r + j * Hp, w1v[j]);
+                }
                 row16_reduce_scatter(pm);
                 row16_reduce_scatter(pa);
                 // 2. lane sub evaluates step ii + sub (lanes past the chunk compute garbage, unused)
@@ -428,13 +431,12 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 float cv[16];
                 seqs_row_bcast16(cvl, cv);
                 // 3. rank-1 updates of the incomplete slots' layer-1 pre-activations, step order
-                const float* w1r = w1b + ii * Hp + sub * UPL;
                 const int kc3 = gi >> 4;
                 switch (kc3 < UPL ? kc3 : UPL) {
-                    case 0: seqs_rank1<0, UPL>(w1r, Hp, cv, pre1); break;
-                    case 1: seqs_rank1<1, UPL>(w1r, Hp, cv, pre1); break;
-                    case 2: if constexpr (UPL > 2) seqs_rank1<2, UPL>(w1r, Hp, cv, pre1); break;
-                    case 3: if constexpr (UPL > 3) seqs_rank1<3, UPL>(w1r, Hp, cv, pre1); break;
+                    case 0: seqs_rank1<0, UPL>(w1v, cv, pre1); break;
+                    case 1: seqs_rank1<1, UPL>(w1v, cv, pre1); break;
+                    case 2: if constexpr (UPL > 2) seqs_rank1<2, UPL>(w1v, cv, pre1); break;
+                    case 3: if constexpr (UPL > 3) seqs_rank1<3, UPL>(w1v, cv, pre1); break;
                     default: break;
                 }
                 seqs_lds_order();  // the chunk tile is rewritten by the next chunk
