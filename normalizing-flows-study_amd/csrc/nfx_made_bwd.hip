@@ -141,7 +141,7 @@ __device__ __forceinline__ bool tiles_finite(const f32x16* t) {
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
-constexpr int kBwdWaves = 8;  // 2 per SIMD; weights are read from L2, LDS holds the tiles
+constexpr int kBwdWaves = 8;  // 2 per SIMD; LDS: the forward weight image + one x tile per wave
 
 template <int HT, int VAR>
 __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
@@ -152,10 +152,16 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     constexpr int S = kTileStride;
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
+    // the forward (parallel) weight image is LDS-resident for the recompute (83 KB at d = 63,
+    // H = 64); the transposed tiles of the data-gradient chain stay in L2
+    {
+        const f32x4* src = reinterpret_cast<const f32x4*>(packed);
+        for (int i = threadIdx.x; i < L.par_total / 4; i += 64 * kBwdWaves) lds4[i] = src[i];
+    }
+    __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* xt = lds + wave * 2 * 32 * S;  // x tile, then gz tile
-    float* gt = xt + 32 * S;
-    const float* W = packed;
+    float* xt = lds + L.par_total + wave * 32 * S;  // x tile; later the direct dL/dx term
+    const float* W = lds;
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
     const int voff = lane < d ? lane * 4 : (1 << 30);
     const int rowb = d * 4;
@@ -203,13 +209,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         float xmax = 0.f;
         {
             const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + base * d, 0, rows * rowb, 0x00020000);
-            const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gout) + base * d, 0, rows * rowb, 0x00020000);
 #pragma unroll
             for (int r = 0; r < 32; ++r) {
                 const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff, r * rowb, 0));
                 xt[r * S + lane] = xv;
                 xmax = tmax(xmax, fabsf(xv));  // NaN-propagating: a NaN fails the test
-                gt[r * S + lane] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, voff, r * rowb, 0));
             }
         }
         // Skip structurally-zero blocks only when the tile's inputs are finite and within the
@@ -300,15 +304,30 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         if (!(ld1 >= -LDLIM && ld1 <= LDLIM)) gld1 = 0.f;
         const float gld1s = __shfl(gld1, col, 64);  // both lane halves of sample col
 
-        // epilogue backward; the direct dz/dx term replaces x in the tile (same lane, same slot)
+        // epilogue backward; the direct dz/dx term replaces x in the tile (same lane, same slot).
+        // dL/dz in accumulator layout straight from global: lane (col, h), block j holds dims
+        // 32j + 8q + 4h + 0..3 of sample col -> four 16-byte loads (range check: rows >= B read 0;
+        // dims >= d belong to the next row and are zeroed)
+        const auto rgz = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gout) + base * d, 0, rows * rowb,
+                                                           0x00020000);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
+            float gzr[16];
+            if (j < NJ) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int dim0 = 32 * j + 8 * q + 4 * h;
+                    const auto u = __builtin_amdgcn_raw_buffer_load_b128(rgz, col * rowb + dim0 * 4, 0, 0);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) gzr[4 * q + e] = dim0 + e < d ? __uint_as_float(u[e]) : 0.f;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int dim = 32 * j + crow(r, h);
                 float* px = xt + col * S + dim;
                 const float xv = *px;
-                const float gz = gt[col * S + dim];
+                const float gz = j < NJ ? gzr[r] : 0.f;
                 const float alpha = d4[2 * j + 1][r];
                 if constexpr (IAF) {
                     // inverse_autoregressive_flow.py:39-54: y = x exp(clamp(a,-2,2)) + clamp(mu,-10,10),
@@ -718,7 +737,7 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
         return check_launch("made_bwdw_kernel");
     }
     const MadeLayout L = made_layout(d, HT);
-    const size_t lds = (size_t)kBwdWaves * 2 * 32 * kTileStride * sizeof(float);
+    const size_t lds = ((size_t)L.par_total + (size_t)kBwdWaves * 32 * kTileStride) * sizeof(float);
     const bool iaf = variant == NFX_IAF_FORWARD;
     const void* k = HT == 1 ? (iaf ? (const void*)made_bwd_kernel<1, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<1, NFX_MAF_INVERSE>)
                             : (iaf ? (const void*)made_bwd_kernel<2, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<2, NFX_MAF_INVERSE>);
