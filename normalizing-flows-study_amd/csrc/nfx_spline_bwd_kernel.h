@@ -58,95 +58,111 @@ __host__ __device__ constexpr SplineGrad spline_grad_layout(int HT, int NTMAX) {
 }
 
 // Spline forward + adjoint for one element (the reference's _rational_quadratic_spline per
-// element and its autograd): given the input v, the 3K-1 raw parameters p[], the upstream
-// gradients go (output) and gl (log-det), returns the spline output (after the spline-level
-// guard), gp[] = dL/dp and gv = dL/dv.
+// element and its autograd), split over the two lane halves that hold the same sample: lane half
+// h owns one SIDE of the spline — h = 0 the bin widths, h = 1 the bin heights (softmax, min-width
+// affine and clamp, knot cumsum, knot differences, and all of their backward) — and the
+// derivative logits of parity h (softplus forward and backward). The gathered bin quantities and
+// the searched side's bin index are exchanged with one v_permlane32_swap each; the scalar RQ map
+// and its adjoint run on both halves (same data, same instructions). Every value goes through
+// exactly the operations of the unsplit formulation, so the results are bit-identical to it.
+// Given the input v, the 3K-1 raw parameters p[] (all of them, on both halves), the upstream
+// gradients go (output) and gl (log-det): out = the spline output (after the spline-level guard),
+// gv = dL/dv, gs[k] = dL/dp[h*K + k] (this half's side), gd[t] = dL/dp[2K + 2t + h].
 template <int K, bool INV>
 __device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32], const SplineConsts& C,
-                                                  float go, float gl, float& out, float (&gp)[32], float& gv) {
+                                                  float go, float gl, float& out, float (&gs)[K],
+                                                  float (&gd)[K / 2], float& gv) {
 #pragma clang fp contract(off)
+    constexpr int ND = K / 2;  // derivative logits per half: k = 2t + h < K - 1
     const float eps = 1e-8f;
     const float B = C.bound;
+    const bool hi = (threadIdx.x & 32) != 0;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) gp[i] = 0.f;
+    for (int k = 0; k < K; ++k) gs[k] = 0.f;
+#pragma unroll
+    for (int t = 0; t < ND; ++t) gd[t] = 0.f;
     out = v;
     gv = go;  // identity outside [-B, B] (and the spline-level guard's fallback)
     if (!(v >= -B && v <= B)) return;
+    // per-half selects between two parameters: the operands pass through an empty asm first, so
+    // the select stays a select of VALUES (a select between two elements of an array would
+    // otherwise become a select of addresses and send the array to scratch)
+    auto pick = [&](int i0, int i1) -> float {
+        float a = p[i0], b = p[i1];
+        asm volatile("" : "+v"(a), "+v"(b));
+        return hi ? b : a;
+    };
 
-    // ---- forward, keeping what the adjoint needs (same arithmetic as rq_spline_elem) ----
-    float sw[K], sh[K], wpre[K], hpre[K], w[K], h[K], cwk[K + 1], chk[K + 1], wd[K], hd[K], dk[K + 1], dpre[K];
+    // ---- this half's side, forward (same arithmetic as rq_spline_elem) ----
+    float sm[K], pre[K], val[K], knot[K + 1], wd[K];
     {
-        float m = p[0];
+        float u[K];
 #pragma unroll
-        for (int k = 1; k < K; ++k) m = tmax(m, p[k]);
-        float s = 0.f;
+        for (int k = 0; k < K; ++k) u[k] = pick(k, K + k);
+        const float mins = hi ? C.min_h : C.min_w, cs = hi ? C.ch : C.cw;
+        float m = u[0];
 #pragma unroll
-        for (int k = 0; k < K; ++k) { sw[k] = exp_safe(p[k] - m); s = s + sw[k]; }
-        const float inv = 1.f / s;
+        for (int k = 1; k < K; ++k) m = tmax(m, u[k]);
+        float ssum = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) { sm[k] = exp_safe(u[k] - m); ssum = ssum + sm[k]; }
+        const float inv = 1.f / ssum;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            sw[k] = sw[k] * inv;
-            wpre[k] = C.min_w + C.cw * sw[k];
-            w[k] = tclamp_min(wpre[k], eps);
+            sm[k] = sm[k] * inv;
+            pre[k] = mins + cs * sm[k];
+            val[k] = tclamp_min(pre[k], eps);
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            acc += (double)val[k];
+            knot[k + 1] = C.two_bound * (float)acc + (-B);
+        }
+        knot[0] = -B;
+        knot[K] = B;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            wd[k] = knot[k + 1] - knot[k];
+            val[k] = tclamp_min(wd[k], eps);
         }
     }
-    {
-        float m = p[K];
-#pragma unroll
-        for (int k = 1; k < K; ++k) m = tmax(m, p[K + k]);
-        float s = 0.f;
-#pragma unroll
-        for (int k = 0; k < K; ++k) { sh[k] = exp_safe(p[K + k] - m); s = s + sh[k]; }
-        const float inv = 1.f / s;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            sh[k] = sh[k] * inv;
-            hpre[k] = C.min_h + C.ch * sh[k];
-            h[k] = tclamp_min(hpre[k], eps);
-        }
-    }
-    {
-        double aw = 0.0, ah = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            aw += (double)w[k];
-            ah += (double)h[k];
-            cwk[k + 1] = C.two_bound * (float)aw + (-B);
-            chk[k + 1] = C.two_bound * (float)ah + (-B);
-        }
-        cwk[0] = -B; cwk[K] = B;
-        chk[0] = -B; chk[K] = B;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            wd[k] = cwk[k + 1] - cwk[k];
-            hd[k] = chk[k + 1] - chk[k];
-            w[k] = tclamp_min(wd[k], eps);
-            h[k] = tclamp_min(hd[k], eps);
-        }
-    }
+    // ---- derivatives: this half computes k = 2t + h, then both halves hold all of them ----
+    float dpre[ND], dk[K + 1];
     dk[0] = 1.f;
     dk[K] = 1.f;
 #pragma unroll
-    for (int k = 0; k < K - 1; ++k) {
-        dpre[k] = C.min_d + tsoftplus(p[2 * K + k]);
-        dk[k + 1] = tclamp_min(dpre[k], eps);
+    for (int t = 0; t < ND; ++t) {
+        const int k0 = 2 * t, k1 = 2 * t + 1;  // this half's k is k0 (h = 0) or k1 (h = 1)
+        const float uu = pick(2 * K + k0, 2 * K + (k1 < K - 1 ? k1 : k0));
+        dpre[t] = C.min_d + tsoftplus(uu);
+        const float mine = tclamp_min(dpre[t], eps);
+        const float other = halves_other(mine, mine);
+        dk[k0 + 1] = hi ? other : mine;
+        if (k1 < K - 1) dk[k1 + 1] = hi ? mine : other;
     }
+    // ---- bin: counted on the searched side's knots (heights when inverting) ----
     int cnt = 0;
 #pragma unroll
-    for (int k = 0; k <= K; ++k) cnt += ((INV ? chk[k] : cwk[k]) <= v) ? 1 : 0;
+    for (int k = 0; k <= K; ++k) cnt += (knot[k] <= v) ? 1 : 0;
+    {
+        const int cnt_other = __float_as_int(halves_other(__int_as_float(cnt), __int_as_float(cnt)));
+        cnt = (hi == INV) ? cnt : cnt_other;
+    }
     int bin = cnt - 1;
     bin = bin < 0 ? 0 : (bin > K - 1 ? K - 1 : bin);
-    float w_k = w[0], x_k = cwk[0], h_k = h[0], y_k = chk[0], d_k = dk[0], d_k1 = dk[1];
+    float vb = val[0], kb = knot[0], d_k = dk[0], d_k1 = dk[1];
 #pragma unroll
     for (int k = 1; k < K; ++k) {
         const bool s = (k == bin);
-        w_k = s ? w[k] : w_k;
-        x_k = s ? cwk[k] : x_k;
-        h_k = s ? h[k] : h_k;
-        y_k = s ? chk[k] : y_k;
+        vb = s ? val[k] : vb;
+        kb = s ? knot[k] : kb;
         d_k = s ? dk[k] : d_k;
         d_k1 = s ? dk[k + 1] : d_k1;
     }
+    const float vo = halves_other(vb, vb), ko = halves_other(kb, kb);
+    const float w_k = hi ? vo : vb, x_k = hi ? ko : kb;
+    const float h_k = hi ? vb : vo, y_k = hi ? kb : ko;
     const float wc = tclamp_min(w_k, eps);
     const float s_k = h_k / wc;
 
@@ -224,34 +240,34 @@ __device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32],
             g_d0 -= lam * hD * A * (1.f - R);
             g_d1 += lam * hD * R * A;
         } else {
-        // xp = 2c / den
-        float g_c = g_xp * 2.f / den;
-        const float g_den = -g_xp * (2.f * c) / (den * den);
-        const float g_den0 = small ? 0.f : g_den;
-        float g_b = -g_den0;
-        const float g_sq = -g_den0;
-        const float g_disc = g_sq / (2.f * sq);
-        const float g_dpr = dpr >= 0.f ? g_disc : 0.f;
-        g_b += g_dpr * (2.f * b);
-        const float g_a = -4.f * c * g_dpr;
-        g_c += -4.f * a * g_dpr;
-        // c = -s dy ; b = h d0 - dy T ; a = dy T + h (s - d0)
-        g_s += -g_c * dy;
-        float g_dy = -g_c * s_k;
-        g_h += g_b * d_k;
-        g_d0 += g_b * h_k;
-        g_dy -= g_b * T;
-        float g_T = -g_b * dy;
-        g_dy += g_a * T;
-        g_T += g_a * dy;
-        g_h += g_a * (s_k - d_k);
-        g_s += g_a * h_k;
-        g_d0 -= g_a * h_k;
-        g_d0 += g_T;
-        g_d1 += g_T;
-        g_s -= 2.f * g_T;
-        g_v += g_dy;
-        g_y -= g_dy;
+            // xp = 2c / den
+            float g_c = g_xp * 2.f / den;
+            const float g_den = -g_xp * (2.f * c) / (den * den);
+            const float g_den0 = small ? 0.f : g_den;
+            float g_b = -g_den0;
+            const float g_sq = -g_den0;
+            const float g_disc = g_sq / (2.f * sq);
+            const float g_dpr = dpr >= 0.f ? g_disc : 0.f;
+            g_b += g_dpr * (2.f * b);
+            const float g_a = -4.f * c * g_dpr;
+            g_c += -4.f * a * g_dpr;
+            // c = -s dy ; b = h d0 - dy T ; a = dy T + h (s - d0)
+            g_s += -g_c * dy;
+            float g_dy = -g_c * s_k;
+            g_h += g_b * d_k;
+            g_d0 += g_b * h_k;
+            g_dy -= g_b * T;
+            float g_T = -g_b * dy;
+            g_dy += g_a * T;
+            g_T += g_a * dy;
+            g_h += g_a * (s_k - d_k);
+            g_s += g_a * h_k;
+            g_d0 -= g_a * h_k;
+            g_d0 += g_T;
+            g_d1 += g_T;
+            g_s -= 2.f * g_T;
+            g_v += g_dy;
+            g_y -= g_dy;
         }
     } else {
         const float xp = (v - x_k) / wc;
@@ -316,66 +332,89 @@ __device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32],
     out = nonfinite(o) ? v : o;
     gv = g_v;
 
-    // ---- scatter the gathered gradients back to the bin arrays ----
-    float gw[K], gh[K], gcw[K + 1], gch[K + 1], gdk[K + 1];
+    // ---- this half's side: scatter to the bin arrays, knot differences, cumsum, softmax ----
+    const float g_val = hi ? g_h : g_w, g_knot = hi ? g_y : g_x;
+    float gval[K], gc[K + 1];
 #pragma unroll
     for (int k = 0; k <= K; ++k) {
-        const bool s0 = (k == bin), s1 = (k == bin + 1);
-        if (k < K) {
-            gw[k] = s0 ? g_w : 0.f;
-            gh[k] = s0 ? g_h : 0.f;
-        }
-        gcw[k] = s0 ? g_x : 0.f;
-        gch[k] = s0 ? g_y : 0.f;
-        gdk[k] = s0 ? g_d0 : (s1 ? g_d1 : 0.f);
+        const bool s0 = (k == bin);
+        if (k < K) gval[k] = s0 ? g_val : 0.f;
+        gc[k] = s0 ? g_knot : 0.f;
     }
-    // w = clamp(diff(cw), eps): the knot differences
+    // val = clamp(diff(knot), eps): the knot differences
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const float a = wd[k] >= eps ? gw[k] : 0.f;
-        gcw[k + 1] += a;
-        gcw[k] -= a;
-        const float b = hd[k] >= eps ? gh[k] : 0.f;
-        gch[k + 1] += b;
-        gch[k] -= b;
+        const float a = wd[k] >= eps ? gval[k] : 0.f;
+        gc[k + 1] += a;
+        gc[k] -= a;
     }
-    // knots 0 and K are pinned (in-place assignment): no gradient. cw_j = 2B cumsum_{i<j} w'_i - B.
-    float gwp[K], ghp[K];
+    // knots 0 and K are pinned (in-place assignment): no gradient. knot_j = 2B cumsum_{i<j} val'_i - B.
+    float gpv[K];
     {
-        float aw = 0.f, ah = 0.f;
+        float a = 0.f;
 #pragma unroll
         for (int i = K - 1; i >= 0; --i) {
-            gwp[i] = aw;
-            ghp[i] = ah;
-            if (i >= 1) {
-                aw += C.two_bound * gcw[i];
-                ah += C.two_bound * gch[i];
-            }
+            gpv[i] = a;
+            if (i >= 1) a += C.two_bound * gc[i];
         }
     }
-    // w' = clamp(min_w + cw * softmax(u), eps) -> softmax backward
+    // val' = clamp(min + c * softmax(u), eps) -> softmax backward
     {
-        float dotw = 0.f, doth = 0.f;
+        const float cs = hi ? C.ch : C.cw;
+        float dot = 0.f;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            gwp[k] = wpre[k] >= eps ? gwp[k] * C.cw : 0.f;
-            ghp[k] = hpre[k] >= eps ? ghp[k] * C.ch : 0.f;
-            dotw += gwp[k] * sw[k];
-            doth += ghp[k] * sh[k];
+            gpv[k] = pre[k] >= eps ? gpv[k] * cs : 0.f;
+            dot += gpv[k] * sm[k];
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            gp[k] = sw[k] * (gwp[k] - dotw);
-            gp[K + k] = sh[k] * (ghp[k] - doth);
-        }
+        for (int k = 0; k < K; ++k) gs[k] = sm[k] * (gpv[k] - dot);
     }
     // derivatives: d_{k+1} = clamp(min_d + softplus(u_k), eps); ends padded with 1 (no gradient)
 #pragma unroll
-    for (int k = 0; k < K - 1; ++k) {
-        const float u = p[2 * K + k];
+    for (int t = 0; t < ND; ++t) {
+        const int k0 = 2 * t, k1 = 2 * t + 1;
+        const int k = hi ? k1 : k0;
+        if (hi && k1 >= K - 1) continue;
+        const float u = pick(2 * K + k0, 2 * K + (k1 < K - 1 ? k1 : k0));
         const float z = exp_safe(u);
         const float sp = u > 20.f ? 1.f : z / (z + 1.f);
-        gp[2 * K + k] = dpre[k] >= eps ? gdk[k + 1] * sp : 0.f;
+        const float gdk = (k + 1 == bin) ? g_d0 : ((k + 1 == bin + 1) ? g_d1 : 0.f);
+        gd[t] = dpre[t] >= eps ? gdk * sp : 0.f;
+    }
+}
+
+// delta3 of a parameter tile in accumulator layout from the split adjoint: lane (col, h),
+// register r needs row R = crow(r, h) of sample col. Rows < K are held by the h = 0 half (widths),
+// K..2K-1 by h = 1 (heights), derivative row 2K + k by half k & 1; each lane sends the partner the
+// rows it holds that the partner needs (one v_permlane32_swap per register).
+template <int K>
+__device__ __forceinline__ void split_grads_to_tile(const float (&gs)[K], const float (&gd)[K / 2], f32x16& e) {
+    const bool hi = (threadIdx.x & 32) != 0;
+    auto held = [&](int R, bool as_hi) -> float {  // value this lane holds for row R (0 if none)
+        if (R < K) return as_hi ? 0.f : gs[R];
+        if (R < 2 * K) return as_hi ? gs[R - K] : 0.f;
+        if (R < 3 * K - 1) {
+            const int k = R - 2 * K;
+            return ((k & 1) == (as_hi ? 1 : 0)) ? gd[k >> 1] : 0.f;
+        }
+        return 0.f;
+    };
+    auto owns = [&](int R, bool as_hi) -> bool {
+        if (R < K) return !as_hi;
+        if (R < 2 * K) return as_hi;
+        if (R < 3 * K - 1) return ((R - 2 * K) & 1) == (as_hi ? 1 : 0);
+        return true;  // padding rows: zero, no exchange needed
+    };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int R0 = crow(r, 0), R1 = crow(r, 1);
+        // the partner (other half) needs its row for r: R1 if I am h = 0, R0 if I am h = 1
+        const float send = hi ? held(R0, true) : held(R1, false);
+        const float recv = halves_other(send, send);
+        const float mine = hi ? held(R1, true) : held(R0, false);
+        const bool own = hi ? owns(R1, true) : owns(R0, false);
+        e[r] = own ? mine : recv;
     }
 }
 
@@ -538,24 +577,17 @@ __global__ __launch_bounds__(256) void spline_bwd_kernel(
                     v = (j == dt) ? cur.xr[j] : v;
                     go = (j == dt) ? cur.gyr[j] : go;
                 }
-                float o, gp[32], gvs;
+                float o, gs[K], gd[K / 2], gvs;
                 // z_dt is non-finite only when the spline fell back to a non-finite input: the
                 // layer guard then blocks the output gradient
-#if NFX_SBWD_EXPT == 1
-                o = v; gvs = go;
-#pragma unroll
-                for (int i = 0; i < 32; ++i) gp[i] = prm[i] * go + cur.gl;
-#else
-                rq_spline_adjoint<K, INV>(v, prm, C, nonfinite(v) ? 0.f : go, cur.gl, o, gp, gvs);
-#endif
+                rq_spline_adjoint<K, INV>(v, prm, C, nonfinite(v) ? 0.f : go, cur.gl, o, gs, gd, gvs);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     zr[j] = (j == dt) ? o : zr[j];
                     gvx[j] = (j == dt) ? gvs : gvx[j];
                 }
                 f32x16 e;  // delta3 of tile t in accumulator layout
-#pragma unroll
-                for (int r = 0; r < 16; ++r) e[r] = h ? gp[crow(r, 1)] : gp[crow(r, 0)];
+                split_grads_to_tile<K>(gs, gd, e);
                 const f32x4* wt = reinterpret_cast<const f32x4*>(P + BL.w3t) + lane;
 #pragma unroll
                 for (int kt = 0; kt < HT; ++kt)
