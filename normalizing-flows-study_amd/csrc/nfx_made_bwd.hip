@@ -141,7 +141,104 @@ __device__ __forceinline__ bool tiles_finite(const f32x16* t) {
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
-constexpr int kBwdWaves = 8;  // 2 per SIMD; LDS: the forward weight image + one x tile per wave
+__host__ __device__ constexpr int NKC_(int d) { return (d + 31) / 32; }
+__host__ __device__ constexpr int NJ_(int d) { return (d + 31) / 32; }
+
+// ---- made_bwd_kernel's LDS weight image ----
+// The forward A-operand tiles ([rq][lane][4], 1024 floats) are copied into LDS with padding —
+// rq blocks 264 floats apart, the upper lane half shifted by 4 — so that they serve BOTH chains:
+// the forward recompute reads them as before (16-byte reads, contiguous per half wave), and the
+// data-gradient chain reads the TRANSPOSED tile from the same copy, one dword per MFMA k-step:
+// lane (i, kh) at step s needs W[row crow(s, kh)][col i] of the forward tile, which lives at
+//   (i >> 3) * 264 + ((i >> 2) & 1) * 132 + (i & 3) + 4 crow(s, kh)      (hidden / output layers,
+//   whose k index is the accumulator row crow(., .))
+//   (i >> 3) * 264 + (i & 1) * 132 + ((i >> 1) & 3) + 4 crow(s, kh)      (layer 1, k = 2 s + kh);
+// modulo 32 banks the lane-dependent part is 8a + 4c + b over the 32 lanes of a half: no
+// conflicts. No transposed image is read from L2 any more.
+constexpr int kPadRQ = 264, kPadH = 4, kPadTile = 4 * kPadRQ;
+struct BwdLds {
+    int w1, w2, w3, w4, b1, b2, b3, b4, x, total;
+};
+__host__ __device__ constexpr BwdLds bwd_lds(int d, int HT) {
+    const int NKC = (d + 31) / 32, NJ = NKC;
+    BwdLds b{};
+    int o = 0;
+    b.w1 = o; o += HT * NKC * kPadTile;
+    b.w2 = o; o += HT * HT * kPadTile;
+    b.w3 = o; o += HT * HT * kPadTile;
+    b.w4 = o; o += NJ * 2 * HT * kPadTile;
+    b.b1 = o; o += HT * 32;
+    b.b2 = o; o += HT * 32;
+    b.b3 = o; o += HT * 32;
+    b.b4 = o; o += NJ * 64;
+    b.x = (o + 3) & ~3;  // per-wave x tiles follow
+    b.total = b.x;
+    return b;
+}
+
+// hidden / output tile `tile` of a padded layer over its first NK k tiles (bias, MFMA chain)
+template <int HT, int NK>
+__device__ __forceinline__ f32x16 pad_tile(const float* wl, const float* bl, int hto, const f32x16 (&hin)[HT],
+                                           int lo, int h) {
+    f32x16 a = load_bias16(bl + hto * 32, h);
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+        const float* tp = wl + (hto * HT + kt) * kPadTile + lo;
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(tp + rq * kPadRQ);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], hin[kt][4 * rq + rr], a);
+        }
+    }
+    return a;
+}
+template <int HT, int N>
+__device__ __forceinline__ f32x16 pad_tile_n(int n, const float* wl, const float* bl, int hto, const f32x16 (&hin)[HT],
+                                             int lo, int h) {
+    if constexpr (N == 0) {
+        return pad_tile<HT, 0>(wl, bl, hto, hin, lo, h);
+    } else {
+        if (n >= N) return pad_tile<HT, N>(wl, bl, hto, hin, lo, h);
+        return pad_tile_n<HT, N - 1>(n, wl, bl, hto, hin, lo, h);
+    }
+}
+template <int HT>
+__device__ __forceinline__ void pad_hidden(const float* wl, const float* bl, const f32x16 (&hin)[HT], f32x16 (&hout)[HT],
+                                           const int (&nk)[HT], bool dense, int lo, int h) {
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a = pad_tile_n<HT, HT>(dense ? HT : nk[hto], wl, bl, hto, hin, lo, h);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+        hout[hto] = a;
+    }
+}
+
+// transposed chain: acc += sum over k tiles kt in [K0, NK) of (forward tile kt * stride + ot)^T
+// . bt[kt]; `tb` = this lane's transposed-read base inside a tile (see above)
+template <int NK, int K0>
+__device__ __forceinline__ f32x16 tchain_k(const float* wl, int stride, int ot, int tb, const f32x16* bt, f32x16 acc) {
+#pragma unroll
+    for (int kt = K0; kt < NK; ++kt) {
+        const float* tp = wl + (kt * stride + ot) * kPadTile + tb;
+#pragma unroll
+        for (int st = 0; st < 16; ++st) acc = mfma32(tp[4 * ((st & 3) + 8 * (st >> 2))], bt[kt][st], acc);
+    }
+    return acc;
+}
+template <int NK, int K0 = 0>
+__device__ __forceinline__ f32x16 tchain_from(int k0, const float* wl, int stride, int ot, int tb, const f32x16* bt,
+                                              f32x16 acc) {
+    if constexpr (K0 >= NK) {
+        return acc;
+    } else {
+        if (k0 <= K0) return tchain_k<NK, K0>(wl, stride, ot, tb, bt, acc);
+        return tchain_from<NK, K0 + 1>(k0, wl, stride, ot, tb, bt, acc);
+    }
+}
+
+constexpr int kBwdWaves = 8;  // 2 per SIMD; LDS: the padded forward weight image + one x tile per wave
 
 template <int HT, int VAR>
 __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
@@ -152,16 +249,31 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     constexpr int S = kTileStride;
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
-    // the forward (parallel) weight image is LDS-resident for the recompute (83 KB at d = 63,
-    // H = 64); the transposed tiles of the data-gradient chain stay in L2
+    // the padded forward weight image (both the recompute and the transposed chains read it)
+    const BwdLds BL = bwd_lds(d, HT);
     {
         const f32x4* src = reinterpret_cast<const f32x4*>(packed);
-        for (int i = threadIdx.x; i < L.par_total / 4; i += 64 * kBwdWaves) lds4[i] = src[i];
+        const int nt1 = HT * NKC_(d), nt23 = HT * HT, nt4 = NJ_(d) * 2 * HT;
+        const int ntiles_w = nt1 + 2 * nt23 + nt4;
+        for (int i = threadIdx.x; i < ntiles_w * 256; i += 64 * kBwdWaves) {
+            const int tl = i >> 8, q = i & 255, rq = q >> 6, ln = q & 63;
+            int srco, dsto;
+            if (tl < nt1) { srco = L.w1 + tl * 1024; dsto = BL.w1 + tl * kPadTile; }
+            else if (tl < nt1 + nt23) { srco = L.w2 + (tl - nt1) * 1024; dsto = BL.w2 + (tl - nt1) * kPadTile; }
+            else if (tl < nt1 + 2 * nt23) { srco = L.w3 + (tl - nt1 - nt23) * 1024; dsto = BL.w3 + (tl - nt1 - nt23) * kPadTile; }
+            else { srco = L.w4 + (tl - nt1 - 2 * nt23) * 1024; dsto = BL.w4 + (tl - nt1 - 2 * nt23) * kPadTile; }
+            *reinterpret_cast<f32x4*>(lds + dsto + rq * kPadRQ + ln * 4 + (ln >> 5) * kPadH) = src[(srco >> 2) + q];
+        }
+        for (int i = threadIdx.x; i < HT * 32; i += 64 * kBwdWaves) {
+            lds[BL.b1 + i] = packed[L.b1 + i];
+            lds[BL.b2 + i] = packed[L.b2 + i];
+            lds[BL.b3 + i] = packed[L.b3 + i];
+        }
+        for (int i = threadIdx.x; i < NJ_(d) * 64; i += 64 * kBwdWaves) lds[BL.b4 + i] = packed[L.b4 + i];
     }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* xt = lds + L.par_total + wave * 32 * S;  // x tile; later the direct dL/dx term
-    const float* W = lds;
+    float* xt = lds + BL.x + wave * 32 * S;  // x tile; later the direct dL/dx term
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
     const int voff = lane < d ? lane * 4 : (1 << 30);
     const int rowb = d * 4;
@@ -223,8 +335,10 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         wave_lds_sync();
         // opaque offsets keep the compiler from hoisting every (loop-invariant) weight read out
         // of the tile loop into registers
-        const float* Wf = W + opaque_zero();
-        const float* Pt = packed + opaque_zero();
+        const float* Wl = lds + opaque_zero();
+        const int lo = lane * 4 + h * kPadH;                                              // forward reads
+        const int tbh = ((col >> 3) * kPadRQ + ((col >> 2) & 1) * (128 + kPadH) + (col & 3) + 16 * h);  // W2..W4^T
+        const int tb1 = ((col >> 3) * kPadRQ + (col & 1) * (128 + kPadH) + ((col >> 1) & 3) + 16 * h);  // W1^T
         {
             // x and the ones rows, feature-major: half-wave h writes dim row 2i+h of 32 samples
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(X1 + base, 0, (int)(((int64_t)(d + 1) * P - base) * 4),
@@ -247,12 +361,13 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         f32x16 h1[HT], h2[HT], h3[HT];
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) {
-            f32x16 a = load_bias16(Wf + L.b1 + ht * 32, h);
+            f32x16 a = load_bias16(Wl + BL.b1 + ht * 32, h);
             const int nkc = dense ? NKC : nk1[ht];
             for (int kc = 0; kc < nkc; ++kc) {
+                const float* tp = Wl + BL.w1 + (ht * NKC + kc) * kPadTile + lo;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const f32x4 w = *reinterpret_cast<const f32x4*>(Wf + L.w1 + ((ht * 4 * NKC + kc * 4 + g) * 64 + lane) * 4);
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(tp + g * kPadRQ);
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], xt[col * S + 32 * kc + 8 * g + 2 * rr + h], a);
                 }
@@ -261,11 +376,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
             for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
             h1[ht] = a;
         }
-        made_hidden_nk<HT>(Wf, L.w2, L.b2, h1, h2, nk2, dense || full2);
+        pad_hidden<HT>(Wl + BL.w2, Wl + BL.b2, h1, h2, nk2, dense || full2, lo, h);
         const uint32_t m1 = relu_bits<HT>(h1);
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) store_fm(H1, h1[ht], 32 * ht, H, B, P, base);
-        made_hidden_nk<HT>(Wf, L.w3, L.b3, h2, h3, nk3, dense || full3);
+        pad_hidden<HT>(Wl + BL.w3, Wl + BL.b3, h2, h3, nk3, dense || full3, lo, h);
         const uint32_t m2 = relu_bits<HT>(h2);
 #pragma unroll
         for (int ht = 0; ht < HT; ++ht) store_fm(H2, h2[ht], 32 * ht, H, B, P, base);
@@ -276,10 +391,9 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             if (j < NJ) {
-                f32x16 mu, al;
-                out_pair_n<HT, HT>(dense ? HT : nk4[j], Wf, L, j, h3, mu, al);
-                d4[2 * j] = mu;
-                d4[2 * j + 1] = al;
+                // output tiles (j, mu) = tile index 2j, (j, alpha) = 2j + 1 of the padded w4
+                d4[2 * j] = pad_tile_n<HT, HT>(dense ? HT : nk4[j], Wl + BL.w4, Wl + BL.b4, 2 * j, h3, lo, h);
+                d4[2 * j + 1] = pad_tile_n<HT, HT>(dense ? HT : nk4[j], Wl + BL.w4, Wl + BL.b4, 2 * j + 1, h3, lo, h);
             } else {
                 d4[2 * j] = d4[2 * j + 1] = f32x16{};
             }
@@ -365,8 +479,8 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
             const int k4 = d4ok ? 2 * kstart(nk4, NJ, ot) : 0;
-            f32x16 acc = NJ == 2 ? chain_gmem_from<4>(k4, Pt + L.t4, ot, 4, d4, f32x16{})
-                                 : chain_gmem_from<2>(k4, Pt + L.t4, ot, 2, d4, f32x16{});
+            f32x16 acc = NJ == 2 ? tchain_from<4>(k4, Wl + BL.w4, HT, ot, tbh, d4, f32x16{})
+                                 : tchain_from<2>(k4, Wl + BL.w4, HT, ot, tbh, d4, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = ((m3 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g[ot] = acc;
@@ -386,7 +500,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         f32x16 g2[HT];
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = chain_gmem_from<HT>(g3ok ? kstart(nk3, HT, ot) : 0, Pt + L.t3, ot, HT, g, f32x16{});
+            f32x16 acc = tchain_from<HT>(g3ok ? kstart(nk3, HT, ot) : 0, Wl + BL.w3, HT, ot, tbh, g, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = ((m2 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g2[ot] = acc;
@@ -398,7 +512,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         const bool g2ok = !dense && tiles_finite<HT>(g2);
 #pragma unroll
         for (int ot = 0; ot < HT; ++ot) {
-            f32x16 acc = chain_gmem_from<HT>(g2ok ? kstart(nk2, HT, ot) : 0, Pt + L.t2, ot, HT, g2, f32x16{});
+            f32x16 acc = tchain_from<HT>(g2ok ? kstart(nk2, HT, ot) : 0, Wl + BL.w2, HT, ot, tbh, g2, f32x16{});
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = ((m1 >> (ot * 16 + r)) & 1u) ? acc[r] : 0.f;
             g[ot] = acc;
@@ -413,7 +527,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
             if (ot < NKC) {
-                const f32x16 gx = chain_gmem_from<HT>(g1ok ? kstart(nk1, HT, ot) : 0, Pt + L.t1, ot, HT, g, f32x16{});
+                const f32x16 gx = tchain_from<HT>(g1ok ? kstart(nk1, HT, ot) : 0, Wl + BL.w1, NKC, ot, tb1, g, f32x16{});
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     float* px = xt + col * S + 32 * ot + crow(r, h);
@@ -737,7 +851,8 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
         return check_launch("made_bwdw_kernel");
     }
     const MadeLayout L = made_layout(d, HT);
-    const size_t lds = ((size_t)L.par_total + (size_t)kBwdWaves * 32 * kTileStride) * sizeof(float);
+    const size_t lds = ((size_t)bwd_lds(d, HT).total + (size_t)kBwdWaves * 32 * kTileStride) * sizeof(float);
+    (void)L;
     const bool iaf = variant == NFX_IAF_FORWARD;
     const void* k = HT == 1 ? (iaf ? (const void*)made_bwd_kernel<1, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<1, NFX_MAF_INVERSE>)
                             : (iaf ? (const void*)made_bwd_kernel<2, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<2, NFX_MAF_INVERSE>);
