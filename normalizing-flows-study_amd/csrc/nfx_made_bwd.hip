@@ -222,8 +222,13 @@ __device__ __forceinline__ f32x16 tchain_k(const float* wl, int stride, int ot, 
 #pragma unroll
     for (int kt = K0; kt < NK; ++kt) {
         const float* tp = wl + (kt * stride + ot) * kPadTile + tb;
+        // the tile's 16 dwords in flight together (counted waits), then the 16 MFMAs
+        float a[16];
 #pragma unroll
-        for (int st = 0; st < 16; ++st) acc = mfma32(tp[4 * ((st & 3) + 8 * (st >> 2))], bt[kt][st], acc);
+        for (int st = 0; st < 16; ++st) a[st] = tp[4 * ((st & 3) + 8 * (st >> 2))];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int st = 0; st < 16; ++st) acc = mfma32(a[st], bt[kt][st], acc);
     }
     return acc;
 }
