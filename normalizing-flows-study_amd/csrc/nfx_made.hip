@@ -217,7 +217,13 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     int rc = check_launch("made_pack_kernel");
     if (rc) return rc;
     made_live_kernel<<<1, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
-    return check_launch("made_live_kernel");
+    rc = check_launch("made_live_kernel");
+    if (rc) return rc;
+    const int HT = (H + 31) / 32;
+    if (HT > 2) return NFX_OK;
+    if (HT == 1) made_seqs_image_kernel<1><<<4, 256, 0, (hipStream_t)stream>>>(packed, d, H);
+    else made_seqs_image_kernel<2><<<16, 256, 0, (hipStream_t)stream>>>(packed, d, H);
+    return check_launch("made_seqs_image_kernel");
 }
 
 static int made_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,

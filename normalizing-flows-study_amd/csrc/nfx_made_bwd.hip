@@ -27,7 +27,7 @@ namespace nfx {
 __global__ void made_bwd_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
-    for (int i = L.t4 + blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
+    for (int i = L.t4 + blockIdx.x * blockDim.x + threadIdx.x; i < L.rimg; i += gridDim.x * blockDim.x) {
         float v = 0.f;
         int base, nk;
         if (i < L.t3) { base = L.t4; nk = 2 * L.NJ; }
@@ -813,7 +813,7 @@ extern "C" int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float*
     if (d <= 0 || d > 4096 || H <= 0 || H > 256)
         return set_error(NFX_EUNSUPPORTED, "made_pack_backward: d=%d H=%d outside d<=4096, H<=256", d, H);
     const MadeLayout L = made_layout(d, (H + 31) / 32);
-    int blocks = (L.total - L.t4 + 255) / 256;
+    int blocks = (L.rimg - L.t4 + 255) / 256;
     if (blocks > 1024) blocks = 1024;
     made_bwd_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
     return check_launch("made_bwd_pack_kernel");

@@ -42,13 +42,17 @@ namespace nfx {
 //   t4 [HT][2*NJ][4][64][4]   W4mᵀ: hidden rows x (mu|alpha block) k tiles
 //   t3 [HT][HT]..., t2 [HT][HT]...  W3mᵀ, W2mᵀ
 //   t1 [NKC][HT]...           W1mᵀ: input rows x hidden k tiles
+// then (HT <= 2) the rank-ordered image made_seqs_kernel copies into LDS as its prologue
+// (made_seqs_image_kernel; layout = the first S.blk floats of seqs_lds).
 struct MadeLayout {
     int d, HT, Hp, NKC, NJ;
     int w1, b1, w2, b2, w3, b3, w4, b4;  // parallel image
     int par_total;                       // floats of the parallel image (LDS-resident prefix)
     int s_w1t, s_b1, s_w2, s_b2, s_w3, s_b3, s_w4, s_b4, s_deg;
     int nk1, nk2, nk3, nk4, tsafe;
-    int t4, t3, t2, t1, total;
+    int t4, t3, t2, t1;
+    int rimg;  // made_seqs_kernel's LDS prologue image (HT <= 2): [w2 | w3 by rank][b1 | b2 | b3 | deg | gend]
+    int total;
 };
 
 __host__ __device__ constexpr int made_up4(int v) { return (v + 3) & ~3; }
@@ -89,6 +93,7 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     L.t3 = o; o += HT * HT * 1024;
     L.t2 = o; o += HT * HT * 1024;
     L.t1 = o; o += L.NKC * HT * 1024;
+    L.rimg = o; o += HT <= 2 ? 2 * L.Hp * L.Hp + 5 * L.Hp : 0;
     L.total = o;
     return L;
 }

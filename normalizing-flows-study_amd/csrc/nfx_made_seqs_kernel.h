@@ -232,21 +232,11 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     const int lane = lane_id(), slot = lane >> 4, sub = lane & 15;
     auto rank_at = [](int pos) { return (pos % UPL) * 16 + pos / UPL; };
 
-    // rank-ordered resident image
-    for (int e = threadIdx.x; e < Hp * Hp; e += 512) {
-        const int p = e / Hp, q = rank_at(e % Hp);
-        const int a = (int)ordU[p], b = (int)ordU[q];
-        lds[S.w2 + e] = P[L.s_w2 + a * Hp + b];
-        lds[S.w3 + e] = P[L.s_w3 + a * Hp + b];
-    }
-    for (int p = threadIdx.x; p < Hp; p += 512) {
-        lds[S.b1 + p] = P[L.s_b1 + (int)ordU[rank_at(p)]];
-        lds[S.b2 + p] = P[L.s_b2 + (int)ordU[p]];
-        lds[S.b3 + p] = P[L.s_b3 + (int)ordU[p]];
-        lds[S.deg + p] = ordD[p];
-        int q = p + 1;
-        while (q < H && ordD[q] == ordD[p]) ++q;
-        lds[S.gend + p] = (float)q;
+    // rank-ordered resident image: prepared once at pack time (made_seqs_image_kernel), one
+    // coalesced copy here
+    {
+        const f32x4* src = reinterpret_cast<const f32x4*>(P + L.rimg);
+        for (int i = threadIdx.x; i < S.blk / 4; i += 512) lds4[i] = src[i];
     }
     // The 4 pad floats of every staged w4 row are never written by the staging, but step 3 reads
     // w1t "rows" past the block end (multiplied by exact-zero chunk values) that land in the w4
@@ -512,6 +502,37 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     if constexpr (LOGP) {
         const double t = block_sum_f64<512>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
+    }
+}
+
+// Pack-time: the rank-ordered LDS prologue image of made_seqs_kernel (W2/W3 rows by completion
+// rank, columns by position, biases, degree tables), from the unit-order copies and the degree
+// tables made_live_kernel wrote. One launch per pack.
+template <int HT>
+__global__ __launch_bounds__(256) void made_seqs_image_kernel(float* __restrict__ packed, int d, int H) {
+    constexpr int Hp = 32 * HT;
+    constexpr int UPL = Hp / 16;
+    const MadeLayout L = made_layout(d, HT);
+    const SeqsLds S = seqs_lds(Hp);
+    const float* P = packed;
+    const float* ordD = P + L.s_deg + Hp;
+    const float* ordU = P + L.s_deg + 2 * Hp;
+    float* img = packed + L.rimg;
+    auto rank_at = [](int pos) { return (pos % UPL) * 16 + pos / UPL; };
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < Hp * Hp; e += gridDim.x * 256) {
+        const int p = e / Hp, q = rank_at(e % Hp);
+        const int a = (int)ordU[p], b = (int)ordU[q];
+        img[S.w2 + e] = P[L.s_w2 + a * Hp + b];
+        img[S.w3 + e] = P[L.s_w3 + a * Hp + b];
+    }
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < Hp; p += gridDim.x * 256) {
+        img[S.b1 + p] = P[L.s_b1 + (int)ordU[rank_at(p)]];
+        img[S.b2 + p] = P[L.s_b2 + (int)ordU[p]];
+        img[S.b3 + p] = P[L.s_b3 + (int)ordU[p]];
+        img[S.deg + p] = ordD[p];
+        int q = p + 1;
+        while (q < H && ordD[q] == ordD[p]) ++q;
+        img[S.gend + p] = (float)q;
     }
 }
 
