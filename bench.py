@@ -578,7 +578,14 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         result["roofline"]["note"] = ("dominant kernel = the fused backward (forward recompute + "
                                       "data-gradient chain, 2x the layer's forward flops); the "
                                       "weight gradients run as the MFMA sample-contraction kernel "
-                                      "(made_wgrad_kernel, HBM-bound: reads the factor rows once)")
+                                      "(made_wgrad_kernel, HBM-bound: reads the factor rows once). "
+                                      "frac counts the dense flops; the recompute and the transposed "
+                                      "chains skip the structurally-zero 32x32 blocks (the transposed "
+                                      "staircase has as many blocks as the forward one): frac_executed")
+        fe = 2 * made_executed_flop_per_sample(63, 64)
+        ach_e = fe * B / (mean_ms * 1e-3) / 1e12
+        result["roofline"].update({"flop_per_sample_executed": fe, "achieved_executed": ach_e,
+                                   "frac_executed": ach_e / PEAK_FP32_TFLOPS})
         if aux_events:
             wd = [e0.elapsed_time(e1) for _, e0, e1 in aux_events]
             wms = sum(wd) / len(wd)
