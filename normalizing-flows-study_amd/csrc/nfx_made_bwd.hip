@@ -279,8 +279,6 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* xt = lds + BL.x + wave * 32 * S;  // x tile; later the direct dL/dx term
-    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
-    const int voff = lane < d ? lane * 4 : (1 << 30);
     const int rowb = d * 4;
     const int NJ = L.NJ, NKC = L.NKC;
     // feature-major factors: [d4 (2d) | d3 | d2 | d1 (H each) | h3, 1 | h2, 1 | h1, 1 (H+1 each) |
@@ -321,17 +319,33 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     const float tsafe = packed[L.tsafe];
 
     for (int64_t t = (int64_t)blockIdx.x * kBwdWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kBwdWaves) {
+        // the per-lane constants are recomputed per tile from threadIdx.x (a few VALU ops) rather
+        // than kept live across the loop: at the 256-VGPR budget they would be spilled, and each
+        // reload waits behind the tile's factor stores (one in-order vmcnt for loads and stores)
+        const int lane = (int)(threadIdx.x & 63) + opaque_zero(), h = lane >> 5, col = lane & 31;
+        const int voff = lane < d ? lane * 4 : (1 << 30);
         const int64_t base = t * 32;
         const int rows = (int)(B - base < 32 ? B - base : 32);
         float xmax = 0.f;
         {
+            // the tile's 32 rows go straight into LDS (buffer_load ... lds: all 32 in flight, no
+            // registers held), then the overflow-safe bound check reads them back. Out-of-range
+            // lanes of an LDS-DMA write nothing, so the padding dims >= d are zeroed explicitly
+            // (layer 1 multiplies them by zero weights: stale NaN there would poison the sample);
+            // rows >= B stay stale, which only touches the tile's unused sample columns.
             const auto rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + base * d, 0, rows * rowb, 0x00020000);
+            if (lane >= d) {
 #pragma unroll
-            for (int r = 0; r < 32; ++r) {
-                const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff, r * rowb, 0));
-                xt[r * S + lane] = xv;
-                xmax = tmax(xmax, fabsf(xv));  // NaN-propagating: a NaN fails the test
+                for (int r = 0; r < 32; ++r) xt[r * S + lane] = 0.f;
             }
+#pragma unroll
+            for (int r = 0; r < 32; ++r)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(xt + r * S), 4, voff,
+                                                     r * rowb, 0, 0);
+            // the DMA completes under vmcnt; wait explicitly before any LDS read of the tile
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int r = 0; r < 32; ++r) xmax = tmax(xmax, fabsf(xt[r * S + lane]));  // NaN-propagating
         }
         // Skip structurally-zero blocks only when the tile's inputs are finite and within the
         // overflow-safe bound (every forward activation finite: bit-identical to dense, as in
