@@ -101,7 +101,10 @@ __device__ __forceinline__ void seqs_lds_order() { asm volatile("" ::: "memory")
 
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    // every control used here reads a valid lane for every lane, so no `old` value is needed
+    // (mov_dpp leaves it undefined: no zeroing v_mov before each DPP op, and the DPP combiner can
+    // fold the move into the consuming add)
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 // out[c] = v of lane c of this lane's 16-lane DPP row (row_newbcast:c, GFX90A+ encoding 0x150 + c).
@@ -211,6 +214,20 @@ __device__ __forceinline__ void seqs_rank1(const float (&w)[16][UPL], const floa
     }
 }
 
+// Unit p (rank, uniform) of a hidden layer: relu(row sum of w . hin + bias[p]), stored into the
+// owning lane's slot (every lane of the row gets the value from the all-reduce).
+template <int UPL>
+__device__ __forceinline__ void seqs_unit(int p, int sub, const float (&w)[UPL], const float (&hin)[UPL], int bv,
+                                          float (&hout)[UPL]) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < UPL; ++k) v = fmaf(w[k], hin[k], v);
+    v = trelu(row16_allsum(v) + __int_as_float(__builtin_amdgcn_readlane(bv, p)));
+#pragma unroll
+    for (int k = 0; k < UPL; ++k)
+        if (p == sub + 16 * k) hout[k] = v;
+}
+
 template <int HT, int VAR, bool LOGP>
 __global__ __launch_bounds__(512) void made_seqs_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
@@ -226,7 +243,6 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
     const float* P = packed;
-    const float* ordD = P + L.s_deg + Hp;      // degree of the rank-p unit
     const float* ordU = P + L.s_deg + 2 * Hp;  // its unit index
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id(), slot = lane >> 4, sub = lane & 15;
@@ -248,8 +264,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         }
     }
     __syncthreads();
-    const float* degR = lds + S.deg;
-    const float* gendR = lds + S.gend;
+    // Per-rank tables held one entry per lane (Hp <= 64) and read with v_readlane at a uniform
+    // rank: the completion chain (next degree, group end, layer-2/3 biases) has no LDS round trip.
+    const int tl = lane & (Hp - 1);
+    const int degv = (int)lds[S.deg + tl];
+    const int gendv = (int)lds[S.gend + tl];
+    const int b2v = __float_as_int(lds[S.b2 + tl]);
+    const int b3v = __float_as_int(lds[S.b3 + tl]);
     float* xin_t = lds + S.wv + wave * kSeqsTile;  // [4][64] inputs of the block
     float* zout_t = xin_t + 4 * kSeqsStep;         // [4][64] guarded outputs of the block
     float* at_t = zout_t + 4 * kSeqsStep;          // [4][64] clamped alphas of the block
@@ -322,7 +343,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         float ld = 0.f, zsq = 0.f;
         bool poisoned = false;
         int gi = 0;  // completed units (ranks < gi)
-        int nextdeg = __builtin_amdgcn_readfirstlane(H > 0 ? (int)degR[0] : d);
+        int nextdeg = H > 0 ? __builtin_amdgcn_readlane(degv, 0) : d;
 
         float xr[4];
         x_load(gb, 0, xr);
@@ -369,8 +390,11 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                     case 3: if constexpr (UPL >= 3) seqs_dots<(UPL >= 3 ? 3 : 1), UPL>(w4r, offs, h3v, pm, pa); break;
                     default: seqs_dots<UPL, UPL>(w4r, offs, h3v, pm, pa); break;
                 }
-                // step-3 rows now: their LDS latency overlaps the reductions and step 2
-                float w1v[16][UPL];
+                // step-3 rows now: their LDS latency overlaps the reductions and step 2; likewise
+                // the W2/W3 rows of the next unit to complete (rank gi)
+                float w1v[16][UPL], w2n[UPL], w3n[UPL];
+                seqs_slots<0, UPL, UPL>(lds + S.w2 + gi * Hp + sub * UPL, w2n);
+                seqs_slots<0, UPL, UPL>(lds + S.w3 + gi * Hp + sub * UPL, w3n);
                 {
                     const float* w1r = w1b + ii * Hp + sub * UPL;
 #pragma unroll
@@ -432,36 +456,28 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 seqs_lds_order();  // the chunk tile is rewritten by the next chunk
                 // 4. the units of degree nextdeg (ranks gi .. q-1) complete: layer 1, 2, 3
                 if (i + nc - 1 == nextdeg) {
-                    const int q = __builtin_amdgcn_readfirstlane((int)gendR[gi]);
+                    const int q = __builtin_amdgcn_readlane(gendv, gi);
 #pragma unroll
                     for (int k = 0; k < UPL; ++k) {
                         const int p = sub + 16 * k;
                         if (p >= gi && p < q) h1v[k] = trelu(pre1[k / 2][k % 2]);
                     }
-                    for (int p = gi; p < q; ++p) {
+                    // layer 2 of every unit of the group, then layer 3 (a unit's h3 reads the h2
+                    // of its own group); rank gi with the rows read at the chunk start
+                    seqs_unit<UPL>(gi, sub, w2n, h1v, b2v, h2v);
+                    for (int p = gi + 1; p < q; ++p) {
                         float w[UPL];
                         seqs_slots<0, UPL, UPL>(lds + S.w2 + p * Hp + sub * UPL, w);
-                        float v = 0.f;
-#pragma unroll
-                        for (int k = 0; k < UPL; ++k) v = fmaf(w[k], h1v[k], v);
-                        v = trelu(row16_allsum(v) + lds[S.b2 + p]);
-#pragma unroll
-                        for (int k = 0; k < UPL; ++k)
-                            if (p == sub + 16 * k) h2v[k] = v;
+                        seqs_unit<UPL>(p, sub, w, h1v, b2v, h2v);
                     }
-                    for (int p = gi; p < q; ++p) {
+                    seqs_unit<UPL>(gi, sub, w3n, h2v, b3v, h3v);
+                    for (int p = gi + 1; p < q; ++p) {
                         float w[UPL];
                         seqs_slots<0, UPL, UPL>(lds + S.w3 + p * Hp + sub * UPL, w);
-                        float v = 0.f;
-#pragma unroll
-                        for (int k = 0; k < UPL; ++k) v = fmaf(w[k], h2v[k], v);
-                        v = trelu(row16_allsum(v) + lds[S.b3 + p]);
-#pragma unroll
-                        for (int k = 0; k < UPL; ++k)
-                            if (p == sub + 16 * k) h3v[k] = v;
+                        seqs_unit<UPL>(p, sub, w, h2v, b3v, h3v);
                     }
                     gi = q;
-                    nextdeg = __builtin_amdgcn_readfirstlane(gi < H ? (int)degR[gi] : d);
+                    nextdeg = gi < H ? __builtin_amdgcn_readlane(degv, gi) : d;
                 }
                 ii += nc;
             }
