@@ -69,7 +69,7 @@ __host__ __device__ constexpr SplineGrad spline_grad_layout(int HT, int NTMAX) {
 // gradients go (output) and gl (log-det): out = the spline output (after the spline-level guard),
 // gv = dL/dv, gs[k] = dL/dp[h*K + k] (this half's side), gd[t] = dL/dp[2K + 2t + h].
 template <int K, bool INV>
-__device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32], const SplineConsts& C,
+__device__ __forceinline__ void rq_spline_adjoint(float v, const float (&p)[32], const SplineConsts C,
                                                   float go, float gl, float& out, float (&gs)[K],
                                                   float (&gd)[K / 2], float& gv) {
 #pragma clang fp contract(off)

@@ -134,7 +134,7 @@ __device__ __forceinline__ f32x2 tsoftplus2(f32x2 x) {
 // all K-1), and the knots of the bin (not the width array) are gathered by a select chain on
 // the monotone comparisons `knot_k <= v` (= searchsorted(right=True) - 1, clamped).
 template <int K, bool INV>
-__device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], const SplineConsts& C,
+__device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], const SplineConsts C,
                                                float& out, float& lad) {
 #pragma clang fp contract(off)
     const float eps = 1e-8f;
