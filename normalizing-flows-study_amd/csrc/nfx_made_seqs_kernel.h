@@ -9,29 +9,30 @@
 // does not change: output i reads only units with deg < i (made.py:72-78), so all steps in
 // (D_g, D_{g+1}] -- a "segment", ~d/H steps -- take their mu/alpha from the same h3 and are
 // mutually independent. They are evaluated together, in chunks of up to 16 steps:
-//   1. a 16-lane DPP row owns one sample (4 samples per wave); lane `sub` owns the hidden units
-//      of completion rank sub + 16k (k < Hp/16). For every step of the chunk each lane forms its
-//      partial mu/alpha dot products over its COMPLETED units only, register r holding step
-//      (r XOR sub); a 4-stage butterfly reduce-scatter (partners lane^8, ^7, ^2, ^1: row_ror:8,
-//      row_half_mirror, quad perms) leaves lane j with the full sums of step j -- 15 DPP adds
-//      per 16 steps, no dependency chain through the steps;
+//   1. a 16-lane DPP row owns one sample (4 samples per wave); lane j forms step j's mu/alpha
+//      dot products over the COMPLETED units (ranks < gi) in full: the step's staged W4 row
+//      holds (mu, alpha) weight pairs by completion rank, the sample's h3 row sits in LDS by
+//      rank (0 until the unit completes; one broadcast read serves the 16 lanes), so no
+//      cross-lane reduction is needed and the work grows with the completed units;
 //   2. lane j evaluates step j's affine map;
-//   3. the rank-1 updates of the layer-1 pre-activations with the chunk's new inputs, in step
-//      order, over the lane's INCOMPLETE units only (W1[a][i] is masked to zero for i > deg(a));
-//   4. the units of degree D_{g+1} complete (layer 1, then 2, then 3, row all-reduces).
+//   3. the rank-1 updates of the layer-1 pre-activations with the chunk's new inputs (DPP row
+//      broadcasts), in step order, over the lane's INCOMPLETE units only (W1[a][i] is masked to
+//      zero for i > deg(a)); lane `sub` owns the hidden units of completion rank sub + 16k;
+//   4. the units of degree D_{g+1} complete (layer 1, then 2, then 3, row all-reduces; the
+//      layer-3 value is written to the sample's h3 row).
 // Owning ranks sub + 16k (interleaved) keeps the completed/incomplete split within one unit per
-// lane at every segment, so the skipping in 1 and 3 is lane-uniform: with c completed units a
-// lane has floor(c/16) or ceil(c/16) completed slots, and steps 1/3 run ceil(c/16) resp.
-// Hp/16 - floor(c/16) slots (template-specialised, ~half the FMAs and LDS reads of dense).
+// lane at every segment, so the skipping in 3 is lane-uniform (template-specialised on
+// floor(c/16) completed slots).
 // The log-det and the fused Gaussian term are summed in step order (the reference's sequential
 // fp32 `ld -= alpha_i` and nfx_gauss_logprob's in-order z^2 sum), so results equal the
 // per-step formulation's up to the reduction order inside each mu/alpha dot product.
 // A non-finite step poisons every later step (the reference feeds NaN/Inf through the dense
 // masked matmul: 0*NaN = NaN), found per chunk with a wave ballot.
-// Weights (permuted to rank order on the fly): W2/W3, biases and the degree tables LDS-resident;
-// per-step rows (W1^T column, W4 mu/alpha rows, b4) staged in 64-step blocks into an LDS double
-// buffer by LDS-DMA, the next block in flight while the current one is processed; mu/alpha
-// weights interleaved per slot so the pair of dot products is one packed FMA (v_pk_fma_f32).
+// Weights (permuted to rank order at pack time): biases and the degree tables LDS-resident, W2/W3
+// rows read from the L2-resident image at the chunk start; per-step rows (W1^T column, W4
+// mu/alpha rows, b4) staged in 64-step blocks into an LDS double buffer by LDS-DMA, the next
+// block in flight while the current one is processed; mu/alpha weights interleaved per rank so
+// the pair of dot products is one packed FMA (v_pk_fma_f32).
 #pragma once
 #include "nfx_made_kernel.h"
 
@@ -39,30 +40,32 @@ namespace nfx {
 
 constexpr int kSeqsWaves = 8;  // 512-thread workgroups, 4 samples per wave
 constexpr int kSeqsStep = 64;  // steps per staged block
-constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * 16;  // per wave: x, z, alpha block tiles; chunk v
+constexpr int kSeqsH3 = 68;  // per-sample h3 row (by rank, Hp <= 64) + 4 pad floats
+constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * kSeqsH3;  // per wave: x, z, alpha block tiles; h3 rows
 
-
-
-// Row stride of the interleaved (mu, alpha) W4 block rows: 2 Hp, padded by 4 floats at Hp = 64
-// so that the 16 lanes of a row group, reading slots of 16 different rows, hit 16 different
-// 16-byte bank granules: (33 (r ^ s) + 2 s) mod 16 is a permutation of s for every r. At Hp = 32
-// the unpadded (16 (r ^ s) + s) mod 16 = s already is.
-__host__ __device__ constexpr int seqs_w4_stride(int Hp) { return 2 * Hp + (Hp == 64 ? 4 : 0); }
+// Row stride of the interleaved (mu, alpha) W4 block rows: 2 Hp + 4, so that the 16 lanes of a
+// row group, reading the same 16-byte column of 16 consecutive rows, hit 16 different bank
+// granules ((ii + j) (Hp / 2 + 1) + 2 q = ii + j + 2 q mod 16 at Hp = 32 and 64).
+__host__ __device__ constexpr int seqs_w4_stride(int Hp) { return 2 * Hp + 4; }
 
 struct SeqsLds {
-    int w2, w3, b1, b2, b3, deg, gend, blk, blkf, wv, total;
+    int w2, w3, tab;                                   // rank-ordered image in global memory
+    int b1, b2, b3, deg, gend, blk, blkf, wv, total;  // LDS
 };
 
-// LDS image (floats). Unit of completion rank p sits at position pos(p) = (p % 16) * UPL + p / 16
-// inside a row (lane sub's slots k = 0..UPL-1 are contiguous); W2/W3 rows are indexed by rank.
-// Block image: w1t [64][Hp] | w4 [64][Hp][mu, alpha] (+4 pad floats per row: the phase-1 reads
-// of 16 different rows by the 16 lanes of a row group are then bank-conflict free) | b4 [mu 64 |
-// alpha 64].
+// Rank-ordered image in global memory (P + L.rimg, built at pack time by made_seqs_image_kernel):
+// W2 / W3 rows by completion rank, columns by position (unit of rank p sits at position
+// pos(p) = (p % 16) * UPL + p / 16: lane sub's slots k = 0..UPL-1 are contiguous), then the
+// tables (b1 by position; b2, b3, degree, group end by rank). The completion chain reads its W2 /
+// W3 rows from there (L2-resident, issued at the chunk start).
+// LDS (floats): the tables | two staged blocks: w1t [64][Hp] by position | w4 [64][Hp][mu, alpha]
+// by RANK (+4 pad floats per row) | b4 [mu 64 | alpha 64] | per-wave tiles.
 __host__ __device__ inline SeqsLds seqs_lds(int Hp) {
     SeqsLds S{};
+    S.w2 = 0;
+    S.w3 = Hp * Hp;
+    S.tab = 2 * Hp * Hp;
     int o = 0;
-    S.w2 = o; o += Hp * Hp;
-    S.w3 = o; o += Hp * Hp;
     S.b1 = o; o += Hp;    // by position
     S.b2 = o; o += Hp;    // by rank
     S.b3 = o; o += Hp;    // by rank
@@ -143,59 +146,8 @@ __device__ __forceinline__ void seqs_slots(const float* row, float (&w)[UPL]) {
     }
 }
 
-// Reduce-scatter over a 16-lane row. On entry lane l, register r holds its partial for slot
-// (r ^ l); on exit p[0] of lane l holds the row total of slot l. Stage with partner l ^ m keeps
-// the registers whose index has the stage's bit clear and adds the partner's register r ^ m,
-// which holds the same slot: (r ^ m) ^ (l ^ m) = r ^ l.
-__device__ __forceinline__ void row16_reduce_scatter(float (&p)[16]) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) p[r] = p[r] + dpp<0x128>(p[r + 8]);  // row_ror:8 = lane ^ 8
-#pragma unroll
-    for (int r = 0; r < 4; ++r) p[r] = p[r] + dpp<0x141>(p[7 - r]);  // half mirror = lane ^ 7
-#pragma unroll
-    for (int r = 0; r < 2; ++r) p[r] = p[r] + dpp<0x4E>(p[r + 2]);   // lane ^ 2
-    p[0] = p[0] + dpp<0xB1>(p[1]);                                    // lane ^ 1
-}
-
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, float b, f32x2 c) {
     return __builtin_elementwise_fma(a, f32x2{b, b}, c);
-}
-
-// Step 1 for KC completed slots. p[r] = this lane's (mu, alpha) row pairs of step ii + (r ^ sub):
-// 2*KC floats; the pair products are packed FMAs (v_pk_fma_f32: mu and alpha of one slot).
-// All 16 rows are read before any is used (sched_barrier): at two waves per SIMD the LDS
-// latency is hidden by reads in flight, not by the other wave.
-template <int KC, int UPL>
-__device__ __forceinline__ void seqs_dots(const float* w4r, const int (&offs)[16], const float (&h3v)[UPL],
-                                          float (&pm)[16], float (&pa)[16]) {
-    f32x4 ta[16], tb[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float* p = w4r + offs[r];
-        if constexpr (KC == 1) {
-            const f32x2 t = *reinterpret_cast<const f32x2*>(p);
-            ta[r] = f32x4{t[0], t[1], 0.f, 0.f};
-        } else {
-            ta[r] = *reinterpret_cast<const f32x4*>(p);
-        }
-        if constexpr (KC == 3) {
-            const f32x2 u = *reinterpret_cast<const f32x2*>(p + 4);
-            tb[r] = f32x4{u[0], u[1], 0.f, 0.f};
-        } else if constexpr (KC == 4) {
-            tb[r] = *reinterpret_cast<const f32x4*>(p + 4);
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        f32x2 acc = {0.f, 0.f};
-        acc = pk_fma(f32x2{ta[r][0], ta[r][1]}, h3v[0], acc);
-        if constexpr (KC >= 2) acc = pk_fma(f32x2{ta[r][2], ta[r][3]}, h3v[1], acc);
-        if constexpr (KC >= 3) acc = pk_fma(f32x2{tb[r][0], tb[r][1]}, h3v[2], acc);
-        if constexpr (KC >= 4) acc = pk_fma(f32x2{tb[r][2], tb[r][3]}, h3v[3], acc);
-        pm[r] = acc[0];
-        pa[r] = acc[1];
-    }
 }
 
 // Step 3 for slots k >= K0 (the others are completed in every lane): pre1 += W1t[i] * v_i in
@@ -217,12 +169,16 @@ __device__ __forceinline__ void seqs_rank1(const float (&w)[16][UPL], const floa
 // Unit p (rank, uniform) of a hidden layer: relu(row sum of w . hin + bias[p]), stored into the
 // owning lane's slot (every lane of the row gets the value from the all-reduce).
 template <int UPL>
-__device__ __forceinline__ void seqs_unit(int p, int sub, const float (&w)[UPL], const float (&hin)[UPL], int bv,
-                                          float (&hout)[UPL]) {
+__device__ __forceinline__ float seqs_unit_value(int p, const float (&w)[UPL], const float (&hin)[UPL], int bv) {
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < UPL; ++k) v = fmaf(w[k], hin[k], v);
-    v = trelu(row16_allsum(v) + __int_as_float(__builtin_amdgcn_readlane(bv, p)));
+    return trelu(row16_allsum(v) + __int_as_float(__builtin_amdgcn_readlane(bv, p)));
+}
+template <int UPL>
+__device__ __forceinline__ void seqs_unit(int p, int sub, const float (&w)[UPL], const float (&hin)[UPL], int bv,
+                                          float (&hout)[UPL]) {
+    const float v = seqs_unit_value<UPL>(p, w, hin, bv);
 #pragma unroll
     for (int k = 0; k < UPL; ++k)
         if (p == sub + 16 * k) hout[k] = v;
@@ -248,10 +204,11 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     const int lane = lane_id(), slot = lane >> 4, sub = lane & 15;
     auto rank_at = [](int pos) { return (pos % UPL) * 16 + pos / UPL; };
 
-    // rank-ordered resident image: prepared once at pack time (made_seqs_image_kernel), one
-    // coalesced copy here
+    // the tables of the rank-ordered image (prepared once at pack time, made_seqs_image_kernel):
+    // one coalesced copy
+    const float* img = P + L.rimg;
     {
-        const f32x4* src = reinterpret_cast<const f32x4*>(P + L.rimg);
+        const f32x4* src = reinterpret_cast<const f32x4*>(img + S.tab);
         for (int i = threadIdx.x; i < S.blk / 4; i += 512) lds4[i] = src[i];
     }
     // The 4 pad floats of every staged w4 row are never written by the staging, but step 3 reads
@@ -274,16 +231,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     float* xin_t = lds + S.wv + wave * kSeqsTile;  // [4][64] inputs of the block
     float* zout_t = xin_t + 4 * kSeqsStep;         // [4][64] guarded outputs of the block
     float* at_t = zout_t + 4 * kSeqsStep;          // [4][64] clamped alphas of the block
+    float* h3_t = at_t + 4 * kSeqsStep;            // [4][kSeqsH3] h3 by rank (0 until complete)
     const int nblk = (d + kSeqsStep - 1) / kSeqsStep;
     // staged-row columns of this lane: w1t rows by position l % Hp; w4 rows interleave
-    // (mu, alpha) per position, instruction `half` of a row covers positions 32 half + l / 2
+    // (mu, alpha) per rank, instruction `half` of a row covers ranks 32 half + l / 2
     const int colW1 = (int)ordU[rank_at(lane % Hp)];
-    const int colW4a = (int)ordU[rank_at((lane / 2) % Hp)];
-    const int colW4b = (int)ordU[rank_at((32 + lane / 2) % Hp)];
-    // phase-1 row offsets: register r <-> step (r ^ sub), this lane's slot pairs
-    int offs[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) offs[r] = (r ^ sub) * RS4 + sub * 2 * UPL;
+    const int colW4a = (int)ordU[(lane / 2) % Hp];
+    const int colW4b = (int)ordU[(32 + lane / 2) % Hp];
 
     // Block staging by LDS-DMA (global_load_lds_dword: lane-linear LDS destination, per-lane
     // source): each wave-instruction fills 64 consecutive floats of the block image (a w1t row
@@ -334,12 +288,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         const int64_t s = gb + wave * 4 + slot;  // this row's sample
         const bool valid = s < B;
         f32x2 pre1[UPL / 2];
-        float h1v[UPL], h2v[UPL], h3v[UPL];
+        float h1v[UPL], h2v[UPL];
 #pragma unroll
         for (int k = 0; k < UPL; ++k) {
             pre1[k / 2][k % 2] = lds[S.b1 + sub * UPL + k];
-            h1v[k] = h2v[k] = h3v[k] = 0.f;
+            h1v[k] = h2v[k] = 0.f;
         }
+        for (int e = lane; e < 4 * kSeqsH3; e += 64) h3_t[e] = 0.f;
         float ld = 0.f, zsq = 0.f;
         bool poisoned = false;
         int gi = 0;  // completed units (ranks < gi)
@@ -376,37 +331,40 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 const int i = i0 + ii;
                 int nc = n - ii < 16 ? n - ii : 16;
                 if (nextdeg - i + 1 < nc) nc = nextdeg - i + 1;
-                // 1. partial mu/alpha dot products over the completed slots
-                float pm[16], pa[16];
-                const float* w4r = w4b + ii * RS4;
-                const int kc1 = (gi + 15) >> 4;
-                switch (kc1 < UPL ? kc1 : UPL) {
-                    case 0:
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) pm[r] = pa[r] = 0.f;
-                        break;
-                    case 1: seqs_dots<1, UPL>(w4r, offs, h3v, pm, pa); break;
-                    case 2: seqs_dots<2, UPL>(w4r, offs, h3v, pm, pa); break;
-                    case 3: if constexpr (UPL >= 3) seqs_dots<(UPL >= 3 ? 3 : 1), UPL>(w4r, offs, h3v, pm, pa); break;
-                    default: seqs_dots<UPL, UPL>(w4r, offs, h3v, pm, pa); break;
+                // 1. lane sub forms step ii + sub's mu/alpha dot products over the completed ranks
+                // (< gi; ranks past it hold h3 = 0): the step's W4 row pair (mu, alpha) by rank
+                // against the sample's h3 row (one broadcast read per 4 ranks), two chains
+                f32x2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+                {
+                    const float* wr = w4b + (ii + sub) * RS4;
+                    const float* hr = h3_t + slot * kSeqsH3;
+                    const int nq = (gi + 3) >> 2;
+#pragma unroll 4
+                    for (int qd = 0; qd < nq; ++qd) {
+                        const f32x4 hv = *reinterpret_cast<const f32x4*>(hr + 4 * qd);
+                        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wr + 8 * qd);
+                        const f32x4 w1 = *reinterpret_cast<const f32x4*>(wr + 8 * qd + 4);
+                        acc0 = pk_fma(f32x2{w0[0], w0[1]}, hv[0], acc0);
+                        acc1 = pk_fma(f32x2{w0[2], w0[3]}, hv[1], acc1);
+                        acc0 = pk_fma(f32x2{w1[0], w1[1]}, hv[2], acc0);
+                        acc1 = pk_fma(f32x2{w1[2], w1[3]}, hv[3], acc1);
+                    }
                 }
                 // step-3 rows now: their LDS latency overlaps the reductions and step 2; likewise
                 // the W2/W3 rows of the next unit to complete (rank gi)
                 float w1v[16][UPL], w2n[UPL], w3n[UPL];
-                seqs_slots<0, UPL, UPL>(lds + S.w2 + gi * Hp + sub * UPL, w2n);
-                seqs_slots<0, UPL, UPL>(lds + S.w3 + gi * Hp + sub * UPL, w3n);
+                seqs_slots<0, UPL, UPL>(img + S.w2 + gi * Hp + sub * UPL, w2n);
+                seqs_slots<0, UPL, UPL>(img + S.w3 + gi * Hp + sub * UPL, w3n);
                 {
                     const float* w1r = w1b + ii * Hp + sub * UPL;
 #pragma unroll
                     for (int j = 0; j < 16; ++j) seqs_slots<0, UPL, UPL>(w1r + j * Hp, w1v[j]);
                 }
-                row16_reduce_scatter(pm);
-                row16_reduce_scatter(pa);
                 // 2. lane sub evaluates step ii + sub (lanes past the chunk compute garbage, unused)
                 const bool vj = sub < nc;
                 const int rj = ii + sub;
-                float mu = pm[0] + bmb[rj];
-                float al = pa[0] + bab[rj];
+                float mu = (acc0[0] + acc1[0]) + bmb[rj];
+                float al = (acc0[1] + acc1[1]) + bab[rj];
                 if (poisoned) {
                     mu = __builtin_nanf("");
                     al = mu;
@@ -467,14 +425,20 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                     seqs_unit<UPL>(gi, sub, w2n, h1v, b2v, h2v);
                     for (int p = gi + 1; p < q; ++p) {
                         float w[UPL];
-                        seqs_slots<0, UPL, UPL>(lds + S.w2 + p * Hp + sub * UPL, w);
+                        seqs_slots<0, UPL, UPL>(img + S.w2 + p * Hp + sub * UPL, w);
                         seqs_unit<UPL>(p, sub, w, h1v, b2v, h2v);
                     }
-                    seqs_unit<UPL>(gi, sub, w3n, h2v, b3v, h3v);
+                    // layer 3 into the sample's LDS h3 row (step 1 reads it by rank)
+                    float* h3r = h3_t + slot * kSeqsH3;
+                    {
+                        const float v = seqs_unit_value<UPL>(gi, w3n, h2v, b3v);
+                        if (sub == 0) h3r[gi] = v;
+                    }
                     for (int p = gi + 1; p < q; ++p) {
                         float w[UPL];
-                        seqs_slots<0, UPL, UPL>(lds + S.w3 + p * Hp + sub * UPL, w);
-                        seqs_unit<UPL>(p, sub, w, h2v, b3v, h3v);
+                        seqs_slots<0, UPL, UPL>(img + S.w3 + p * Hp + sub * UPL, w);
+                        const float v = seqs_unit_value<UPL>(p, w, h2v, b3v);
+                        if (sub == 0) h3r[p] = v;
                     }
                     gi = q;
                     nextdeg = gi < H ? __builtin_amdgcn_readlane(degv, gi) : d;
@@ -541,14 +505,15 @@ __global__ __launch_bounds__(256) void made_seqs_image_kernel(float* __restrict_
         img[S.w2 + e] = P[L.s_w2 + a * Hp + b];
         img[S.w3 + e] = P[L.s_w3 + a * Hp + b];
     }
+    float* tab = img + S.tab;
     for (int p = blockIdx.x * 256 + threadIdx.x; p < Hp; p += gridDim.x * 256) {
-        img[S.b1 + p] = P[L.s_b1 + (int)ordU[rank_at(p)]];
-        img[S.b2 + p] = P[L.s_b2 + (int)ordU[p]];
-        img[S.b3 + p] = P[L.s_b3 + (int)ordU[p]];
-        img[S.deg + p] = ordD[p];
+        tab[S.b1 + p] = P[L.s_b1 + (int)ordU[rank_at(p)]];
+        tab[S.b2 + p] = P[L.s_b2 + (int)ordU[p]];
+        tab[S.b3 + p] = P[L.s_b3 + (int)ordU[p]];
+        tab[S.deg + p] = ordD[p];
         int q = p + 1;
         while (q < H && ordD[q] == ordD[p]) ++q;
-        img[S.gend + p] = (float)q;
+        tab[S.gend + p] = (float)q;
     }
 }
 
