@@ -232,7 +232,19 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     float* zout_t = xin_t + 4 * kSeqsStep;         // [4][64] guarded outputs of the block
     float* at_t = zout_t + 4 * kSeqsStep;          // [4][64] clamped alphas of the block
     float* h3_t = at_t + 4 * kSeqsStep;            // [4][kSeqsH3] h3 by rank (0 until complete)
-    const int nblk = (d + kSeqsStep - 1) / kSeqsStep;
+    // Staged blocks end where a segment ends (after the step of a completion degree) whenever a
+    // segment boundary falls within kSeqsStep steps, so that no chunk is cut by a block boundary
+    // (at cfg5i: 65 chunks per sample instead of 77). Block [i0, blk_end(i0)), uniform.
+    auto blk_end = [&](int i0) -> int {
+        const int lim = i0 + kSeqsStep;
+        if (lim >= d) return d;
+        // lane g < H holds rank g's degree; degrees ascend with the rank, so the highest lane
+        // whose segment end falls in (i0, lim] has the largest one
+        const int e = degv + 1;
+        const uint64_t m = __ballot(lane < H && e > i0 && e <= lim);
+        if (m == 0) return lim;  // no segment ends inside: a full block
+        return __builtin_amdgcn_readlane(e, 63 - __builtin_clzll(m));
+    };
     // staged-row columns of this lane: w1t rows by position l % Hp; w4 rows interleave
     // (mu, alpha) per rank, instruction `half` of a row covers ranks 32 half + l / 2
     const int colW1 = (int)ordU[rank_at(lane % Hp)];
@@ -246,9 +258,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     // discarded). Issued a block ahead into the other buffer.
     constexpr int IPR = 2 * Hp / 64;  // instructions per w4 row
     constexpr int NI = Hp + kSeqsStep * IPR + 2;
-    auto blk_stage = [&](int kb, int buf) {
-        const int i0 = kb * kSeqsStep;
-        const int n = d - i0 < kSeqsStep ? d - i0 : kSeqsStep;
+    auto blk_stage = [&](int i0, int n, int buf) {
         float* dst = lds + S.blk + buf * S.blkf;
         for (int j = wave; j < NI; j += kSeqsWaves) {
             size_t src;
@@ -273,9 +283,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             seqs_dma_dword(P + src, dst + off);
         }
     };
-    auto x_load = [&](int64_t gb, int kb, float (&xr)[4]) {
-        const int i0 = kb * kSeqsStep;
-        const int n = d - i0 < kSeqsStep ? d - i0 : kSeqsStep;
+    auto x_load = [&](int64_t gb, int i0, int n, float (&xr)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t sr = gb + wave * 4 + q;
@@ -301,16 +309,15 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         int nextdeg = H > 0 ? __builtin_amdgcn_readlane(degv, 0) : d;
 
         float xr[4];
-        x_load(gb, 0, xr);
+        int i0 = 0, n = blk_end(0), buf = 0;
+        x_load(gb, i0, n, xr);
         __syncthreads();  // previous group's readers of the staging buffers are done
-        blk_stage(0, 0);
+        blk_stage(i0, n, 0);
         seqs_dma_wait();
         __syncthreads();
 
-        for (int kb = 0; kb < nblk; ++kb) {
-            const int i0 = kb * kSeqsStep;
-            const int n = d - i0 < kSeqsStep ? d - i0 : kSeqsStep;
-            const float* blk = lds + S.blk + (kb & 1) * S.blkf;
+        while (i0 < d) {
+            const float* blk = lds + S.blk + buf * S.blkf;
             const float* w1b = blk;
             const float* w4b = blk + W4F;
             const float* bmb = blk + B4F;
@@ -320,10 +327,11 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 xin_t[q * kSeqsStep + lane] = xr[q];
                 if (lane >= n) zout_t[q * kSeqsStep + lane] = at_t[q * kSeqsStep + lane] = 0.f;
             }
-            const bool more = kb + 1 < nblk;
-            if (more) {
-                blk_stage(kb + 1, (kb + 1) & 1);  // its readers finished the previous block
-                x_load(gb, kb + 1, xr);
+            const int i0n = i0 + n;
+            const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
+            if (nn > 0) {
+                blk_stage(i0n, nn, buf ^ 1);  // its readers finished the previous block
+                x_load(gb, i0n, nn, xr);
             }
             seqs_lds_order();
 
@@ -466,6 +474,9 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             }
             seqs_dma_wait();  // the next block's LDS-DMA has landed
             __syncthreads();  // ... for every wave; and every wave is done with this block
+            i0 = i0n;
+            n = nn;
+            buf ^= 1;
         }
         if (valid && sub == 0) {
             if (nonfinite(ld)) ld = 0.f;
