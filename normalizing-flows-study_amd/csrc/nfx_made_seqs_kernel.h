@@ -41,7 +41,8 @@ namespace nfx {
 constexpr int kSeqsWaves = 8;  // 512-thread workgroups, 4 samples per wave
 constexpr int kSeqsStep = 64;  // steps per staged block
 constexpr int kSeqsH3 = 68;  // per-sample h3 row (by rank, Hp <= 64) + 4 pad floats
-constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * kSeqsH3;  // per wave: x, z, alpha block tiles; h3 rows
+// per wave: x, z, alpha block tiles; h3 rows; 64 floats where the lanes past a chunk store
+constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * kSeqsH3 + 64;
 
 // Row stride of the interleaved (mu, alpha) W4 block rows: 2 Hp + 4, so that the 16 lanes of a
 // row group, reading the same 16-byte column of 16 consecutive rows, hit 16 different bank
@@ -373,10 +374,8 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 const int rj = ii + sub;
                 float mu = (acc0[0] + acc1[0]) + bmb[rj];
                 float al = (acc0[1] + acc1[1]) + bab[rj];
-                if (poisoned) {
-                    mu = __builtin_nanf("");
-                    al = mu;
-                }
+                mu = poisoned ? __builtin_nanf("") : mu;
+                al = poisoned ? __builtin_nanf("") : al;
                 const float xin = xin_t[slot * kSeqsStep + rj];
                 float vi, vo, a;
                 if constexpr (VAR == NFX_MAF_FORWARD) {
@@ -392,18 +391,17 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 // the first non-finite step of the chunk poisons the later ones (and the rest)
                 const uint64_t bad = __ballot(vj && nonfinite(vi));
                 const unsigned rowbad = (unsigned)(bad >> (slot * 16)) & 0xFFFFu;
-                if (rowbad) {
-                    if (sub > __builtin_ctz(rowbad)) {
-                        vi = __builtin_nanf("");
-                        a = vi;
-                    }
-                    poisoned = true;
-                }
+                const bool kill = rowbad != 0u && sub > __builtin_ctz(rowbad | 0x10000u);
+                vi = kill ? __builtin_nanf("") : vi;
+                a = kill ? __builtin_nanf("") : a;
+                poisoned = poisoned || rowbad != 0u;
                 if constexpr (VAR == NFX_MAF_FORWARD) vo = nonfinite(vi) ? 0.f : vi;
                 else vo = nonfinite(vi) ? xin : vi;
-                if (vj) {
-                    zout_t[slot * kSeqsStep + rj] = vo;
-                    at_t[slot * kSeqsStep + rj] = a;
+                {
+                    // branch-free: lanes past the chunk store into the tile's spare 64 floats
+                    float* dump = h3_t + 4 * kSeqsH3 + lane;
+                    *(vj ? zout_t + slot * kSeqsStep + rj : dump) = vo;
+                    *(vj ? at_t + slot * kSeqsStep + rj : dump) = a;
                 }
                 // every lane of the row needs the chunk's 16 values: DPP row broadcasts
                 // (row_newbcast:c), no LDS round trip on the chunk's critical path
