@@ -93,6 +93,8 @@ def test_small_made_flows(cuda_device, name, kind):
 @pytest.mark.parametrize("d,H,B", [(5, 16, 1), (33, 32, 65), (63, 96, 130), (100, 128, 257), (7, 64, 1000),
                                    (65, 64, 129), (100, 32, 700), (200, 64, 1500), (784, 64, 77),
                                    (300, 16, 33), (130, 48, 70), (129, 64, 35),
+                                   # segments longer than a 64-step staged block (sequential kernel)
+                                   (400, 4, 50), (1000, 8, 20), (777, 64, 9),
                                    # 128 < H <= 256: nfx_made_big.hip
                                    (5, 256, 70), (63, 160, 100), (100, 256, 65), (300, 256, 33), (2, 200, 40),
                                    (64, 129, 97)])
