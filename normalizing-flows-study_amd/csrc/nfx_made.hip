@@ -221,8 +221,8 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     if (rc) return rc;
     const int HT = (H + 31) / 32;
     if (HT > 2) return NFX_OK;
-    if (HT == 1) made_seqs_image_kernel<1><<<4, 256, 0, (hipStream_t)stream>>>(packed, d, H);
-    else made_seqs_image_kernel<2><<<16, 256, 0, (hipStream_t)stream>>>(packed, d, H);
+    if (HT == 1) made_seqs_image_kernel<1><<<64, 256, 0, (hipStream_t)stream>>>(packed, d, H);
+    else made_seqs_image_kernel<2><<<64, 256, 0, (hipStream_t)stream>>>(packed, d, H);
     return check_launch("made_seqs_image_kernel");
 }
 

@@ -52,10 +52,17 @@ struct MadeLayout {
     int nk1, nk2, nk3, nk4, tsafe;
     int t4, t3, t2, t1;
     int rimg;  // made_seqs_kernel's LDS prologue image (HT <= 2): [w2 | w3 by rank][b1 | b2 | b3 | deg | gend]
+    int sw1, sw4, sb4;  // made_seqs_kernel's block-ready step rows (HT <= 2), d + kSeqsPadRows rows each
     int total;
 };
 
 __host__ __device__ constexpr int made_up4(int v) { return (v + 3) & ~3; }
+
+// made_seqs_kernel's staged step rows: W4 (mu, alpha) pairs by completion rank + 4 pad floats
+// (bank-conflict-free column reads of 16 consecutive rows), and the zero rows past d that let a
+// 64-step block always be copied whole.
+__host__ __device__ constexpr int seqs_w4_stride(int Hp) { return 2 * Hp + 4; }
+constexpr int kSeqsPadRows = 64;
 
 __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     MadeLayout L{};
@@ -94,6 +101,11 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     L.t2 = o; o += HT * HT * 1024;
     L.t1 = o; o += L.NKC * HT * 1024;
     L.rimg = o; o += HT <= 2 ? 2 * L.Hp * L.Hp + 5 * L.Hp : 0;
+    o = made_up4(o);
+    const int rows = HT <= 2 ? d + kSeqsPadRows : 0;
+    L.sw1 = o; o += made_up4(rows * L.Hp);
+    L.sw4 = o; o += made_up4(rows * seqs_w4_stride(L.Hp));
+    L.sb4 = o; o += made_up4(2 * rows);
     L.total = o;
     return L;
 }

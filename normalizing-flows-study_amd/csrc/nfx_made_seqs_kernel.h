@@ -44,10 +44,10 @@ constexpr int kSeqsH3 = 68;  // per-sample h3 row (by rank, Hp <= 64) + 4 pad fl
 // per wave: x, z, alpha block tiles; h3 rows; 64 floats where the lanes past a chunk store
 constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * kSeqsH3 + 64;
 
-// Row stride of the interleaved (mu, alpha) W4 block rows: 2 Hp + 4, so that the 16 lanes of a
-// row group, reading the same 16-byte column of 16 consecutive rows, hit 16 different bank
-// granules ((ii + j) (Hp / 2 + 1) + 2 q = ii + j + 2 q mod 16 at Hp = 32 and 64).
-__host__ __device__ constexpr int seqs_w4_stride(int Hp) { return 2 * Hp + 4; }
+// seqs_w4_stride (nfx_made_kernel.h): row stride of the interleaved (mu, alpha) W4 block rows,
+// 2 Hp + 4, so that the 16 lanes of a row group, reading the same 16-byte column of 16
+// consecutive rows, hit 16 different bank granules ((ii + j)(Hp / 2 + 1) + 2 q = ii + j + 2 q mod 16).
+static_assert(kSeqsPadRows == kSeqsStep, "a staged block is copied whole from the padded rows");
 
 struct SeqsLds {
     int w2, w3, tab;                                   // rank-ordered image in global memory
@@ -97,6 +97,20 @@ __device__ __forceinline__ void seqs_dma_dword(const float* src, float* lds_dst)
         : "memory");
 }
 __device__ __forceinline__ void seqs_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// One global_load_lds_dwordx4: lane l's 16 bytes from `src` (per lane) to LDS lds_dst + 16 l.
+__device__ __forceinline__ void seqs_dma_x4(const float* src, float* lds_dst) {
+    const uint32_t m = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) float*)lds_dst);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(m))
+        : "memory");
+}
 
 // Keeps the compiler from moving LDS accesses across this point. A wave's DS operations execute
 // in order, so wave-private tiles need nothing more -- and, unlike a fence, this emits no
@@ -200,10 +214,8 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
     const float* P = packed;
-    const float* ordU = P + L.s_deg + 2 * Hp;  // its unit index
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id(), slot = lane >> 4, sub = lane & 15;
-    auto rank_at = [](int pos) { return (pos % UPL) * 16 + pos / UPL; };
 
     // the tables of the rank-ordered image (prepared once at pack time, made_seqs_image_kernel):
     // one coalesced copy
@@ -211,15 +223,6 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     {
         const f32x4* src = reinterpret_cast<const f32x4*>(img + S.tab);
         for (int i = threadIdx.x; i < S.blk / 4; i += 512) lds4[i] = src[i];
-    }
-    // The 4 pad floats of every staged w4 row are never written by the staging, but step 3 reads
-    // w1t "rows" past the block end (multiplied by exact-zero chunk values) that land in the w4
-    // rows: zero the pads once so those products are exact zeros, not 0 * (stale LDS) = NaN.
-    if constexpr (RS4 > 2 * Hp) {
-        for (int e = threadIdx.x; e < 2 * kSeqsStep * (RS4 - 2 * Hp); e += 512) {
-            const int buf = e / (kSeqsStep * (RS4 - 2 * Hp)), t = e % (kSeqsStep * (RS4 - 2 * Hp));
-            lds[S.blk + buf * S.blkf + W4F + (t / (RS4 - 2 * Hp)) * RS4 + 2 * Hp + t % (RS4 - 2 * Hp)] = 0.f;
-        }
     }
     __syncthreads();
     // Per-rank tables held one entry per lane (Hp <= 64) and read with v_readlane at a uniform
@@ -246,42 +249,26 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         if (m == 0) return lim;  // no segment ends inside: a full block
         return __builtin_amdgcn_readlane(e, 63 - __builtin_clzll(m));
     };
-    // staged-row columns of this lane: w1t rows by position l % Hp; w4 rows interleave
-    // (mu, alpha) per rank, instruction `half` of a row covers ranks 32 half + l / 2
-    const int colW1 = (int)ordU[rank_at(lane % Hp)];
-    const int colW4a = (int)ordU[(lane / 2) % Hp];
-    const int colW4b = (int)ordU[(32 + lane / 2) % Hp];
-
-    // Block staging by LDS-DMA (global_load_lds_dword: lane-linear LDS destination, per-lane
-    // source): each wave-instruction fills 64 consecutive floats of the block image (a w1t row
-    // piece, half or all of a padded w4 row, a b4 half), columns gathered into rank positions.
-    // Rows past the end of d re-read the last valid row (finite; multiplied by exact zeros or
-    // discarded). Issued a block ahead into the other buffer.
-    constexpr int IPR = 2 * Hp / 64;  // instructions per w4 row
-    constexpr int NI = Hp + kSeqsStep * IPR + 2;
-    auto blk_stage = [&](int i0, int n, int buf) {
+    // Block staging by LDS-DMA: a block is kSeqsStep consecutive rows of the block-ready image
+    // (made_seqs_image_kernel: w1t rows by position, W4 pair rows by rank + pads, b4), copied
+    // whole with 16-byte LDS-DMA pieces (1 KiB per wave instruction) — rows past the block (the
+    // next block's, or zero rows past d) are finite, which the lanes past a chunk rely on.
+    // Issued a block ahead into the other buffer.
+    constexpr int N1 = kSeqsStep * Hp / 256, N4 = kSeqsStep * RS4 / 256;
+    static_assert(N1 * 256 == kSeqsStep * Hp && N4 * 256 == kSeqsStep * RS4, "whole 1 KiB pieces");
+    auto blk_stage = [&](int i0, int buf) {
         float* dst = lds + S.blk + buf * S.blkf;
-        for (int j = wave; j < NI; j += kSeqsWaves) {
-            size_t src;
-            int off;
-            if (j < Hp) {
-                int row = (j * 64 + lane) / Hp;
-                row = row < n ? row : n - 1;
-                src = (size_t)L.s_w1t + (size_t)(i0 + row) * Hp + colW1;
-                off = 64 * j;
-            } else if (j < Hp + kSeqsStep * IPR) {
-                const int jj = j - Hp, half = jj % IPR;
-                int row = jj / IPR;
-                off = W4F + row * RS4 + 64 * half;
-                row = row < n ? row : n - 1;
-                const int h = lane & 1;
-                src = (size_t)L.s_w4 + (size_t)(h * d + i0 + row) * Hp + (half ? colW4b : colW4a);
+        const float* sw1 = P + L.sw1 + (size_t)i0 * Hp;
+        const float* sw4 = P + L.sw4 + (size_t)i0 * RS4;
+        for (int j = wave; j < N1 + N4 + 2; j += kSeqsWaves) {
+            if (j < N1) {
+                seqs_dma_x4(sw1 + 256 * j + 4 * lane, dst + 256 * j);
+            } else if (j < N1 + N4) {
+                seqs_dma_x4(sw4 + 256 * (j - N1) + 4 * lane, dst + W4F + 256 * (j - N1));
             } else {
-                const int c = lane < n ? lane : n - 1, jb = j - (Hp + kSeqsStep * IPR);
-                src = (size_t)L.s_b4 + (size_t)jb * d + i0 + c;
-                off = B4F + 64 * jb;
+                const int jb = j - N1 - N4;
+                seqs_dma_dword(P + L.sb4 + (size_t)jb * (d + kSeqsPadRows) + i0 + lane, dst + B4F + 64 * jb);
             }
-            seqs_dma_dword(P + src, dst + off);
         }
     };
     auto x_load = [&](int64_t gb, int i0, int n, float (&xr)[4]) {
@@ -292,6 +279,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         }
     };
 
+#ifdef NFX_SEQS_TIMING
+    long long tacc[7] = {0, 0, 0, 0, 0, 0, 0};
+    long long tmark = clock64();
+#define NFX_TMARK(k) do { const long long t_ = clock64(); tacc[k] += t_ - tmark; tmark = t_; } while (0)
+#else
+#define NFX_TMARK(k) do { } while (0)
+#endif
     double lpacc = 0.0;
     for (int64_t gb = (int64_t)blockIdx.x * kSeqsWaves * 4; gb < B; gb += (int64_t)gridDim.x * kSeqsWaves * 4) {
         const int64_t s = gb + wave * 4 + slot;  // this row's sample
@@ -313,7 +307,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         int i0 = 0, n = blk_end(0), buf = 0;
         x_load(gb, i0, n, xr);
         __syncthreads();  // previous group's readers of the staging buffers are done
-        blk_stage(i0, n, 0);
+        blk_stage(i0, 0);
         seqs_dma_wait();
         __syncthreads();
 
@@ -331,11 +325,12 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             const int i0n = i0 + n;
             const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
             if (nn > 0) {
-                blk_stage(i0n, nn, buf ^ 1);  // its readers finished the previous block
+                blk_stage(i0n, buf ^ 1);  // its readers finished the previous block
                 x_load(gb, i0n, nn, xr);
             }
             seqs_lds_order();
 
+            NFX_TMARK(6);  // block start: input tile, block end, LDS-DMA and x issue
             for (int ii = 0; ii < n;) {
                 const int i = i0 + ii;
                 int nc = n - ii < 16 ? n - ii : 16;
@@ -369,6 +364,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
 #pragma unroll
                     for (int j = 0; j < 16; ++j) seqs_slots<0, UPL, UPL>(w1r + j * Hp, w1v[j]);
                 }
+                NFX_TMARK(0);  // chunk start + dot products
                 // 2. lane sub evaluates step ii + sub (lanes past the chunk compute garbage, unused)
                 const bool vj = sub < nc;
                 const int rj = ii + sub;
@@ -403,6 +399,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                     *(vj ? zout_t + slot * kSeqsStep + rj : dump) = vo;
                     *(vj ? at_t + slot * kSeqsStep + rj : dump) = a;
                 }
+                NFX_TMARK(1);  // rank-1 / W2 / W3 row reads, affine map, poison ballot, step stores
                 // every lane of the row needs the chunk's 16 values: DPP row broadcasts
                 // (row_newbcast:c), no LDS round trip on the chunk's critical path
                 const float cvl = vj ? vi : 0.f;
@@ -418,6 +415,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                     default: break;
                 }
                 seqs_lds_order();  // the chunk tile is rewritten by the next chunk
+                NFX_TMARK(2);  // broadcasts + rank-1 updates
                 // 4. the units of degree nextdeg (ranks gi .. q-1) complete: layer 1, 2, 3
                 if (i + nc - 1 == nextdeg) {
                     const int q = __builtin_amdgcn_readlane(gendv, gi);
@@ -449,6 +447,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                     gi = q;
                     nextdeg = gi < H ? __builtin_amdgcn_readlane(degv, gi) : d;
                 }
+                NFX_TMARK(3);  // completion
                 ii += nc;
             }
             seqs_lds_order();
@@ -470,8 +469,10 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 const int64_t so = gb + wave * 4 + q;
                 if (so < B && lane < n) out[so * d + i0 + lane] = zout_t[q * kSeqsStep + lane];
             }
+            NFX_TMARK(4);  // log-det / z^2 sums of the block, output rows
             seqs_dma_wait();  // the next block's LDS-DMA has landed
             __syncthreads();  // ... for every wave; and every wave is done with this block
+            NFX_TMARK(5);  // vmcnt(0) + barrier
             i0 = i0n;
             n = nn;
             buf ^= 1;
@@ -488,6 +489,11 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             }
         }
     }
+#ifdef NFX_SEQS_TIMING
+    // timing build only: workgroup 0's first lane overwrites sample 0's first outputs
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int k = 0; k < 7; ++k) out[k] = (float)tacc[k];
+#endif
     if constexpr (LOGP) {
         const double t = block_sum_f64<512>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
@@ -515,6 +521,23 @@ __global__ __launch_bounds__(256) void made_seqs_image_kernel(float* __restrict_
         img[S.w3 + e] = P[L.s_w3 + a * Hp + b];
     }
     float* tab = img + S.tab;
+    // block-ready step rows (made_seqs_kernel's LDS-DMA staging source), zero rows past d
+    const int rows = d + kSeqsPadRows;
+    constexpr int RS4 = seqs_w4_stride(Hp);
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < rows * Hp; e += gridDim.x * 256) {
+        const int i = e / Hp, pos = e % Hp;
+        packed[L.sw1 + e] = i < d ? P[L.s_w1t + (size_t)i * Hp + (int)ordU[rank_at(pos)]] : 0.f;
+    }
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < rows * RS4; e += gridDim.x * 256) {
+        const int i = e / RS4, c = e % RS4;
+        float v = 0.f;
+        if (i < d && c < 2 * Hp) v = P[L.s_w4 + (size_t)((c & 1) * d + i) * Hp + (int)ordU[c >> 1]];
+        packed[L.sw4 + e] = v;
+    }
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < 2 * rows; e += gridDim.x * 256) {
+        const int jb = e / rows, i = e % rows;
+        packed[L.sb4 + e] = i < d ? P[L.s_b4 + jb * d + i] : 0.f;
+    }
     for (int p = blockIdx.x * 256 + threadIdx.x; p < Hp; p += gridDim.x * 256) {
         tab[S.b1 + p] = P[L.s_b1 + (int)ordU[rank_at(p)]];
         tab[S.b2 + p] = P[L.s_b2 + (int)ordU[p]];
