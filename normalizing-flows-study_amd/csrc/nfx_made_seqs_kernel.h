@@ -271,11 +271,17 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             }
         }
     };
+    // the wave's 4 rows of the block's inputs: range-checked buffer loads (rows >= B and dims
+    // past the block read 0), no branches
     auto x_load = [&](int64_t gb, int i0, int n, float (&xr)[4]) {
+        const int64_t r0 = gb + wave * 4;
+        const int64_t nrows = B - r0 < 4 ? (B - r0 > 0 ? B - r0 : 0) : 4;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + (r0 < B ? r0 : 0) * d, 0,
+                                                          (int)(nrows * d * 4), 0x00020000);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int64_t sr = gb + wave * 4 + q;
-            xr[q] = (sr < B && lane < n) ? in[sr * d + i0 + lane] : 0.f;
+            const int voff = lane < n ? (q * d + i0 + lane) * 4 : (int)0x7FFFFFF0;
+            xr[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0));
         }
     };
 
