@@ -190,6 +190,10 @@ int nfx_made_affine_logprob(const float* packed, const float* in, float* out, fl
  * ------------------------------------------------------------------------------------- */
 int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
 size_t nfx_made_backward_factor_floats(int64_t B, int d, int H);
+/* Largest B one nfx_made_affine_backward / nfx_made_seq_backward / nfx_made_backward_weights
+ * call accepts (the factor rows use 32-bit buffer offsets); larger batches are split by the
+ * caller (the gradients are sums over samples). Above it the calls return NFX_EUNSUPPORTED. */
+int64_t nfx_made_backward_max_batch(int d, int H);
 int nfx_made_affine_backward(const float* packed, const float* in, const float* grad_out,
                              const float* grad_log_det, float* grad_in, float* factors, int64_t B,
                              int d, int H, int variant, void* stream);

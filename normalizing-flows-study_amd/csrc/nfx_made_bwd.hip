@@ -1,6 +1,16 @@
-// Backward (training) pass of the MAF density direction — MaskedAutoregressiveFlow.inverse
-// (masked_autoregressive_flow.py:18-44) under autograd, d <= 64, H <= 64, no BatchNorm.
-// SURVEY.md §8(f) item 1.
+// Backward (training) pass of the PARALLEL MADE directions — MaskedAutoregressiveFlow.inverse
+// (MAF density, masked_autoregressive_flow.py:18-44) and InverseAutoregressiveFlow.forward (IAF
+// sampling, inverse_autoregressive_flow.py:30-63) under autograd, no BatchNorm.
+// SURVEY.md §8(f) item 1. Two kernels:
+//   made_bwd_kernel<HT, VAR>   d <= 64, H <= 64: weights (forward image + padded transposed
+//                              copy) LDS-resident, x tiles by LDS-DMA;
+//   made_bwdw_kernel<HT, VAR>  d <= 4096, H <= 128 (e.g. IAF(784, 64) sampling): x streamed
+//                              through a 32 x 32 LDS stage per input chunk, the output layer per
+//                              (mu, alpha) block pair in two passes, weights read from L2.
+// Both serve both parallel directions (VAR = NFX_MAF_INVERSE | NFX_IAF_FORWARD epilogue).
+// Batch limit: the feature-major factor rows are addressed with 32-bit buffer offsets, so
+// nfx_made_affine_backward accepts B <= nfx_made_backward_max_batch(d, H) (the host chunks the
+// batch above it).
 //
 // One fused kernel per layer recomputes the forward on fp32 MFMA (same tile kernel structure
 // as made_tile_kernel: a wave owns 32 samples, hidden activations stay in accumulator registers)
@@ -14,7 +24,7 @@
 // and the weight gradients are MFMA sample contractions over them
 // (nfx_made_wgrad.hip: gW4 = δ4·h3ᵀ, …, gW1 = δ1·xᵀ), masked like the reference's weight*mask.
 //
-// Epilogue backward, per element (torch semantics of the reference ops):
+// Epilogue backward (MAF density), per element (torch semantics of the reference ops):
 //   a = clamp(alpha, -3, 3); e = exp(-a); zr = (x - mu) * e; z = finite(zr) ? zr : 0
 //   ld_raw = -sum a; ld1 = finite(ld_raw) ? ld_raw : 0; ld = clamp(ld1, -100, 100)
 //   gzr = finite(zr) ? gz : 0;  gld1 = gld * [-100 <= ld1 <= 100] * finite(ld_raw)
@@ -833,6 +843,20 @@ extern "C" int nfx_made_pack_backward(const NfxMlpRaw* net, int d, int H, float*
     return check_launch("made_bwd_pack_kernel");
 }
 
+// Largest batch one backward call accepts: every feature-major factor region (at most
+// max(2d, d + 1, 32 HT + 1) rows of pitch B) must stay within a 32-bit buffer range, and the
+// weight-gradient contraction reads 32-row tiles with 32-bit offsets (32 B 4 < 2^31).
+extern "C" int64_t nfx_made_backward_max_batch(int d, int H) {
+    if (d <= 0 || H <= 0) return 0;
+    const int64_t HT = (H + 31) / 32;
+    int64_t rows = 2 * (int64_t)d;
+    if (d + 1 > rows) rows = d + 1;
+    if (32 * HT + 1 > rows) rows = 32 * HT + 1;
+    const int64_t lim = ((int64_t)1 << 31) - 1;
+    const int64_t b1 = lim / (4 * rows), b2 = lim / (4 * 32);
+    return b1 < b2 ? b1 : b2;
+}
+
 extern "C" size_t nfx_made_backward_factor_floats(int64_t B, int d, int H) {
     if (B < 0 || d <= 0 || H <= 0) return 0;
     return (size_t)B * (size_t)(3 * d + 6 * H + 4);
@@ -847,6 +871,10 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_affine_backward: bad shape");
     if (d > 4096 || H > 128)
         return set_error(NFX_EUNSUPPORTED, "made_affine_backward: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (B > nfx_made_backward_max_batch(d, H))
+        return set_error(NFX_EUNSUPPORTED, "made_affine_backward: B=%lld above nfx_made_backward_max_batch(%d, %d) = "
+                                           "%lld (32-bit factor offsets); split the batch", (long long)B, d, H,
+                         (long long)nfx_made_backward_max_batch(d, H));
     if (B == 0) return NFX_OK;
     if (!packed || !in || !grad_out || !grad_log_det || !grad_in || !factors)
         return set_error(NFX_EINVAL, "made_affine_backward: null pointer");

@@ -305,6 +305,8 @@ static made_seq_bwd_t seq_bwd_pick(int HT) {
 
 using namespace nfx;
 
+extern "C" int64_t nfx_made_backward_max_batch(int d, int H);
+
 extern "C" int nfx_made_seq_backward(const float* packed, const float* in, const float* grad_out,
                                      const float* grad_log_det, float* grad_in, float* factors, int64_t B, int d, int H,
                                      int variant, void* stream) {
@@ -314,6 +316,10 @@ extern "C" int nfx_made_seq_backward(const float* packed, const float* in, const
     if (B < 0 || d <= 0 || H <= 0) return set_error(NFX_EINVAL, "made_seq_backward: bad shape");
     if (d > 4096 || H > 128)
         return set_error(NFX_EUNSUPPORTED, "made_seq_backward: d=%d H=%d outside d<=4096, H<=128", d, H);
+    if (B > nfx_made_backward_max_batch(d, H))
+        return set_error(NFX_EUNSUPPORTED, "made_seq_backward: B=%lld above nfx_made_backward_max_batch(%d, %d) = "
+                                           "%lld (32-bit factor offsets); split the batch", (long long)B, d, H,
+                         (long long)nfx_made_backward_max_batch(d, H));
     if (B == 0) return NFX_OK;
     if (!packed || !in || !grad_out || !grad_log_det || !grad_in || !factors)
         return set_error(NFX_EINVAL, "made_seq_backward: null pointer");

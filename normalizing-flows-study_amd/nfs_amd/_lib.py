@@ -35,7 +35,8 @@ EXPORTED_SYMBOLS = (
     "nfx_rqs_unit",
     "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
-    "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_affine_backward",
+    "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_backward_max_batch",
+    "nfx_made_affine_backward",
     "nfx_made_seq_backward", "nfx_made_factor_pitch", "nfx_made_param_floats", "nfx_made_wgrad_workspace_bytes", "nfx_made_backward_weights",
     "nfx_affine_train_pack_floats", "nfx_affine_train_stats_doubles", "nfx_affine_train_grad_doubles",
     "nfx_affine_train_param_floats", "nfx_affine_train_workspace_bytes", "nfx_affine_train_pack",
@@ -104,6 +105,7 @@ _SIGNATURES = {
     "nfx_made_affine_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_made_pack_backward": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
     "nfx_made_backward_factor_floats": (_sz, [_i64, _int, _int]),
+    "nfx_made_backward_max_batch": (_i64, [_int, _int]),
     "nfx_made_affine_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_made_seq_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_made_factor_pitch": (_i64, [_i64]),

@@ -162,12 +162,27 @@ class _MadeAffineFlow(HipFlow):
         return d <= MAX_D and H <= MAX_H_BWD
 
     def _hip_backward(self, x, gz, gld, direction):
-        """dL/dx and the parameter gradients (in self.parameters() order) of one call."""
+        """dL/dx and the parameter gradients (in self.parameters() order) of one call. Batches
+        above nfx_made_backward_max_batch (32-bit factor offsets) run in chunks: dL/dx is per
+        sample and every parameter gradient is a sum over samples."""
         x = x.contiguous()
         B, d = x.shape
         H = self.conditioner.hidden_dim
         gz = torch.zeros_like(x) if gz is None else gz.contiguous().float()
         gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
+        cap = int(_lib.lib().nfx_made_backward_max_batch(d, H))
+        if B > cap:
+            gxs, acc = [], None
+            for lo in range(0, B, cap):
+                gxc, gpc = self._hip_backward_chunk(x[lo:lo + cap], gz[lo:lo + cap], gld[lo:lo + cap], direction)
+                gxs.append(gxc)
+                acc = gpc if acc is None else [a + g for a, g in zip(acc, gpc)]
+            return torch.cat(gxs), acc
+        return self._hip_backward_chunk(x, gz, gld, direction)
+
+    def _hip_backward_chunk(self, x, gz, gld, direction):
+        B, d = x.shape
+        H = self.conditioner.hidden_dim
         packed = self._packed(x.device, self._build_pack)
         L = _lib.lib()
         gx = torch.empty_like(x)

@@ -79,11 +79,14 @@ class HipFlowFunction(torch.autograd.Function):
         layer = ctx.layer
         params = [p for p in layer.parameters()]
         if getattr(layer, "_hip_backward_ok", None) is not None and layer._hip_backward_ok(x, ctx.direction):
-            # fused gfx950 backward (MAF density direction, spline coupling)
+            # fused gfx950 backward (MADE flows, spline coupling, eval-mode affine coupling)
             STATS["hip"] += 1
             gx, gparams = layer._hip_backward(x.detach(), gy, gld, ctx.direction)
             gparams = [g if p.requires_grad else None for p, g in zip(params, gparams)]
             return (None, None, gx, *gparams)
+        # composite recompute through ATen on the GPU: counted as a torch call, so
+        # STATS["torch"] == 0 after a backward proves every layer ran a fused backward kernel
+        STATS["torch"] += 1
         with torch.enable_grad():
             xr = x.detach().requires_grad_(True)
             y, ld = layer._torch_call(xr, ctx.direction)
@@ -219,8 +222,13 @@ def drop_pack_caches(module):
     parameters) and before a graph capture that must record the pack kernels."""
     for m in module.modules():
         if isinstance(m, HipFlow):
-            for k in [k for k in m.__dict__ if k.startswith("_nfx_") and k.endswith("pack_cache")]:
-                del m.__dict__[k]
+            drop_layer_pack_caches(m)
+
+
+def drop_layer_pack_caches(layer):
+    """Forget the cached packed-weight images of one HipFlow layer (every `_packed` slot)."""
+    for k in [k for k in layer.__dict__ if k.startswith("_nfx_") and k.endswith("pack_cache")]:
+        del layer.__dict__[k]
 
 
 class SequentialFlow(Flow):

@@ -136,8 +136,7 @@ class GraphedTrainStep:
 
     def _forget(self):
         for m in self._hipflows:
-            for k in [k for k in m.__dict__ if k.startswith("_nfx_") and k.endswith("pack_cache")]:
-                del m.__dict__[k]
+            _flows.drop_layer_pack_caches(m)
 
     def _step(self, zero=True):
         if zero:

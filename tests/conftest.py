@@ -1,5 +1,6 @@
 import json
 import os
+import re
 import sys
 
 import numpy as np
@@ -52,47 +53,108 @@ def cuda_device():
     return torch.device("cuda:0")
 
 
-def fp32_jitter(fn, *inputs, k=8, seed=0):
-    """Per-element fp32 sensitivity of `fn` (an fp32 oracle closure returning a tuple of
-    tensors): the largest deviation from fn(*inputs) over k evaluations whose inputs are
-    jittered by -1/0/+1 ulp per element. A one-ulp nudge of the inputs re-randomises every
-    internal fp32 rounding downstream (MLP logits, softmax, knot cumsum, the root), so the spread
-    is the variation a different but equally valid fp32 evaluation order can produce. NaN
-    deviations (a jitter crossing a guard) count as infinitely sensitive."""
+_NET_KEY = re.compile(r"^(.*?(?:param_net|s_net|b_net|net)\.)(\d+)\.(\w+)$")
+
+
+def permute_hidden(sd, gen):
+    """The same network with its hidden units listed in a random order: rows of every Linear
+    (weight, bias, MADE mask) feeding a hidden layer, the BatchNorm parameters/buffers of that
+    layer, and the matching columns of the next Linear are permuted together. Mathematically
+    the identical function; in fp32 every matmul sums its products in a different order — an
+    equally valid evaluation of the reference math (the GPU kernels sum in MFMA order)."""
+    nets = {}
+    for key in sd:
+        m = _NET_KEY.match(key)
+        if m:
+            nets.setdefault(m.group(1), {}).setdefault(int(m.group(2)), {})[m.group(3)] = key
+    out = dict(sd)
+    for layers in nets.values():
+        lin = sorted(i for i, f in layers.items() if "weight" in f and sd[f["weight"]].dim() == 2)
+        for a, b in zip(lin, lin[1:]):
+            n = out[layers[a]["weight"]].shape[0]
+            perm = torch.randperm(n, generator=gen)
+            for f in ("weight", "bias", "mask"):
+                if f in layers[a]:
+                    out[layers[a][f]] = out[layers[a][f]][perm]
+            for i in range(a + 1, b):
+                for key in layers.get(i, {}).values():
+                    t = out[key]
+                    if t.dim() == 1 and t.shape[0] == n:
+                        out[key] = t[perm].clone()
+            for f in ("weight", "mask"):
+                if f in layers[b]:
+                    out[layers[b][f]] = out[layers[b][f]][:, perm]
+    return {k: (v.contiguous().clone() if torch.is_tensor(v) else v) for k, v in out.items()}
+
+
+class Ensemble:
+    """Equally valid fp32 evaluations of one oracle output: `members` [M, N] float64 (NaN where
+    a member crossed a guard the base evaluation did not: such a member is NOT used), and the
+    number of those guard crossings."""
+
+    def __init__(self, members, n_guard):
+        self.members = members
+        self.n_guard = n_guard
+
+
+def fp32_jitter(fn, *inputs, k=8, seed=0, sd=None, n_perm=8):
+    """Ensemble of equally valid fp32 evaluations of an fp32 oracle closure (returns one
+    `Ensemble` per output of `fn`):
+      * k evaluations with every input element jittered by -1/0/+1 ulp — a one-ulp nudge
+        re-randomises every internal fp32 rounding downstream (MLP logits, softmax, knot
+        cumsum, the root);
+      * with `sd` given (then `fn(sd, *inputs)`), n_perm evaluations of the same network with
+        its hidden units permuted (`permute_hidden`) — a different summation order in every
+        matmul, the freedom the GPU's MFMA order uses.
+    A member that is NaN where the base evaluation is finite (a jitter crossing a guard) is
+    dropped for that element and counted; it never widens any bound."""
     g = torch.Generator().manual_seed(seed)
+    call = (lambda s, *v: fn(s, *v)) if sd is not None else (lambda s, *v: fn(*v))
     with torch.no_grad():
-        base = [o.double() for o in fn(*inputs)]
-        dev = [torch.zeros_like(o) for o in base]
+        base = [o.double() for o in call(sd, *inputs)]
+        mem = [[b.clone()] for b in base]
         for _ in range(k):
             jit = []
             for t in inputs:
                 step = torch.randint(-1, 2, t.shape, generator=g).to(t.dtype) * t.abs() * 2.0 ** -23
                 jit.append(torch.where(torch.isfinite(t), t + step, t))
-            for i, o in enumerate(fn(*jit)):
-                dd = (o.double() - base[i]).abs()
-                dd = torch.where(torch.isnan(dd) & ~torch.isnan(base[i]), torch.full_like(dd, float("inf")), dd)
-                dev[i] = torch.maximum(dev[i], torch.nan_to_num(dd, nan=0.0))
-    return [d.numpy() for d in dev]
+            for i, o in enumerate(call(sd, *jit)):
+                mem[i].append(o.double())
+        if sd is not None:
+            for _ in range(n_perm):
+                for i, o in enumerate(call(permute_hidden(sd, g), *inputs)):
+                    mem[i].append(o.double())
+    out = []
+    for i, b in enumerate(base):
+        M = torch.stack([m.reshape(-1) for m in mem[i]]).numpy()
+        bn = np.isnan(b.reshape(-1).numpy())
+        guard = np.isnan(M) & ~bn[None, :]
+        M = np.where(np.isfinite(M) | bn[None, :], M, np.nan)  # drop non-finite members of finite elements
+        out.append(Ensemble(M, int(guard.sum())))
+    return out
 
 
-def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=None, what="", kind=None, max_ill=0.02, sens=None):
+BIG_ERR = 1e-2
+
+
+def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=None, what="", kind=None, max_ill=0.02, sens=None,
+                       rows=None):
     """Per-element parity of ill-conditioned fp32 math (RQ spline chains, train-mode chains).
 
-    Every element must lie within SURVEY §8(c)'s fixed tolerance of the reference's own fp32
-    result (cpu32):
-      values    |gpu - cpu32| <= 1e-5 (1 + |cpu32|)           log-dets   |gpu - cpu32| <= 1e-4
-    except elements whose MEASURED fp32 conditioning c = max(|cpu32 - ref64|, sens) widens the
-    bound to  tol + 8 c : ref64 is the float64 evaluation of the same math (the oracle run in
-    double) and sens (conftest.fp32_jitter) the spread of one-ulp-jittered fp32 evaluations —
-    how far an equally valid fp32 evaluation order can land. Near a knot with steep end
-    derivatives the reference's own fp32 log-det is up to ~1e-3 off float64, and there the
-    bound follows the measured sensitivity element by element (no blanket floor). At most
-    `max_ill` of the elements (default 2 %, at least 3) may need the widened bound; the count is
-    printed. Whole-tensor guards: mean|gpu - ref64| <= 1.5 mean|cpu32 - ref64| + 1e-7 and
-    max|gpu - ref64| <= 4 max|cpu32 - ref64| + slack (as accurate as the reference, never
-    systematically worse). NaN patterns must agree. `kind` ("y" or "ld") defaults from `what`;
-    `floor` is accepted for old call sites and ignored."""
-    import re
+    Fixed tolerance: values |d| <= 1e-5 (1 + |ref|), log-dets |d| <= 1e-4.
+    Every element must be
+      (a) within the fixed tolerance of the reference's own fp32 result (cpu32) or of one of the
+          equally valid fp32 evaluations in `sens` (conftest.fp32_jitter: one-ulp input jitter,
+          hidden-unit order), or
+      (b) inside the hull of those evaluations and the float64 evaluation ref64, widened by the
+          fixed tolerance — "relaxed"; at most `max_ill` (2 %, at least 3) of the elements.
+    No unbounded widening exists: an evaluation that crossed a guard (NaN) is dropped, never
+    turned into an infinite sensitivity. Every accepted element whose error exceeds 1e-2 is
+    printed with its justification: valid fp32 evaluations that differ by at least that much
+    (the element sits on an fp32-chaotic branch; `rows` adds its input row to the line).
+    Whole-tensor guards: mean|gpu - ref64| <= 1.5 mean|cpu32 - ref64| + 1e-7 and
+    max|gpu - ref64| <= 4 max|cpu32 - ref64| + slack. NaN patterns must agree. `kind` ("y" or
+    "ld") defaults from `what`; `floor` is accepted for old call sites and ignored."""
     if kind is None:
         kind = "ld" if re.search(r"\bld\b|log_det", what) else "y"
     g = np.asarray(gpu, np.float64).ravel()
@@ -100,27 +162,48 @@ def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=None, what="", kind=
     r = np.asarray(ref64, np.float64).ravel()
     assert np.array_equal(np.isnan(g), np.isnan(c)), f"{what}: NaN pattern differs from the reference"
     ok = ~np.isnan(c) & ~np.isnan(r)
-    sv = np.zeros_like(r) if sens is None else np.asarray(sens, np.float64).ravel()
-    g, c, r, sv = g[ok], c[ok], r[ok], sv[ok]
+    idx = np.nonzero(ok)[0]
+    M = None if sens is None else np.asarray(sens.members, np.float64)[:, ok]
+    g, c, r = g[ok], c[ok], r[ok]
     if g.size == 0:
         return {"n": 0, "relaxed": 0}
-    ec = np.abs(c - r)
-    cond = np.maximum(ec, sv)
     tol = 1e-5 * (1 + np.abs(c)) if kind == "y" else np.full_like(c, 1e-4)
     err = np.abs(g - c)
-    bad = err > tol + 8 * cond
-    assert not bad.any(), (f"{what}: {int(bad.sum())} elements exceed fixed tolerance + 8x their fp32 "
-                           f"conditioning; worst excess {(err - tol - 8 * cond)[bad].max():.3g} "
-                           f"(err {err[bad].max():.3g})")
-    relaxed = err > tol
+    near = err <= tol
+    lo, hi = np.minimum(c, r), np.maximum(c, r)
+    if M is not None:
+        with np.errstate(invalid="ignore"):
+            near |= np.any(np.abs(M - g[None, :]) <= tol[None, :], axis=0)
+            lo = np.fmin(lo, np.nanmin(np.where(np.isnan(M), np.inf, M), axis=0))
+            hi = np.fmax(hi, np.nanmax(np.where(np.isnan(M), -np.inf, M), axis=0))
+    hull = (g >= lo - tol) & (g <= hi + tol)
+    bad = ~near & ~hull
+    if bad.any():
+        j = int(np.argmax(np.where(bad, err, -1)))
+        raise AssertionError(f"{what}: {int(bad.sum())} elements outside the fixed tolerance of every valid fp32 "
+                             f"evaluation and outside their hull; worst element {int(idx[j])}: gpu {g[j]!r} "
+                             f"reference {c[j]!r} float64 {r[j]!r} hull [{lo[j]!r}, {hi[j]!r}]")
+    relaxed = ~near
     n_rel = int(relaxed.sum())
     if not os.environ.get("NFX_MEASURE_ILL"):
-        assert n_rel <= max(3, max_ill * g.size), (f"{what}: {n_rel}/{g.size} elements need the "
-                                                  f"conditioning-widened bound (> {max_ill:.0%})")
+        assert n_rel <= max(3, max_ill * g.size), (f"{what}: {n_rel}/{g.size} elements need the hull of the "
+                                                  f"valid fp32 evaluations (> {max_ill:.0%})")
     eg = np.abs(g - r)
+    ec = np.abs(c - r)
     assert eg.mean() <= 1.5 * ec.mean() + 1e-7, f"{what}: mean err {eg.mean():.3g} vs reference {ec.mean():.3g}"
     assert eg.max() <= 4 * ec.max() + slack, f"{what}: max err {eg.max():.3g} vs reference {ec.max():.3g}"
-    print(f"[fp32 parity] {what}: {g.size - n_rel}/{g.size} within the fixed tolerance, {n_rel} "
-          f"({n_rel / g.size:.2%}) within tol + 8x measured conditioning; "
-          f"{int((cond > tol).sum())} with conditioning above the tolerance; max err {err.max():.3g}")
+    n_near_c = int((err <= tol).sum())
+    guard = "" if sens is None else f"; {sens.n_guard} guard-crossing evaluations dropped"
+    print(f"[fp32 parity] {what}: {n_near_c}/{g.size} within the fixed tolerance of the reference, "
+          f"{g.size - n_near_c - n_rel} of another valid fp32 evaluation, {n_rel} ({n_rel / g.size:.2%}) in their "
+          f"hull; max err {err.max():.3g}{guard}")
+    rows_np = None if rows is None else np.asarray(rows, np.float64).reshape(-1, 1) if np.asarray(rows).ndim == 1 \
+        else np.asarray(rows, np.float64)
+    for j in np.nonzero(err > BIG_ERR)[0]:
+        e = int(idx[j])
+        row = "" if rows_np is None else f" input row {rows_np[e // (len(np.asarray(gpu).ravel()) // len(rows_np))].tolist()}"
+        print(f"[fp32 parity]   {what} element {e}{row}: err {err[j]:.3g} — fp32-chaotic branch: valid fp32 "
+              f"evaluations span [{lo[j]:.6g}, {hi[j]:.6g}] (spread {hi[j] - lo[j]:.3g}; reference fp32 "
+              f"{c[j]:.6g}, float64 {r[j]:.6g}, gpu {g[j]:.6g})")
+        assert hi[j] - lo[j] >= BIG_ERR, f"{what}: element {e} err {err[j]:.3g} without an fp32-chaotic justification"
     return {"n": int(g.size), "relaxed": n_rel}

@@ -27,6 +27,12 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
                       both directions + log_prob, and a train-mode forward (running-stat update)
   g13_sequential.npz  SequentialFlow (sequential_flow.py:5-34): 4 CouplingLayers d=2 as in
                       examples/visualization_demo.py:26-36, and a mixed d=5 chain
+  g14_grads.npz       gradients (dL/dx + every parameter) through the reference's own MAF(10,32),
+                      IAF(10,32), MAF(63,64), IAF(784,64) (both directions, the sequential ones through
+                      all d MADE calls) and SplineCouplingLayer K=8 (d=2, H=64) / K=10 (d=3, H=32)
+  g15_fig_train.npz   the benchmark-figure model RealNVP(2,10,128) (plots/_common.py:161) trained as
+                      plots/_common.py:194-211: train-mode step on 2,000 two-moons points (z, ld, loss,
+                      gradients, running stats) and 5 Adam + clip steps (losses, final state)
   g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes (+ cfg5: IAF(784,64)
                       inverse NLL at B=8192 and forward checksums at B=524288)
 
@@ -477,6 +483,101 @@ def g13(flows):
     np.savez_compressed(os.path.join(HERE, "g13_sequential.npz"), **out)
 
 
+def g14(flows):
+    """Gradients through the reference's own layers under autograd (loss = sum(y * wy) +
+    sum(ld * wl), random weights wy, wl): MaskedAutoregressiveFlow and InverseAutoregressiveFlow in
+    both directions (masked_autoregressive_flow.py:18-78, inverse_autoregressive_flow.py:30-103,
+    the sequential directions differentiated through all d MADE calls) and SplineCouplingLayer
+    (spline_coupling_layer.py:96-309), K = 8 and 10, both directions. Stores y, ld, dL/dx and
+    every parameter gradient per case."""
+    out = {}
+    g = torch.Generator().manual_seed(140)
+    cases = [
+        ("maf10", lambda: flows.MaskedAutoregressiveFlow(10, 32), 0.1, 300, 1.0),
+        ("iaf10", lambda: flows.InverseAutoregressiveFlow(10, 32), 0.1, 300, 1.0),
+        ("maf63", lambda: flows.MaskedAutoregressiveFlow(63, 64), 0.02, 128, 1.0),
+        ("iaf784", lambda: flows.InverseAutoregressiveFlow(784, 64), 0.01, 8, 1.0),
+        ("sp8", lambda: flows.SplineCouplingLayer(2, 64, torch.tensor([1.0, 0.0]), num_bins=8), 0.1, 500, 2.5),
+        ("sp10", lambda: flows.SplineCouplingLayer(3, 32, torch.tensor([0.0, 1.0, 0.0]), num_bins=10), 0.1, 500, 2.5),
+    ]
+    for i, (name, ctor, sigma, B, scale) in enumerate(cases):
+        torch.manual_seed(1400 + i)
+        m = ctor()
+        perturb(m, sigma, 1410 + i)
+        m.eval()
+        out.update(sd_arrays(m, name + ".init."))
+        d = m.dim if hasattr(m, "dim") else m.data_dim
+        x = torch.randn(B, d, generator=g) * scale
+        if name.startswith("sp"):
+            x[:4, -1] = torch.tensor([6.0, -7.0, 4.999, -4.999])  # outside / at the spline bound
+        wy = torch.randn(B, d, generator=g)
+        wl = torch.randn(B, generator=g)
+        out.update({f"{name}.x": x.numpy(), f"{name}.wy": wy.numpy(), f"{name}.wl": wl.numpy()})
+        for dname, fn in (("inv", m.inverse), ("fwd", m.forward)):
+            m.zero_grad()
+            xr = x.clone().requires_grad_(True)
+            y, ld = fn(xr)
+            ((y * wy).sum() + (ld * wl).sum()).backward()
+            out[f"{name}.{dname}.y"] = y.detach().numpy()
+            out[f"{name}.{dname}.ld"] = ld.detach().numpy()
+            out[f"{name}.{dname}.gx"] = xr.grad.numpy()
+            for k, p in m.named_parameters():
+                out[f"{name}.{dname}.grad.{k}"] = p.grad.numpy()
+        print("g14", name, flush=True)
+    np.savez_compressed(os.path.join(HERE, "g14_grads.npz"), **out)
+
+
+def figure_moons(n, seed):
+    """plots/_common.py:103-112 (two_moons: make_moons(noise=0.07) standardized, float32)."""
+    from sklearn.datasets import make_moons
+    x, _ = make_moons(n_samples=n, noise=0.07, random_state=seed)
+    x = np.asarray(x, dtype=np.float32)
+    return torch.from_numpy((x - x.mean(0)) / (x.std(0) + 1e-8))
+
+
+def g15(models):
+    """The reference's benchmark-figure model in training: RealNVP(2, 10, 128)
+    (plots/_common.py:161), full-batch step on 2,000 two-moons points (NDATA, :183) in train mode
+    with the loop of plots/_common.py:194-211 (Adam lr 1e-3, clip_grad_norm_ 5.0). Stores the
+    first step's z, ld, loss and raw gradients (before the clip), the running statistics after it,
+    and the losses + final state of 5 full steps."""
+    from torch.distributions import MultivariateNormal
+    out = {}
+    x = figure_moons(2000, 0)
+    out["fig.x"] = x.numpy()
+    base = MultivariateNormal(torch.zeros(2), torch.eye(2))
+
+    def fresh():
+        torch.manual_seed(150)
+        m = models.RealNVP(2, 10, 128)
+        perturb(m, 0.03, 151)
+        return m.train()
+
+    m = fresh()
+    out.update(sd_arrays(m, "fig.init."))
+    z, ld = m.inverse(x)
+    loss = -(base.log_prob(z) + ld).mean()
+    loss.backward()
+    out.update({"fig.z": z.detach().numpy(), "fig.ld": ld.detach().numpy(), "fig.loss": np.float64(loss.item())})
+    for k, p in m.named_parameters():
+        out["fig.grad." + k] = p.grad.numpy()
+    out.update({k: v for k, v in sd_arrays(m, "fig.after.").items() if k.endswith(("running_mean", "running_var"))})
+    m = fresh()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(5):
+        z, ld = m.inverse(x)
+        loss = -(base.log_prob(z) + ld).mean()
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 5.0)
+        opt.step()
+        losses.append(loss.item())
+    out["fig.losses5"] = np.asarray(losses, dtype=np.float64)
+    out.update(sd_arrays(m, "fig.step5."))
+    np.savez_compressed(os.path.join(HERE, "g15_fig_train.npz"), **out)
+
+
 def g8_cfg5(f6):
     """cfg5 IAF(784,64) (G6 weights): inverse NLL at B=8192 (seed 1237) and forward checksums at
     B=524288 (seed 1238); merged into g8_full_nll.json."""
@@ -565,6 +666,12 @@ def main():
     if a.only == "g13":
         g13(flows)
         return
+    if a.only == "g14":
+        g14(flows)
+        return
+    if a.only == "g15":
+        g15(models)
+        return
     if a.only == "g8_cfg5":
         g8_cfg5(g6(flows))
         return
@@ -580,6 +687,8 @@ def main():
     g10(flows)
     g12(flows, models)
     g13(flows)
+    g14(flows)
+    g15(models)
     if not a.skip_full:
         g8(m2, m3, m5)
         g8_cfg5(f6)

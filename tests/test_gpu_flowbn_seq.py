@@ -80,10 +80,10 @@ def test_between_layer_bn_eval_vs_reference(cuda_device, name):
             z64, l64 = oracle.flow_model(sd, spec_fn(False), x.cpu().double(), -1, bn_prefix=bnp)
             x64, lf64 = oracle.flow_model(sd, spec_fn(False), z.cpu().double(), 1, bn_prefix=bnp)
         sd32 = {k: v for k, v in oracle_sd(g, name + ".").items() if not k.startswith("after_train.")}
-        si = fp32_jitter(lambda v: oracle.flow_model(sd32, spec_fn(False), v, -1, bn_prefix=bnp), x.cpu())
-        sf = fp32_jitter(lambda v: oracle.flow_model(sd32, spec_fn(False), v, 1, bn_prefix=bnp), z.cpu())
-        assert_fp32_parity(zi.cpu(), ref["inv_z"], z64, what="inv z", sens=si[0])
-        assert_fp32_parity(ldi.cpu(), ref["inv_ld"], l64, what="inv ld", sens=si[1])
+        si = fp32_jitter(lambda s, v: oracle.flow_model(s, spec_fn(False), v, -1, bn_prefix=bnp), x.cpu(), sd=sd32)
+        sf = fp32_jitter(lambda s, v: oracle.flow_model(s, spec_fn(False), v, 1, bn_prefix=bnp), z.cpu(), sd=sd32)
+        assert_fp32_parity(zi.cpu(), ref["inv_z"], z64, what="inv z", sens=si[0], rows=x.cpu())
+        assert_fp32_parity(ldi.cpu(), ref["inv_ld"], l64, what="inv ld", sens=si[1], rows=x.cpu())
         assert_fp32_parity(xf.cpu(), ref["fwd_x"], x64, what="fwd x", sens=sf[0])
         assert_fp32_parity(ldf.cpu(), ref["fwd_ld"], lf64, what="fwd ld", sens=sf[1])
         nll_ref = -float(torch.from_numpy(ref["log_prob"][:2000]).double().mean())  # 24 edge rows at the end
@@ -125,11 +125,11 @@ def test_between_layer_bn_train_forward_updates_running_stats(cuda_device, name)
             x64, l64 = oracle.flow_model(sd, spec_fn(True), z.cpu().double(), 1, bn_prefix=bnp, training=True)
         sd32 = {k: v for k, v in oracle_sd(g, name + ".").items() if not k.startswith("after_train.")}
 
-        def fwd_train(v):  # a fresh copy per call: train mode updates the running stats in place
-            s2 = {k: t.clone() for k, t in sd32.items()}
+        def fwd_train(s, v):  # a fresh copy per call: train mode updates the running stats in place
+            s2 = {k: t.clone() for k, t in s.items()}
             return oracle.flow_model(s2, spec_fn(True), v, 1, bn_prefix=bnp, training=True)
 
-        st = fp32_jitter(fwd_train, z.cpu())
+        st = fp32_jitter(fwd_train, z.cpu(), sd=sd32)
         assert_fp32_parity(xt.cpu(), g[f"{name}.train_fwd_x"], x64, what="train fwd x", sens=st[0])
         assert_fp32_parity(ldt.cpu(), g[f"{name}.train_fwd_ld"], l64, what="train fwd ld", sens=st[1])
         return
@@ -160,8 +160,8 @@ def test_between_layer_bn_gradients_vs_float64(cuda_device, name, direction):
     gx, gp = run(m, x.to(cuda_device), w.to(cuda_device))
     stats = dict(nfs_amd.STATS)
     gx64, gp64 = run(m64, x.double(), w.double())
-    # the layer backward of the MAF sampling direction recomputes through the composite on the
-    # GPU (sequential; §8(f)1), everything else runs fused kernels
+    # every layer backward is a fused kernel (HipFlowFunction counts a composite recompute as
+    # a torch call), incl. the sequential MAF sampling direction (made_seq_bwd_kernel)
     assert stats["torch"] == 0, stats
     scale = float(gx64.abs().max())
     rel = float((gx.cpu().double() - gx64).abs().max()) / max(scale, 1e-12)
@@ -220,10 +220,10 @@ def test_sequential_flow_vs_reference(cuda_device, name):
             z64, l64 = oracle.sequential_flow(sd, G13_SPECS[name], x.cpu().double(), -1)
             x64, lf64 = oracle.sequential_flow(sd, G13_SPECS[name], z.cpu().double(), 1)
         sd32 = oracle_sd(g, name + ".")
-        si = fp32_jitter(lambda v: oracle.sequential_flow(sd32, G13_SPECS[name], v, -1), x.cpu())
-        sf = fp32_jitter(lambda v: oracle.sequential_flow(sd32, G13_SPECS[name], v, 1), z.cpu())
-        assert_fp32_parity(zi.cpu(), g[f"{name}.inv_z"], z64, what="inv z", sens=si[0])
-        assert_fp32_parity(ldi.cpu(), g[f"{name}.inv_ld"], l64, what="inv ld", sens=si[1])
+        si = fp32_jitter(lambda s, v: oracle.sequential_flow(s, G13_SPECS[name], v, -1), x.cpu(), sd=sd32)
+        sf = fp32_jitter(lambda s, v: oracle.sequential_flow(s, G13_SPECS[name], v, 1), z.cpu(), sd=sd32)
+        assert_fp32_parity(zi.cpu(), g[f"{name}.inv_z"], z64, what="inv z", sens=si[0], rows=x.cpu())
+        assert_fp32_parity(ldi.cpu(), g[f"{name}.inv_ld"], l64, what="inv ld", sens=si[1], rows=x.cpu())
         assert_fp32_parity(xf.cpu(), g[f"{name}.fwd_x"], x64, what="fwd x", sens=sf[0])
         assert_fp32_parity(ldf.cpu(), g[f"{name}.fwd_ld"], lf64, what="fwd ld", sens=sf[1])
     # the in-place chain equals the reference's per-layer composition bit for bit

@@ -70,8 +70,8 @@ def test_spline_model_vs_reference(cuda_device, tag):
         z64, l64 = oracle.flow_model(sd, spec, torch.from_numpy(g["x"]).double(), -1)
         x64, lf64 = oracle.flow_model(sd, spec, torch.from_numpy(g["z"]).double(), 1)
     sd32 = oracle_sd(g, tag)
-    si = fp32_jitter(lambda v: oracle.flow_model(sd32, spec, v, -1), torch.from_numpy(g["x"]))
-    sf = fp32_jitter(lambda v: oracle.flow_model(sd32, spec, v, 1), torch.from_numpy(g["z"]))
+    si = fp32_jitter(lambda s, v: oracle.flow_model(s, spec, v, -1), torch.from_numpy(g["x"]), sd=sd32)
+    sf = fp32_jitter(lambda s, v: oracle.flow_model(s, spec, v, 1), torch.from_numpy(g["z"]), sd=sd32)
     assert_fp32_parity(zi.cpu(), g[tag + "inv_z"], z64, what="inv z", sens=si[0])
     assert_fp32_parity(ldi.cpu(), g[tag + "inv_ld"], l64, what="inv ld", sens=si[1])
     assert_fp32_parity(xf.cpu(), g[tag + "fwd_x"], x64, what="fwd x", sens=sf[0])
@@ -97,8 +97,8 @@ def test_small_spline_layers(cuda_device, name):
         xd = x.cpu().double()
         yf64, lf64 = oracle.spline_coupling(sd64(sd), "", xd, 1)
         yi64, li64 = oracle.spline_coupling(sd64(sd), "", xd, -1)
-    sf = fp32_jitter(lambda v: oracle.spline_coupling(sd, "", v, 1), x.cpu())
-    si = fp32_jitter(lambda v: oracle.spline_coupling(sd, "", v, -1), x.cpu())
+    sf = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, 1), x.cpu(), sd=sd)
+    si = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, -1), x.cpu(), sd=sd)
     assert_fp32_parity(yf.cpu(), g[name + ".fwd_y"], yf64, what="fwd y", sens=sf[0])
     assert_fp32_parity(lf.cpu(), g[name + ".fwd_ld"], lf64, what="fwd ld", sens=sf[1])
     assert_fp32_parity(yi.cpu(), g[name + ".inv_y"], yi64, what="inv y", sens=si[0])
@@ -123,11 +123,11 @@ def test_spline_layer_shapes_vs_oracle(cuda_device, K, H):
             yg, lg = (layer.forward if direction > 0 else layer.inverse)(x.to(cuda_device))
             yr, lr = oracle.spline_coupling(sd, "", x, direction, K=K)
             y64, l64 = oracle.spline_coupling(sd64(sd), "", x.double(), direction, K=K)
-        sy, sl = fp32_jitter(lambda v: oracle.spline_coupling(sd, "", v, direction, K=K), x)
-        # stress weights (0.2 perturbation, K up to 11): up to ~4 % of the log-dets sit next to
-        # steep knots and need the conditioning-widened bound
+        sy, sl = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, direction, K=K), x, sd=sd)
+        # stress weights (0.2 perturbation, K up to 11): log-dets next to steep knots are
+        # ill-conditioned; they must match a valid fp32 evaluation (input jitter, hidden order)
         assert_fp32_parity(yg.cpu(), yr, y64, what=f"y dir={direction}", sens=sy)
-        assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}", sens=sl, max_ill=0.05)
+        assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}", sens=sl)
 
 
 def test_spline_rescale_and_edges(cuda_device):
@@ -149,8 +149,8 @@ def test_spline_rescale_and_edges(cuda_device):
             yr, lr = oracle.spline_coupling(sd, "", x, direction, K=6, data_min=-3.0, data_max=4.0)
             y64, l64 = oracle.spline_coupling(sd64(sd), "", x.double(), direction, K=6, data_min=-3.0, data_max=4.0)
         assert np.array_equal(np.isfinite(yg.cpu().numpy()), np.isfinite(yr.numpy()))
-        sy, sl = fp32_jitter(lambda v: oracle.spline_coupling(sd, "", v, direction, K=6, data_min=-3.0,
-                                                             data_max=4.0), x)
+        sy, sl = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, direction, K=6, data_min=-3.0,
+                                                                data_max=4.0), x, sd=sd)
         assert_fp32_parity(yg.cpu(), yr, y64, what=f"y dir={direction}", sens=sy)
         assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}", sens=sl)
 
@@ -214,6 +214,6 @@ def test_spline_extreme_logits_vs_oracle(cuda_device, K):
             y64, l64 = oracle.spline_coupling(sd64(sd), "", x.double(), direction, K=K)
         assert torch.isfinite(yr).all() and torch.isfinite(lr).all()
         assert torch.isfinite(yg).all() and torch.isfinite(lg).all()
-        sy, sl = fp32_jitter(lambda v: oracle.spline_coupling(sd, "", v, direction, K=K), x)
+        sy, sl = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, direction, K=K), x, sd=sd)
         assert_fp32_parity(yg.cpu(), yr, y64, what=f"y dir={direction}", sens=sy)
         assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}", sens=sl)
