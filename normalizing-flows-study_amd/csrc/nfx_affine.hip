@@ -211,8 +211,10 @@ int resident_grid(const void* kernel, int threads, size_t lds_bytes, int64_t wor
 int prepare_lds(const void* kernel, size_t bytes) {
     if (bytes > 65536) {
         if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) !=
-            hipSuccess)
+            hipSuccess) {
+            (void)hipGetLastError();  // do not leave the error sticky for the caller's next HIP call
             return set_error(NFX_ELAUNCH, "hipFuncSetAttribute(dynamic LDS %zu B) failed", bytes);
+        }
     }
     return NFX_OK;
 }

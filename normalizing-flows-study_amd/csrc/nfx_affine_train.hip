@@ -27,6 +27,7 @@
 
 #include "nfx_affine_kernel.h"
 #include "nfx_affine_train_kernel.h"
+#include "nfx_affine_trainw_kernel.h"
 #include "nfx_pack.h"
 
 namespace nfx {
@@ -303,7 +304,97 @@ int train_sum_finish(const float* part, int nw, int len, double* out, hipStream_
     return check_launch("affine_train_sum_finish");
 }
 
+// Wide path (nfx_affine_trainw_kernel.h): per-net compact partials part[net][w][len] -> G.
+// Element i of net n goes to a0 + n * astride + i (i < seg) or b0 + n * bstride + (i - seg).
+// 16 threads per element over workgroups w, w+16, ..., then the 16 partials in order.
+__global__ __launch_bounds__(256) void affine_trainw_finish(const float* part, int nwx, int len, int seg, int a0,
+                                                            int astride, int b0, int bstride, double* G) {
+    __shared__ double red[16][17];
+    const int e = threadIdx.x & 15, g = threadIdx.x >> 4, n = blockIdx.y;
+    const int i = blockIdx.x * 16 + e;
+    double a = 0.0;
+    if (i < len) {
+        const float* p = part + (size_t)n * nwx * len + i;
+#pragma unroll 4
+        for (int w = g; w < nwx; w += 16) a += (double)p[(size_t)w * len];
+    }
+    red[g][e] = a;
+    __syncthreads();
+    if (g == 0 && i < len) {
+        for (int k = 1; k < 16; ++k) a += red[k][e];
+        G[i < seg ? a0 + n * astride + i : b0 + n * bstride + (i - seg)] = a;
+    }
+}
+
 static int pad_d(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 8 ? 8 : 0)); }
+
+static affine_trainw_kernel_t pick_trainw(int HT, int D, int stage) {
+    switch (HT) {
+        case 3: return affine_trainw_pick_ht<3>(D, stage);
+        case 4: return affine_trainw_pick_ht<4>(D, stage);
+        default: return nullptr;
+    }
+}
+
+// Workgroups along x of a wide-path pass (deterministic, host-computable: the workspace is
+// sized with it): per-net passes <= one workgroup per CU per net, BWD3 <= two per CU.
+static int64_t trainw_gx(int64_t ntiles, int stage) {
+    const bool both = trainw_both_nets(stage);
+    const int64_t work = both ? ntiles : (ntiles + kTWGroups - 1) / kTWGroups;
+    const int64_t cap = (int64_t)num_cus() * (both ? 2 : 1);
+    const int64_t g = work < cap ? work : cap;
+    return g < 1 ? 1 : g;
+}
+
+extern "C" size_t nfx_affine_train_workspace_bytes(int64_t B, int d, int H);
+
+// Wide-path backward stage: 1 = OUT + BWD1, 2 = BWD2 (incl. the BN1-backward sums), 3 = BWD3.
+static int trainw_backward(const float* tpack, const float* x, const float* gy, const float* gld, float* gx,
+                           int64_t B, int d, int D, int HT, int direction, int stage, const double* stats2, double* G,
+                           void* workspace, hipStream_t s) {
+    const int Hp = 32 * HT;
+    const TrainGrad GL = train_grad_layout(D, HT);
+    const int64_t ntiles = (B + 31) / 32;
+    const size_t full = nfx_affine_train_workspace_bytes(B, d, 32 * HT);
+    const size_t obytes = (size_t)2 * B * D * sizeof(float);
+    const size_t gbytes = ((size_t)ntiles * 2 * HT * 1024 * sizeof(float) + 255) & ~(size_t)255;
+    char* ws = reinterpret_cast<char*>(workspace);
+    float* obuf = reinterpret_cast<float*>(ws + (full - obytes));
+    float* gbuf = reinterpret_cast<float*>(ws + (full - obytes - gbytes));
+    auto launch = [&](int st) -> int {
+        affine_trainw_kernel_t k = pick_trainw(HT, D, st);
+        if (!k) return set_error(NFX_EUNSUPPORTED, "affine_train_backward: no wide kernel for HT=%d D=%d", HT, D);
+        const size_t lds = (size_t)trainw_lds(D, HT, st).total * sizeof(float);
+        int rc = prepare_lds((const void*)k, lds);
+        if (rc) return rc;
+        const int64_t gxn = trainw_gx(ntiles, st);
+        const unsigned ny = trainw_both_nets(st) ? 1 : 2;
+        k<<<dim3((unsigned)gxn, ny), trainw_waves(HT, st) * 64, lds, s>>>(tpack, x, gy, gld, gx, gbuf, obuf, G, stats2,
+                                                                           workspace, B, d, direction, ntiles);
+        if ((rc = check_launch("affine_trainw_kernel"))) return rc;
+        if (st == TW_OUT) return NFX_OK;
+        if (st == TW_BWD3) {
+            affine_train_sum_finish<<<(GL.len3 + 15) / 16, 256, 0, s>>>(reinterpret_cast<const float*>(workspace),
+                                                                         (int)gxn, GL.len3, G + GL.g3w);
+            return check_launch("affine_train_sum_finish");
+        }
+        const int len = trainw_len(D, HT, st);
+        if (st == TW_BWD1)
+            affine_trainw_finish<<<dim3((len + 15) / 16, 2), 256, 0, s>>>(
+                reinterpret_cast<const float*>(workspace), (int)gxn, len, 2 * Hp, GL.g1s, 2 * Hp, GL.g1w, D * Hp + D, G);
+        else
+            affine_trainw_finish<<<dim3((len + 15) / 16, 2), 256, 0, s>>>(
+                reinterpret_cast<const float*>(workspace), (int)gxn, len, 2 * Hp, GL.g2s, 2 * Hp, GL.g2w, Hp * Hp + Hp,
+                G);
+        return check_launch("affine_trainw_finish");
+    };
+    int rc;
+    if (stage == 1) {
+        if ((rc = launch(TW_OUT))) return rc;
+        return launch(TW_BWD1);
+    }
+    return launch(stage == 2 ? TW_BWD2 : TW_BWD3);
+}
 
 static affine_train_kernel_t pick_train(int HT, int D, int stage) {
     switch (HT) {
@@ -315,8 +406,8 @@ static affine_train_kernel_t pick_train(int HT, int D, int stage) {
 
 static int train_check(int d, int H, const char* what) {
     if (d <= 0 || H <= 0) return set_error(NFX_EINVAL, "%s: bad shape d=%d H=%d", what, d, H);
-    if (!pad_d(d) || H > 64)
-        return set_error(NFX_EUNSUPPORTED, "%s: d=%d H=%d outside the compiled train-mode family (d<=8, H<=64)",
+    if (!pad_d(d) || H > 128)
+        return set_error(NFX_EUNSUPPORTED, "%s: d=%d H=%d outside the compiled train-mode family (d<=8, H<=128)",
                          what, d, H);
     return NFX_OK;
 }
@@ -341,7 +432,7 @@ using namespace nfx;
 
 extern "C" size_t nfx_affine_train_pack_floats(int d, int H) {
     const int D = pad_d(d);
-    if (!D || H <= 0 || H > 64) return 0;
+    if (!D || H <= 0 || H > 128) return 0;
     return (size_t)((train_layout(D, (H + 31) / 32).total + 3) & ~3);
 }
 
@@ -352,7 +443,7 @@ extern "C" size_t nfx_affine_train_stats_doubles(int H) {
 
 extern "C" size_t nfx_affine_train_grad_doubles(int d, int H) {
     const int D = pad_d(d);
-    if (!D || H <= 0 || H > 64) return 0;
+    if (!D || H <= 0 || H > 128) return 0;
     return (size_t)train_grad_layout(D, (H + 31) / 32).total;
 }
 
@@ -361,13 +452,28 @@ extern "C" size_t nfx_affine_train_param_floats(int d, int H) {
     return (size_t)2 * (H * d + H + 2 * H + H * H + H + 2 * H + d * H + d);
 }
 
-// Workspace: per-wave partials (max over passes) + the g_y1 tiles BWD2 hands to BWD3.
+// Workspace: per-wave partials (max over passes) + the g_y1 tiles BWD2 hands to BWD3
+// (+ on the wide path, HT > 2, the raw net outputs [2][B][D] of the OUT pass).
 extern "C" size_t nfx_affine_train_workspace_bytes(int64_t B, int d, int H) {
     const int D = pad_d(d);
-    if (!D || H <= 0 || H > 64 || B < 0) return 0;
+    if (!D || H <= 0 || H > 128 || B < 0) return 0;
     const int HT = (H + 31) / 32, Hp = 32 * HT;
     const TrainGrad GL = train_grad_layout(D, HT);
     const int64_t ntiles = (B + 31) / 32;
+    if (HT > 2) {
+        size_t partials = 0;
+        for (int st = TW_STATS1; st <= TW_BWD3; ++st) {
+            const int64_t gx = trainw_gx(ntiles, st);
+            size_t bytes;
+            if (st == TW_STATS1 || st == TW_STATS2) bytes = (size_t)2 * gx * 2 * Hp * 3 * sizeof(double);
+            else if (st == TW_BWD3) bytes = (size_t)gx * GL.len3 * sizeof(float);
+            else bytes = (size_t)2 * gx * trainw_len(D, HT, st) * sizeof(float);
+            if (bytes > partials) partials = bytes;
+        }
+        partials = (partials + 255) & ~(size_t)255;
+        const size_t gbytes = ((size_t)ntiles * 2 * HT * 1024 * sizeof(float) + 255) & ~(size_t)255;
+        return partials + gbytes + (size_t)2 * B * D * sizeof(float);
+    }
     int64_t nw = 4 * (int64_t)num_cus() * 2;  // upper bound on resident waves (<= 2 WGs/CU)
     const int64_t cap = 4 * ((ntiles + 3) / 4);
     if (nw > cap) nw = cap < 4 ? 4 : cap;
@@ -408,6 +514,21 @@ extern "C" int nfx_affine_train_stats(const float* tpack, const float* x, int64_
     if (B < 1) return set_error(NFX_EINVAL, "affine_train_stats: batch statistics need B >= 1 (B=%lld)", (long long)B);
     if (!tpack || !x || !stats || !workspace) return set_error(NFX_EINVAL, "affine_train_stats: null pointer");
     const int D = pad_d(d), HT = (H + 31) / 32, Hp = 32 * HT;
+    if (HT > 2) {  // wide path: one net per workgroup (blockIdx.y)
+        const int st = layer == 1 ? TW_STATS1 : TW_STATS2;
+        affine_trainw_kernel_t kw = pick_trainw(HT, D, st);
+        const size_t lds = (size_t)trainw_lds(D, HT, st).total * sizeof(float);
+        if ((rc = prepare_lds((const void*)kw, lds))) return rc;
+        const int64_t ntiles = (B + 31) / 32, gx = trainw_gx(ntiles, st);
+        hipStream_t s = (hipStream_t)stream;
+        kw<<<dim3((unsigned)gx, 2), trainw_waves(HT, st) * 64, lds, s>>>(tpack, x, nullptr, nullptr, nullptr, nullptr,
+                                                                          nullptr, nullptr, nullptr, workspace, B, d, 1,
+                                                                          ntiles);
+        if ((rc = check_launch("affine_trainw_kernel(stats)"))) return rc;
+        affine_train_stats_finish<<<(2 * Hp + 15) / 16, 256, 0, s>>>(reinterpret_cast<const double*>(workspace),
+                                                                     (int)(2 * gx), Hp, stats);
+        return check_launch("affine_train_stats_finish");
+    }
     affine_train_kernel_t k = pick_train(HT, D, layer == 1 ? TS_STATS1 : TS_STATS2);
     const size_t lds = affine_train_lds(D, HT);
     if ((rc = prepare_lds((const void*)k, lds))) return rc;
@@ -463,6 +584,8 @@ extern "C" int nfx_affine_train_backward(const float* tpack, const float* x, con
         return set_error(NFX_EINVAL, "affine_train_backward: null pointer");
     const int D = pad_d(d), HT = (H + 31) / 32;
     const TrainGrad GL = train_grad_layout(D, HT);
+    if (HT > 2) return trainw_backward(tpack, x, gy, gld, gx, B, d, D, HT, direction, stage, stats2, G, workspace,
+                                       (hipStream_t)stream);
     const int ts = stage == 1 ? TS_BWD1 : (stage == 2 ? TS_BWD2 : TS_BWD3);
     affine_train_kernel_t k = pick_train(HT, D, ts);
     const size_t lds = affine_train_lds(D, HT);

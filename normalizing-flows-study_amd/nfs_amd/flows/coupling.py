@@ -30,7 +30,7 @@ from .flow import HipFlow, STATS
 MAX_D = 64          # eval kernels: affine_coupling_kernel (d <= 8) / affine_wide_kernel (d <= 64)
 MAX_D_TRAIN = 8     # train-mode / backward kernels
 MAX_H = 128
-MAX_H_TRAIN = 64
+MAX_H_TRAIN = 128  # HT <= 2: affine_train_kernel; HT 3, 4: affine_trainw_kernel (wide)
 ctypes_vp = ctypes.c_void_p
 
 # (kernel-name, start-event, end-event) of every train-mode layer pass while a list is installed

@@ -97,7 +97,21 @@ class Ensemble:
         self.n_guard = n_guard
 
 
-def fp32_jitter(fn, *inputs, k=8, seed=0, sd=None, n_perm=8):
+def jitter_weights(sd, gen):
+    """Every floating-point parameter/buffer nudged by -1/0/+1 ulp (masks kept): the rounding a
+    weight image picks up when it is re-laid out, BatchNorm-folded or summed in another order,
+    and the last-bit freedom of the transcendental results derived from it."""
+    out = {}
+    for k, v in sd.items():
+        if torch.is_tensor(v) and v.is_floating_point() and not k.endswith("mask"):
+            step = torch.randint(-1, 2, v.shape, generator=gen).to(v.dtype) * v.abs() * 2.0 ** -23
+            out[k] = torch.where(torch.isfinite(v), v + step, v)
+        else:
+            out[k] = v.clone() if torch.is_tensor(v) else v
+    return out
+
+
+def fp32_jitter(fn, *inputs, k=8, seed=0, sd=None, n_perm=8, n_wjit=8):
     """Ensemble of equally valid fp32 evaluations of an fp32 oracle closure (returns one
     `Ensemble` per output of `fn`):
       * k evaluations with every input element jittered by -1/0/+1 ulp — a one-ulp nudge
@@ -105,7 +119,8 @@ def fp32_jitter(fn, *inputs, k=8, seed=0, sd=None, n_perm=8):
         cumsum, the root);
       * with `sd` given (then `fn(sd, *inputs)`), n_perm evaluations of the same network with
         its hidden units permuted (`permute_hidden`) — a different summation order in every
-        matmul, the freedom the GPU's MFMA order uses.
+        matmul, the freedom the GPU's MFMA order uses — and n_wjit evaluations with every weight
+        nudged by -1/0/+1 ulp (`jitter_weights`).
     A member that is NaN where the base evaluation is finite (a jitter crossing a guard) is
     dropped for that element and counted; it never widens any bound."""
     g = torch.Generator().manual_seed(seed)
@@ -123,6 +138,9 @@ def fp32_jitter(fn, *inputs, k=8, seed=0, sd=None, n_perm=8):
         if sd is not None:
             for _ in range(n_perm):
                 for i, o in enumerate(call(permute_hidden(sd, g), *inputs)):
+                    mem[i].append(o.double())
+            for _ in range(n_wjit):
+                for i, o in enumerate(call(jitter_weights(sd, g), *inputs)):
                     mem[i].append(o.double())
     out = []
     for i, b in enumerate(base):
@@ -145,9 +163,11 @@ def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=None, what="", kind=
     Every element must be
       (a) within the fixed tolerance of the reference's own fp32 result (cpu32) or of one of the
           equally valid fp32 evaluations in `sens` (conftest.fp32_jitter: one-ulp input jitter,
-          hidden-unit order), or
-      (b) inside the hull of those evaluations and the float64 evaluation ref64, widened by the
-          fixed tolerance — "relaxed"; at most `max_ill` (2 %, at least 3) of the elements.
+          hidden-unit order, one-ulp weight jitter), or
+      (b) inside the hull [lo, hi] of those evaluations and the float64 evaluation ref64,
+          extended by the fixed tolerance plus the hull's own width (a finite sample of valid
+          evaluations underestimates their spread): [lo - tol - w, hi + tol + w], w = hi - lo —
+          "relaxed"; at most `max_ill` (2 %, at least 3) of the elements.
     No unbounded widening exists: an evaluation that crossed a guard (NaN) is dropped, never
     turned into an infinite sensitivity. Every accepted element whose error exceeds 1e-2 is
     printed with its justification: valid fp32 evaluations that differ by at least that much
@@ -176,13 +196,16 @@ def assert_fp32_parity(gpu, cpu32, ref64, slack=1e-5, floor=None, what="", kind=
             near |= np.any(np.abs(M - g[None, :]) <= tol[None, :], axis=0)
             lo = np.fmin(lo, np.nanmin(np.where(np.isnan(M), np.inf, M), axis=0))
             hi = np.fmax(hi, np.nanmax(np.where(np.isnan(M), -np.inf, M), axis=0))
-    hull = (g >= lo - tol) & (g <= hi + tol)
+    # a hull of M samples underestimates the spread of the distribution it samples: extend it by
+    # its own width w (a fixed-size guard, not a multiple of an unbounded sensitivity)
+    w = hi - lo
+    hull = (g >= lo - tol - w) & (g <= hi + tol + w)
     bad = ~near & ~hull
     if bad.any():
         j = int(np.argmax(np.where(bad, err, -1)))
         raise AssertionError(f"{what}: {int(bad.sum())} elements outside the fixed tolerance of every valid fp32 "
                              f"evaluation and outside their hull; worst element {int(idx[j])}: gpu {g[j]!r} "
-                             f"reference {c[j]!r} float64 {r[j]!r} hull [{lo[j]!r}, {hi[j]!r}]")
+                             f"reference {c[j]!r} float64 {r[j]!r} hull [{lo[j]!r}, {hi[j]!r}] (+- tol + width)")
     relaxed = ~near
     n_rel = int(relaxed.sum())
     if not os.environ.get("NFX_MEASURE_ILL"):

@@ -46,6 +46,15 @@ def _close(a, b, rel=2e-5, what=""):
     assert err <= rel, f"{what}: max rel err {err:.3e} > {rel:.1e}"
 
 
+def _close_or_ref(a, b64, b32, rel=2e-5, what=""):
+    """Outputs: max |a - b64| / (1 + |b64|) <= max(rel, 4x the reference's own fp32 error) — at
+    H = 128 the batch-statistics chain is a little worse conditioned than the fixed 2e-5."""
+    a, b64, b32 = (t.detach().double().cpu() for t in (a, b64, b32))
+    err = ((a - b64).abs() / (1 + b64.abs())).max().item() if a.numel() else 0.0
+    err32 = ((b32 - b64).abs() / (1 + b64.abs())).max().item() if a.numel() else 0.0
+    assert err <= max(rel, 4 * err32), f"{what}: max rel err {err:.3e} > max({rel:.1e}, 4 x fp32 ref {err32:.3e})"
+
+
 PRE_BN_BIAS = ("net.0.bias", "net.3.bias")
 
 
@@ -179,6 +188,9 @@ def _perturbed_layer(d, H, seed, mask_even=True):
 @pytest.mark.parametrize("d,H,B,direction", [
     (2, 64, 2, -1), (2, 64, 31, -1), (2, 64, 1000, 1), (2, 64, 65537, -1),
     (1, 32, 500, -1), (3, 16, 777, 1), (5, 48, 4097, -1), (8, 64, 3000, 1), (2, 20, 129, -1),
+    # wide hidden layers (affine_trainw_kernel: one net per workgroup, wave per hidden tile)
+    (2, 128, 2000, -1), (2, 128, 3, 1), (4, 96, 777, 1), (8, 128, 3000, -1), (2, 128, 65537, 1),
+    (3, 100, 513, -1), (6, 72, 1000, 1),
 ])
 def test_layer_vs_float64_autograd(cuda_device, d, H, B, direction):
     layer = _perturbed_layer(d, H, 100 + d * 7 + H, mask_even=(B % 2 == 0))
@@ -199,8 +211,8 @@ def test_layer_vs_float64_autograd(cuda_device, d, H, B, direction):
     yg, ldg = gpu.forward(xg) if direction > 0 else gpu.inverse(xg)
     ((yg * wy.to(cuda_device)).sum() + (ldg * wl.to(cuda_device)).sum()).backward()
     assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 2, nfs_amd.STATS
-    _close(yg, yr, what="y")
-    _close(ldg, ldr, what="log_det")
+    _close_or_ref(yg, yr, y32, what="y")
+    _close_or_ref(ldg, ldr, ld32, what="log_det")
     _gclose(xg.grad, xr.grad, what="dL/dx")
     gmax = max(p.grad.abs().max().item() for p in ref.parameters())
     for (k, pg), (_, pr), (_, p32) in zip(gpu.named_parameters(), ref.named_parameters(), ref32.named_parameters()):
@@ -254,6 +266,7 @@ def test_eval_after_train_uses_running_stats(cuda_device):
 @pytest.mark.parametrize("d,H,B,direction", [
     (2, 64, 1, -1), (2, 64, 1000, 1), (2, 64, 65537, -1), (1, 32, 500, -1), (3, 16, 777, 1),
     (5, 48, 4097, -1), (8, 64, 3000, 1), (2, 20, 129, -1),
+    (2, 128, 1, -1), (2, 128, 2000, 1), (8, 128, 3000, -1), (5, 96, 4097, 1), (2, 128, 65537, -1),
 ])
 def test_eval_mode_backward_vs_float64_autograd(cuda_device, d, H, B, direction):
     """Eval-mode CouplingLayer under autograd (running-statistics BatchNorm, coupling_layer.py:
@@ -306,3 +319,113 @@ def test_eval_mode_realnvp_step_matches_float64(cuda_device):
     assert abs(loss.item() - lr.item()) <= 1e-5
     for (k, pg), (_, pr) in zip(gpu.named_parameters(), ref.named_parameters()):
         _gclose(pg.grad, pr.grad, frac=5e-4, what=k + " (eval step)")
+
+
+def _fig_loss(z, ld):
+    return -(-0.5 * (z.pow(2).sum(1) + 2 * np.log(2 * np.pi)) + ld).mean()
+
+
+def test_figure_model_train_step_vs_reference(cuda_device):
+    """The reference's benchmark-figure model, RealNVP(2, 10, 128) (plots/_common.py:161), in its
+    training step (plots/_common.py:194-211: train-mode BatchNorm, full batch of 2,000 two-moons
+    points) against the reference's own outputs, loss, gradients and running statistics (G15),
+    and against float64 autograd: every layer runs the wide train-mode kernels (H = 128), no ATen."""
+    g = load_golden("g15_fig_train.npz")
+    m = _load(nfs_amd.RealNVP(2, 10, 128), g, "fig.init.")
+    ref64 = copy.deepcopy(m).double().train()
+    gpu = m.to(cuda_device).train()
+    x = torch.from_numpy(g["fig.x"])
+    nfs_amd.reset_stats()
+    z, ld = gpu.inverse(x.to(cuda_device))
+    loss = _fig_loss(z, ld)
+    loss.backward()
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 20, nfs_amd.STATS
+    z64, ld64 = ref64.inverse(x.double())
+    l64 = _fig_loss(z64, ld64)
+    l64.backward()
+    assert_fp32_parity(z.detach().cpu(), g["fig.z"], z64.detach(), slack=2e-5, what="fig z")
+    assert_fp32_parity(ld.detach().cpu(), g["fig.ld"], ld64.detach(), slack=2e-5, what="fig log_det")
+    assert abs(loss.item() - float(g["fig.loss"])) <= 1e-5 and abs(loss.item() - l64.item()) <= 2e-5
+    gmax = max(float(np.abs(g["fig.grad." + k]).max()) for k, _ in gpu.named_parameters())
+    for (k, p), (_, p64) in zip(gpu.named_parameters(), ref64.named_parameters()):
+        # vs the reference's fp32 gradients, with the reference's own distance from float64 as
+        # the yardstick (through 10 train-mode layers a few BatchNorm sums are 4e-4 off exact)
+        _gclose(p.grad, g["fig.grad." + k], what=k, gmax=gmax, ref32=p64.grad)
+        _gclose(p.grad, p64.grad, what=k + " (float64)", gmax=gmax, ref32=g["fig.grad." + k])
+    for k, v in gpu.state_dict().items():
+        if k.endswith(("running_mean", "running_var")):
+            _close(v, g["fig.after." + k], rel=1e-6, what=k)
+
+
+def _fig_train(m, x, steps, dtype=None):
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(steps):
+        z, ld = m.inverse(x)
+        loss = _fig_loss(z, ld)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 5.0)
+        opt.step()
+        losses.append(loss.item())
+    return opt, losses
+
+
+def test_figure_model_five_adam_steps_vs_reference(cuda_device):
+    """Five full steps of the reference's figure training loop (Adam lr 1e-3, clip_grad_norm_ 5.0,
+    plots/_common.py:194-211) on the HIP path. The trajectory is ill-conditioned in fp32: Adam
+    normalises every update element-wise, so rounding noise in near-zero gradient entries becomes
+    +-lr parameter steps, and the reference's own fp32 loss at step 3 is 3.8e-3 off its float64
+    trajectory (one ulp of weight jitter moves it as much). Each loss must be within 5e-5 of the
+    reference's (G15) or 1e-4 of the float64 trajectory, and the final parameters within 2e-4
+    (relative) of the trajectory the losses followed."""
+    g = load_golden("g15_fig_train.npz")
+    x = torch.from_numpy(g["fig.x"])
+    m64 = _load(nfs_amd.RealNVP(2, 10, 128), g, "fig.init.").double().train()
+    _, l64 = _fig_train(m64, x.double(), 5)
+    ref = g["fig.losses5"]
+    m = _load(nfs_amd.RealNVP(2, 10, 128), g, "fig.init.").to(cuda_device).train()
+    nfs_amd.reset_stats()
+    _, losses = _fig_train(m, x.to(cuda_device), 5)
+    assert nfs_amd.STATS["torch"] == 0, nfs_amd.STATS
+    losses = np.asarray(losses)
+    ok = (np.abs(losses - ref) <= 5e-5) | (np.abs(losses - np.asarray(l64)) <= 1e-4)
+    assert ok.all(), (losses.tolist(), ref.tolist(), l64)
+    final = {k: torch.from_numpy(g["fig.step5." + k]) for k in m.state_dict() if "fig.step5." + k in g} \
+        if np.abs(losses - ref).max() <= 5e-5 else m64.state_dict()
+    for k, v in m.state_dict().items():
+        # as test_realnvp_adam_steps_vs_reference: biases feeding a BatchNorm (zero gradient up to
+        # rounding noise, which Adam turns into +-lr steps) and the running means that track
+        # them are not compared
+        if k.endswith(("num_batches_tracked", "net.0.bias", "net.3.bias", "running_mean")):
+            continue
+        _close(v, final[k], rel=2e-4, what=k)
+
+
+def test_figure_model_graphed_step_equals_eager(cuda_device):
+    """The figure model's training step captured as one hipGraph (nfs_amd.GraphedTrainStep: 10
+    wide train-mode layers forward + fused backward, clip_grad_norm_, capturable Adam) replays
+    the eager step bit for bit (every reduction has a fixed order)."""
+    g = load_golden("g15_fig_train.npz")
+    x = torch.from_numpy(g["fig.x"]).to(cuda_device)
+    a = _load(nfs_amd.RealNVP(2, 10, 128), g, "fig.init.").to(cuda_device).train()
+    b = copy.deepcopy(a)
+    opt_a = torch.optim.Adam(a.parameters(), lr=1e-3, capturable=True)
+    opt_b = torch.optim.Adam(b.parameters(), lr=1e-3, capturable=True)
+    la = []
+    for _ in range(5):
+        z, ld = a.inverse(x)
+        loss = _fig_loss(z, ld)
+        opt_a.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(list(a.parameters()), 5.0)
+        opt_a.step()
+        la.append(loss.item())
+    nfs_amd.reset_stats()
+    step = nfs_amd.GraphedTrainStep(b, x, opt_b, warmup=1, clip_grad_norm=5.0,
+                                    loss_fn=lambda mod, xx: _fig_loss(*mod.inverse(xx)))
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] > 0, nfs_amd.STATS
+    lb = [step().item() for _ in range(4)]
+    assert la[1:] == lb, (la, lb)
+    for (k, pa), (_, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(pa, pb), k
