@@ -129,6 +129,17 @@ def build(config):
         return m, d, f, spec, \
             f"{config} 6x{kind.upper()}(2,64) sampling ({what}): model.forward(z), n=4000 per call " \
             f"(plots/_common.py:165-167,264-274)"
+    if config == "trainfig":
+        # the reference's benchmark-figure model in its training loop (plots/_common.py:161,
+        # 178-183, 194-211): RealNVP(2, 10, 128), full batch of 2,000 two-moons points, train-mode
+        # BatchNorm, Adam lr 1e-3, clip_grad_norm_ 5.0; weights + data from the G15 fixture
+        m = nfs_amd.RealNVP(2, 10, 128)
+        H = 128
+        f = 2 * (3 * 2 * H * H + 2 * H + 2 * 2 * H)  # BWD2 per net, as cfg2t
+        import oracle
+        return m, 2, f, oracle.realnvp_spec(10, training=True), \
+            ("trainfig RealNVP(2,10,128) training step, full batch of 2,000 two-moons points "
+             "(plots/_common.py:161,194-211: train-mode BatchNorm, Adam lr 1e-3, clip_grad_norm_ 5.0)")
     if config in ("cfg2t", "train5k"):
         torch.manual_seed(0)
         m = nfs_amd.RealNVP(2, 8, 64)
@@ -172,9 +183,11 @@ def build(config):
         return m, d, f, spec, "cfg5i IAF(784, 64) log_prob (sequential inverse), eval"
     raise ValueError(config)
 
+TRAIN_CONFIGS = ("cfg4t", "cfg2t", "train5k", "cfg3t", "trainfig")
+
 # Batch of each config: the BASELINE global batch (strong scaling splits it over the ranks,
 # --weak gives every rank all of it).
-DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
+DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "trainfig": 2_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
                  "cfg4": 4_000_000, "cfg4t": 500_000, "cfg5f": 524_288, "cfg5i": 8_192,
                  "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000, "sample4k_iaf": 4_000}
 # The reference's only published throughput (assets/benchmark.png via
@@ -208,6 +221,15 @@ def load_reference_weights(model, config):
         gk = spec["prefix"] + (k[len(spec["sub"]):] if spec["sub"] and k.startswith(spec["sub"]) else k)
         sd[k] = torch.from_numpy(np.array(arrs[gk])) if gk in arrs else v
     model.load_state_dict(sd)
+
+
+def figure_batch():
+    """G15: the figure model's initial weights and its 2,000 standardized two-moons points
+    (plots/_common.py:103-112), as the reference generated them."""
+    import numpy as np
+    with np.load(os.path.join(GOLDEN, "g15_fig_train.npz"), allow_pickle=False) as z:
+        arrs = {k: z[k] for k in z.files}
+    return arrs
 
 
 def g8_meta(config):
@@ -344,12 +366,19 @@ CPU_ROWS = {"cfg2": 1_000_000, "cfg3": 1_000_000, "cfg4": 1_000_000, "cfg5f": 16
 def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     """One benchmark line (dict on rank 0, None elsewhere)."""
     model, d, f_layer, spec, desc = build(config)
-    training = config in ("cfg4t", "cfg2t", "train5k", "cfg3t")
-    coupling_train = config in ("cfg2t", "train5k")
+    training = config in TRAIN_CONFIGS
+    coupling_train = config in ("cfg2t", "train5k", "trainfig")
+    clip = 5.0 if config == "trainfig" else None
+    lr = 1e-3 if config == "trainfig" else 1e-5
     sampling = config == "cfg5f" or config.startswith("sample4k")
     pinned = config in REFERENCE_RUN
     if pinned:
         load_reference_weights(model, config)
+    fig = None
+    if config == "trainfig":
+        fig = figure_batch()
+        model.load_state_dict({k: (torch.from_numpy(fig["fig.init." + k].copy()) if "fig.init." + k in fig else v)
+                               for k, v in model.state_dict().items()})
     if coupling_train and world > 1:
         from nfs_amd.distributed import enable_sync_batchnorm
         enable_sync_batchnorm(True)  # batch statistics over all ranks = the full-batch step
@@ -364,7 +393,9 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         lo, hi = 0, B_unit
         B, B_global = B_unit, B_unit * world
     x_ref = None
-    if pinned and B_unit == g8_meta(config)["B"]:
+    if fig is not None:
+        x = torch.from_numpy(fig["fig.x"][lo:hi].copy()).to(dev)
+    elif pinned and B_unit == g8_meta(config)["B"]:
         meta = g8_meta(config)
         x_ref = torch.randn(meta["B"], meta["d"], generator=torch.Generator().manual_seed(meta["seed"]))
         x = x_ref[lo:hi].to(dev)
@@ -376,12 +407,12 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     graphed = None
     if graph and not training:
         graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-5, capturable=graph) if training else None
+    opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=graph) if training else None
     graphed_train = None
     if graph and training:
         if world > 1:
             raise SystemExit("--graph training is single-GPU (the SyncBN / gradient collectives run eagerly)")
-        graphed_train = nfs_amd.GraphedTrainStep(flow, x, opt, warmup=a.warmup)
+        graphed_train = nfs_amd.GraphedTrainStep(flow, x, opt, warmup=a.warmup, clip_grad_norm=clip)
 
     eager_only = [False]  # the per-kernel event pass runs eager steps (a graph replay records no events)
 
@@ -397,6 +428,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
             loss = -logp.mean()
             loss.backward()
             average_gradients(model, local_count=B)
+            if clip is not None:
+                torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
             opt.step()
             return torch.stack([-loss.detach().double() * B, torch.tensor(float(B), device=dev, dtype=torch.float64)])
         if graphed is not None:
@@ -473,7 +506,10 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     durs = [e0.elapsed_time(e1) for _, e0, e1 in events]
     kname = events[0][0] if events else "?"
     mean_ms = sum(durs) / max(1, len(durs))
-    achieved = f_layer * B / (mean_ms * 1e-3) / 1e12
+    # one-launch coupling chain (nfx_affine_chain): one event covers every layer
+    layers_per_launch = len(flow.flows) if kname == "affine_chain_kernel" else 1
+    f_launch = f_layer * layers_per_launch
+    achieved = f_launch * B / (mean_ms * 1e-3) / 1e12
 
     # result vs the reference's own full-scale run (global over ranks)
     ref_check = None
@@ -536,7 +572,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         "roofline": {"bound": "mfma", "pipe": "valu" if config == "cfg5i" else "mfma",
                      "kernel": kname, "achieved": achieved,
                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
-                     "traffic": traffic, "flop_per_sample_per_launch": f_layer,
+                     "traffic": traffic, "flop_per_sample_per_launch": f_launch,
+                     "layers_per_launch": layers_per_launch,
                      "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs),
                      "traffic_source": os.path.relpath(tp, ROOT) if traffic is not None else None},
         "cpu_baseline": None,
@@ -559,6 +596,10 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         result["nll_f64"] = None
     if coupling_train:
         result["metric"] = "training samples/sec/GPU (RealNVP d=2 train-mode step)"
+        if fig is not None:
+            result["metric"] = "training samples/sec/GPU (RealNVP(2,10,128) figure-model train-mode step)"
+            result["data"] = ("the reference's own initial weights and 2,000 standardized two-moons points "
+                              "(tests/golden/g15_fig_train.npz, written by importing the reference)")
         result["nll_f64"] = None
         result["roofline"]["note"] = ("dominant kernel = BWD2 of the train-mode coupling backward "
                                       "(layer-2 recompute, W2^T e2 and the sample-contraction dW2 on "
@@ -613,7 +654,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg2t", "train5k", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i", "sample4k",
+                    choices=["cfg2", "cfg2t", "train5k", "trainfig", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i",
+                             "sample4k",
                              "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
     ap.add_argument("--batch", type=int, default=None,
                     help="global batch (default: the BASELINE batch, 1M; 4M cfg4; 512Ki cfg5f; 8Ki cfg5i)")
@@ -643,7 +685,7 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
-    training = a.config in ("cfg4t", "cfg2t", "train5k", "cfg3t")
+    training = a.config in TRAIN_CONFIGS
     graph = a.graph if training else not a.eager
     strong = not a.weak
     result = run_config(a.config, a, world, rank, dev, strong, graph, not a.no_cpu)

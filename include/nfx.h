@@ -103,6 +103,24 @@ int nfx_affine_coupling_logprob(const float* packed, const float* in, float* out
 #define NFX_AFFINE_SMALL 2
 int nfx_affine_kernel_policy(int policy);
 
+/* A whole chain of affine coupling layers in ONE launch (eval mode; NormalizingFlowModel /
+ * RealNVP / SequentialFlow of CouplingLayers without between-layer BatchNorm): packs[l] is
+ * layer l's image from nfx_affine_pack (all layers the same d in {2, 4, 8} and H <= 128),
+ * n_layers <= 64. direction +1 runs layers 0 .. n-1 (forward), -1 runs n-1 .. 0 (inverse).
+ * The per-layer arithmetic is nfx_affine_coupling's small-batch kernel (bit-identical to the
+ * per-layer calls with policy NFX_AFFINE_SMALL); rows and the running log-det stay in LDS
+ * between layers. log_det: written (accumulate = 0) or added to, as a chain of per-layer calls
+ * would. `packs` is a HOST array of device pointers. The _logprob variant (inverse only) also
+ * writes logp and the float64 [sum, count] partials like nfx_affine_coupling_logprob
+ * (workspace: nfx_gauss_workspace_bytes(B)). Returns NFX_EUNSUPPORTED for batches whose rows
+ * do not fit a workgroup's LDS (B > 4096 * 170 * 32 at d = 2). */
+int nfx_affine_chain(const float* const* packs, int n_layers, const float* in, float* out,
+                     float* log_det, int64_t B, int d, int H, int direction, int accumulate,
+                     void* stream);
+int nfx_affine_chain_logprob(const float* const* packs, int n_layers, const float* in, float* out,
+                             float* log_det, float* logp, double* sums, void* workspace, int64_t B,
+                             int d, int H, int accumulate, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Rational-quadratic spline coupling — SplineCouplingLayer
  * (src/flows/spline/spline_coupling_layer.py:6-323): forward :96-137, inverse :139-180,
@@ -168,6 +186,18 @@ int nfx_made_affine(const float* packed, const float* in, float* out, float* log
 /* Density direction + fused log_prob epilogue (see nfx_affine_coupling_logprob):
  * NFX_MAF_INVERSE with d <= 64 or H <= 64 (and H <= 128), NFX_IAF_INVERSE (sequential) with H <= 64;
  * NFX_EUNSUPPORTED otherwise (use nfx_gauss_logprob after nfx_made_affine). */
+/* Which kernel runs the SEQUENTIAL MADE directions (NFX_MAF_FORWARD, NFX_IAF_INVERSE) at
+ * H <= 64: the segment-parallel one (16 lanes per sample, 4 samples per wave) or the
+ * wave-per-sample one (64 lanes per sample: a ~4x shorter dependent chain per sample, for
+ * small batches / strong scaling). Same function (mu/alpha dot products associated
+ * differently, within fp32 rounding). NFX_MADE_SEQ_AUTO (default, or $NFX_MADE_SEQ_POLICY)
+ * takes the wave-per-sample kernel up to 8 samples per CU (2,048 on 256 CUs), the segment kernel
+ * above. policy >= 0 sets it and returns the previous one; negative reads.
+ * Process-wide; host-only. */
+#define NFX_MADE_SEQ_AUTO 0
+#define NFX_MADE_SEQ_SEGMENT 1
+#define NFX_MADE_SEQ_WAVE 2
+int nfx_made_seq_policy(int policy);
 int nfx_made_affine_logprob(const float* packed, const float* in, float* out, float* log_det,
                             float* logp, double* sums, void* workspace, int64_t B, int d, int H,
                             int variant, int accumulate, void* stream);

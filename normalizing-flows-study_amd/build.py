@@ -17,8 +17,11 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "build")
-OUT = os.path.join(HERE, "nfs_amd", "libnfx.so")
+# NFX_BUILD_VARIANT=<name> (with NFX_EXTRA_CFLAGS, e.g. -DNFX_SEQW_TIMING) builds a diagnostic
+# variant into build-<name>/ and nfs_amd/libnfx_<name>.so (load it with NFX_LIB=...).
+_VARIANT = os.environ.get("NFX_BUILD_VARIANT", "")
+BUILD = os.path.join(HERE, "build" + (f"-{_VARIANT}" if _VARIANT else ""))
+OUT = os.path.join(HERE, "nfs_amd", f"libnfx_{_VARIANT}.so" if _VARIANT else "libnfx.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 ARCH = os.environ.get("NFX_OFFLOAD_ARCH", "gfx950")
 
@@ -58,7 +61,7 @@ def build(jobs=None, force=False, verbose=True):
 
     def compile_one(so):
         s, o = so
-        cmd = [cc] + CFLAGS + ["-c", s, "-o", o]
+        cmd = [cc] + CFLAGS + os.environ.get("NFX_EXTRA_CFLAGS", "").split() + ["-c", s, "-o", o]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {os.path.basename(s)}:\n{r.stderr[-4000:]}")

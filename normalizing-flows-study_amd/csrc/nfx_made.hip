@@ -2,6 +2,9 @@
 // Kernels: nfx_made_kernel.h (parallel instantiations in nfx_made_par.hip).
 #include "nfx_made_kernel.h"
 #include "nfx_made_wide_kernel.h"
+#include <atomic>
+#include <cstdlib>
+
 #include "nfx_made_seqs_kernel.h"
 #include "nfx_pack.h"
 
@@ -226,6 +229,23 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     return check_launch("made_seqs_image_kernel");
 }
 
+namespace nfx {
+int made_seqw_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d, int H,
+                     int variant, int accumulate, float* logp, double* partials, bool fused, int* grid_out,
+                     hipStream_t s);
+}  // namespace nfx
+
+// Sequential-direction kernel choice (nfx_made_seq_policy): NFX_MADE_SEQ_AUTO (default, or
+// $NFX_MADE_SEQ_POLICY), NFX_MADE_SEQ_SEGMENT (made_seqs_kernel: 16 lanes per sample) or
+// NFX_MADE_SEQ_WAVE (made_seqw_kernel: a wave per sample).
+static std::atomic<int>& made_seq_policy() {
+    static std::atomic<int> v{[] {
+        const char* e = getenv("NFX_MADE_SEQ_POLICY");
+        return e ? atoi(e) : NFX_MADE_SEQ_AUTO;
+    }()};
+    return v;
+}
+
 static int made_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
                        int d, int H, int variant, int accumulate, float* logp, double* sums,
                        void* workspace, hipStream_t s) {
@@ -303,6 +323,17 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, nullptr, nullptr, 0.f);
         return check_launch("made_parallel_kernel");
     }
+    // AUTO: the wave-per-sample kernel while the batch leaves the segment kernel's 4-sample waves
+    // short of 2 per SIMD (measured, IAF(784, 64): 74.8 vs 107.9 us at 1,024; 116 vs 138 us at
+    // 4,096 for the segment kernel, profiles/r03i_seqw_sweep.jsonl)
+    const int seq_pol = made_seq_policy().load(std::memory_order_relaxed);
+    if (seqs && (seq_pol == NFX_MADE_SEQ_WAVE || (seq_pol == NFX_MADE_SEQ_AUTO && B <= 2048 * (int64_t)num_cus() / 256))) {
+        int grid = 0;
+        int rc = made_seqw_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, partials, fused, &grid,
+                                  s);
+        if (rc || !fused) return rc;
+        return gauss_finish(partials, grid, sums, B, s);
+    }
     if (seqs) {
         made_seqs_kernel_t k = HT == 1 ? made_seqs_pick_ht<1>(variant, fused) : made_seqs_pick_ht<2>(variant, fused);
         const size_t lds = (size_t)seqs_lds(L.Hp).total * sizeof(float);
@@ -323,6 +354,12 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     const int64_t grid = (B + 63) / 64;
     k<<<(unsigned)grid, 64, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate);
     return check_launch("made_seq_kernel");
+}
+
+extern "C" int nfx_made_seq_policy(int policy) {
+    if (policy < 0) return made_seq_policy().load();
+    if (policy > NFX_MADE_SEQ_WAVE) return set_error(NFX_EINVAL, "made_seq_policy: unknown policy %d", policy);
+    return made_seq_policy().exchange(policy);
 }
 
 extern "C" int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,

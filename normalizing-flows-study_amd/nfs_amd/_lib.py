@@ -25,16 +25,19 @@ NFX_IAF_INVERSE = 3
 NFX_AFFINE_AUTO = 0
 NFX_AFFINE_STREAMING = 1
 NFX_AFFINE_SMALL = 2
+NFX_MADE_SEQ_AUTO = 0
+NFX_MADE_SEQ_SEGMENT = 1
+NFX_MADE_SEQ_WAVE = 2
 
 # Every symbol include/nfx.h declares (tests check the built library exports all of them).
 EXPORTED_SYMBOLS = (
     "nfx_abi_version", "nfx_last_error", "nfx_debug_fill_lds",
     "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
-    "nfx_affine_kernel_policy",
+    "nfx_affine_kernel_policy", "nfx_affine_chain", "nfx_affine_chain_logprob",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
     "nfx_rqs_unit",
     "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
-    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob",
+    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob", "nfx_made_seq_policy",
     "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_backward_max_batch",
     "nfx_made_affine_backward",
     "nfx_made_seq_backward", "nfx_made_factor_pitch", "nfx_made_param_floats", "nfx_made_wgrad_workspace_bytes", "nfx_made_backward_weights",
@@ -88,6 +91,9 @@ _SIGNATURES = {
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_affine_kernel_policy": (_int, [_int]),
+    "nfx_affine_chain": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
+    "nfx_affine_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,
+                                        _int, _vp]),
     "nfx_arqs_packed_floats": (_sz, [_int, _int, _int]),
     "nfx_arqs_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _int, _vp, _vp]),
     "nfx_arqs": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _int, ctypes.c_double,
@@ -101,6 +107,7 @@ _SIGNATURES = {
     "nfx_rqs_unit": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int, _vp]),
     "nfx_made_packed_floats": (_sz, [_int, _int]),
     "nfx_made_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
+    "nfx_made_seq_policy": (_int, [_int]),
     "nfx_made_affine": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_made_affine_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_made_pack_backward": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),

@@ -19,6 +19,7 @@ sample dimension). `nfs_amd.distributed.enable_sync_batchnorm()` takes those sta
 all data-parallel ranks (SyncBN).
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -36,6 +37,45 @@ ctypes_vp = ctypes.c_void_p
 # (kernel-name, start-event, end-event) of every train-mode layer pass while a list is installed
 # here (bench.py roofline timing); None = no events.
 TRAIN_EVENTS = None
+
+# One-launch layer chains (nfx_affine_chain, csrc/nfx_affine_chain.hip) are used for batches up to
+# this many samples; above it the per-layer streaming kernels (higher MFMA efficiency) run.
+CHAIN_MAX_B = int(os.environ.get("NFX_CHAIN_MAX_B", str(1 << 16)))
+
+
+def chain_ok(flows, x):
+    """A run of eval-mode CouplingLayers with one (d, H), d in {2, 4, 8}, H <= 128, on fp32 ROCm
+    rows, small enough for the one-launch chain kernel."""
+    if not flows or len(flows) > 64 or x.shape[0] > CHAIN_MAX_B or x.shape[0] == 0:
+        return False
+    f0 = flows[0]
+    if not isinstance(f0, CouplingLayer):
+        return False
+    d, H = f0.data_dim, f0._hidden()
+    if d not in (2, 4, 8) or H > MAX_H or x.shape[1] != d:
+        return False
+    for f in flows:
+        if type(f) is not CouplingLayer or f.data_dim != d or f._hidden() != H or f._torch_only():
+            return False
+    return True
+
+
+def chain_launch(flows, x, out, ld, direction, accumulate, logprob=None):
+    """All `flows` (in module order) in one nfx_affine_chain launch; with logprob=(logp, sums,
+    workspace) an inverse chain also writes the Gaussian log-density and NLL partials."""
+    packs = (ctypes_vp * len(flows))(*[_lib.ptr(f._packed(x.device, f._build_pack)) for f in flows])
+    L = _lib.lib()
+    d, H = flows[0].data_dim, flows[0]._hidden()
+    p = _lib.ptr
+    if logprob is not None:
+        logp, sums, ws = logprob
+        _lib.check(L.nfx_affine_chain_logprob(packs, len(flows), p(x), p(out), p(ld), p(logp), p(sums), p(ws),
+                                              x.shape[0], d, H, int(bool(accumulate)), _lib.stream_of(x)),
+                   "nfx_affine_chain_logprob")
+    else:
+        _lib.check(L.nfx_affine_chain(packs, len(flows), p(x), p(out), p(ld), x.shape[0], d, H, int(direction),
+                                      int(bool(accumulate)), _lib.stream_of(x)), "nfx_affine_chain")
+    STATS["hip"] += 1
 
 
 def _pad_d(d):
@@ -176,7 +216,8 @@ class CouplingLayer(HipFlow):
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
-                ev.append((f"affine_train_kernel<STATS{layer}>", e0, e1))
+                kn = "affine_trainw_kernel" if H > 64 else "affine_train_kernel"
+                ev.append((f"{kn}<STATS{layer}>", e0, e1))
             _dist.merge_bn_stats(stats[layer - 1].view(2, -1, 3))
             _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), p(stats[0]),
                                                p(stats[1]) if layer == 2 else None, d, H, p(tpack),
@@ -264,7 +305,8 @@ class CouplingLayer(HipFlow):
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()
-                ev.append((f"affine_train_kernel<BWD{stage}>", e0, e1))
+                kn = "affine_trainw_kernel" if H > 64 else "affine_train_kernel"
+                ev.append((f"{kn}<BWD{stage}>", e0, e1))
             if sync and stage in s_blocks:
                 _dist.allreduce_bn_sums(s_blocks[stage])
         grads = torch.empty(L.nfx_affine_train_param_floats(d, H), device=dev, dtype=torch.float32)

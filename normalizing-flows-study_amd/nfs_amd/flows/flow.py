@@ -273,6 +273,11 @@ class SequentialFlow(Flow):
     def _hip_chain(self, x, direction):
         x = x.contiguous()
         ld = torch.zeros(x.shape[0], device=x.device, dtype=torch.float32)
+        from . import coupling as _coupling
+        if _coupling.chain_ok(list(self.flows), x):  # one launch (csrc/nfx_affine_chain.hip)
+            out = torch.empty_like(x)
+            _coupling.chain_launch(list(self.flows), x, out, ld, direction, True)
+            return out, ld
         bufs = [torch.empty_like(x), torch.empty_like(x)]
         cur, k = x, 0
         for f in (self.flows if direction > 0 else reversed(self.flows)):

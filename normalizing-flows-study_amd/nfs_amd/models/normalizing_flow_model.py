@@ -18,6 +18,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..distributed import merge_bn_stats, sync_bn_world
+from ..flows import coupling as _coupling
 from ..flows.flow import HipFlow, STATS
 
 
@@ -127,8 +128,20 @@ class NormalizingFlowModel(nn.Module):
         x = x.contiguous()
         B = x.shape[0]
         ld = torch.empty(B, device=x.device, dtype=torch.float32)
-        bufs = [torch.empty_like(x), torch.empty_like(x)]
         n = len(self.flows)
+        if not self.batch_norm_between_layers and _coupling.chain_ok(list(self.flows), x):
+            # the whole chain in one launch (csrc/nfx_affine_chain.hip), same roundings
+            out = torch.empty_like(x)
+            ev = self.layer_events
+            if ev is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            _coupling.chain_launch(list(self.flows), x, out, ld, direction, False, logprob)
+            if ev is not None:
+                e1.record()
+                ev.append(("affine_chain_kernel", e0, e1))
+            return (out, ld, True) if logprob is not None else (out, ld)
+        bufs = [torch.empty_like(x), torch.empty_like(x)]
         order = range(n) if direction > 0 else reversed(range(n))
         cur, k, first, fused = x, 0, True, False
         for i in order:

@@ -16,6 +16,17 @@ from conftest import golden_json, load_golden, oracle_sd, state_dict_from
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["wave", "segment"])
+def seq_policy(request, cuda_device):
+    """Run a test on both sequential-direction kernels (nfx_made_seq_policy): the wave-per-sample
+    made_seqw_kernel (default) and the segment-parallel made_seqs_kernel."""
+    from nfs_amd import _lib
+    L = _lib.lib()
+    old = L.nfx_made_seq_policy(_lib.NFX_MADE_SEQ_WAVE if request.param == "wave" else _lib.NFX_MADE_SEQ_SEGMENT)
+    yield request.param
+    L.nfx_made_seq_policy(old)
+
+
 def assert_y(y, ref, tol=2e-5):
     y, ref = np.asarray(y, np.float64), np.asarray(ref, np.float64)
     err = np.abs(y - ref) / (1 + np.abs(ref))
@@ -47,7 +58,7 @@ def test_maf63_inverse_parallel_vs_reference(cuda_device):
     assert abs(nll - float(g["nll_f64"])) <= 1e-6 * abs(float(g["nll_f64"]))
 
 
-def test_maf63_forward_sequential_vs_reference(cuda_device):
+def test_maf63_forward_sequential_vs_reference(cuda_device, seq_policy):
     m, g = maf63(cuda_device)
     with torch.no_grad():
         x, ld = m.forward(torch.from_numpy(g["z"]).to(cuda_device))
@@ -55,7 +66,7 @@ def test_maf63_forward_sequential_vs_reference(cuda_device):
     assert_ld(ld.cpu(), g["fwd_ld"])
 
 
-def test_iaf784_vs_reference(cuda_device):
+def test_iaf784_vs_reference(cuda_device, seq_policy):
     g = load_golden("g6_iaf784.npz")
     f = nfs_amd.InverseAutoregressiveFlow(784, 64)
     f.load_state_dict(state_dict_from(g, "", f))
@@ -98,7 +109,7 @@ def test_small_made_flows(cuda_device, name, kind):
                                    # 128 < H <= 256: nfx_made_big.hip
                                    (5, 256, 70), (63, 160, 100), (100, 256, 65), (300, 256, 33), (2, 200, 40),
                                    (64, 129, 97)])
-def test_made_shapes_vs_oracle(cuda_device, d, H, B):
+def test_made_shapes_vs_oracle(cuda_device, d, H, B, seq_policy):
     torch.manual_seed(d * 31 + H)
     for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
         f = cls(d, H)
@@ -117,7 +128,7 @@ def test_made_shapes_vs_oracle(cuda_device, d, H, B):
 
 
 @pytest.mark.parametrize("d,H", [(6, 16), (100, 64), (40, 224)])
-def test_made_nonfinite_inputs(cuda_device, d, H):
+def test_made_nonfinite_inputs(cuda_device, d, H, seq_policy):
     """inf/NaN rows: parallel directions propagate 0*inf = NaN through the dense masked weights;
     sequential directions reproduce the reference's contamination of every later step."""
     torch.manual_seed(3)
@@ -187,7 +198,7 @@ def _iaf784(dev):
     return nfs_amd.NormalizingFlowModel([f]).to(dev).eval()
 
 
-def test_full_scale_nll_cfg5i(cuda_device):
+def test_full_scale_nll_cfg5i(cuda_device, seq_policy):
     """BASELINE cfg5 density direction at full size: IAF(784,64) log_prob through the sequential
     inverse (inverse_autoregressive_flow.py:65-103), B = 8192, NLL vs the reference (G8)."""
     meta = golden_json("g8_full_nll.json")["cfg5i_iaf_d784_B8192"]

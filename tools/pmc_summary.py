@@ -18,7 +18,8 @@ import statistics
 import sys
 
 HOT = ("affine_coupling_kernel", "spline_coupling_kernel", "made_parallel_kernel", "made_tile_kernel", "made_seq_kernel",
-       "made_wide_kernel", "made_seqs_kernel", "gauss_logprob_kernel", "rqs_unit_kernel")
+       "made_wide_kernel", "made_seqs_kernel", "made_seqw_kernel", "gauss_logprob_kernel", "rqs_unit_kernel",
+       "affine_chain_kernel", "affine_small_kernel", "affine_trainw_kernel", "affine_train_kernel")
 
 
 def rows(path_glob):

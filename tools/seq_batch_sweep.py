@@ -1,6 +1,10 @@
-"""Sequential IAF(784, 64) inverse (cfg5i shape): kernel time per batch size, HIP events around
-the layer call.   python tools/seq_batch_sweep.py
+"""Sequential IAF(784, 64) inverse (cfg5i shape) + fused Gaussian log_prob: kernel time per
+batch size for each sequential-MADE kernel (nfx_made_seq_policy: wave-per-sample made_seqw_kernel
+vs segment-parallel made_seqs_kernel), HIP events around the log_prob call.
+
+    python tools/seq_batch_sweep.py [B ...]
 """
+import json
 import os
 import sys
 
@@ -8,6 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "normalizing-flows-study_amd"))
 import torch  # noqa: E402
 import nfs_amd  # noqa: E402
+from nfs_amd import _lib  # noqa: E402
 
 d, H = 784, 64
 torch.manual_seed(0)
@@ -15,17 +20,25 @@ f = nfs_amd.InverseAutoregressiveFlow(d, H)
 with torch.no_grad():
     for p in f.parameters():
         p.add_(0.05 * torch.randn_like(p))
-f = f.cuda().eval()
-for B in (8192, 16384, 32768, 65536):
+m = nfs_amd.NormalizingFlowModel([f]).cuda().eval()
+L = _lib.lib()
+batches = [int(b) for b in sys.argv[1:]] or [256, 512, 1024, 2048, 4096, 8192, 16384, 32768]
+for B in batches:
     x = torch.randn(B, d, device="cuda")
-    with torch.no_grad():
-        for _ in range(2):
-            f.inverse(x)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            f.inverse(x)
-        e1.record()
-        torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 5
-    print(f"B={B} {ms:.3f} ms {B / ms / 1e3:.1f} M samples/s", flush=True)
+    row = {"B": B}
+    for name, pol in (("wave", _lib.NFX_MADE_SEQ_WAVE), ("segment", _lib.NFX_MADE_SEQ_SEGMENT)):
+        L.nfx_made_seq_policy(pol)
+        with torch.no_grad():
+            for _ in range(2):
+                m.log_prob(x, return_sums=True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                m.log_prob(x, return_sums=True)
+            e1.record()
+            torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 10
+        row[name + "_us"] = round(ms * 1e3, 1)
+        row[name + "_Msps"] = round(B / ms / 1e3, 2)
+    print(json.dumps(row), flush=True)
+L.nfx_made_seq_policy(_lib.NFX_MADE_SEQ_AUTO)
