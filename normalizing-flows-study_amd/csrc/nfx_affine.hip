@@ -188,7 +188,11 @@ static int affine_launch(const float* packed, const float* in, float* out, float
         if (rc || !fused) return rc;
         return gauss_finish(partials, grid_small, sums, B, stream);
     }
-    int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
+    // Up to one 32-sample half chunk per wave: when the resident waves outnumber the 64-sample
+    // chunks (small batches, e.g. a strong-scaled 125k shard), the kernel's split gives every wave
+    // a half chunk instead of leaving half the waves idle behind full chunks (the layer time is one
+    // wave's chain: 64 -> 32 samples halves it)
+    int grid = resident_grid((const void*)k, 256, lds, ((B + 31) / 32 + 3) / 4);
     if (grid > kMaxPartials) grid = kMaxPartials;
     k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, accumulate, nchunks, logp, partials, gauss_const(d));
     rc = check_launch("affine_coupling_kernel");

@@ -166,7 +166,8 @@ static int spline_launch(const float* packed, const float* in, float* out, float
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
     const int64_t nchunks = (B + 63) / 64;
-    int grid = resident_grid((const void*)k, 256, lds, (nchunks + 3) / 4);
+    // up to one 32-sample half chunk per wave at small batches (as nfx_affine.hip)
+    int grid = resident_grid((const void*)k, 256, lds, ((B + 31) / 32 + 3) / 4);
     if (grid > kMaxPartials) grid = kMaxPartials;
     double* partials = reinterpret_cast<double*>(workspace);
     k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, d, C, accumulate, nchunks, logp, partials,
