@@ -540,6 +540,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     if rank != 0:
         return None
     traffic = None
+    rocprof = None
     tp = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
     if os.path.exists(tp):
         with open(tp) as fh:
@@ -547,6 +548,20 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         spl = tj.get("samples_per_launch")
         if spl:
             traffic = tj["hbm_bytes_per_launch"] / spl * B
+        # the same kernel's mean duration under rocprofv3 --kernel-trace (the profile the traffic
+        # counters come from), dispatch-weighted over its template instances: frac quoted on it too
+        src = os.path.join(ROOT, "profiles", tj.get("source", ""))
+        if spl and os.path.isfile(src):
+            with open(src) as fh:
+                sj = json.load(fh)
+            sj = sj.get(config, sj)  # per-config file: {kernel: stats}
+            ks = [sj[k] for k in tj.get("kernel", []) if k in sj and sj[k].get("mean_us")]
+            n = sum(k["dispatches"] for k in ks)
+            if n:
+                mus = sum(k["mean_us"] * k["dispatches"] for k in ks) / n
+                ach = f_launch * spl / (mus * 1e-6) / 1e12
+                rocprof = {"mean_launch_us": mus, "samples_per_launch": spl, "achieved": ach,
+                           "frac": ach / PEAK_FP32_TFLOPS, "source": os.path.relpath(src, ROOT)}
     result = {
         "metric": METRIC,
         "value": B_global * a.steps / t_max,
@@ -575,7 +590,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                      "traffic": traffic, "flop_per_sample_per_launch": f_launch,
                      "layers_per_launch": layers_per_launch,
                      "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs),
-                     "traffic_source": os.path.relpath(tp, ROOT) if traffic is not None else None},
+                     "traffic_source": os.path.relpath(tp, ROOT) if traffic is not None else None,
+                     "rocprof": rocprof},
         "cpu_baseline": None,
     }
     if config == "cfg4":
