@@ -14,16 +14,15 @@ template <int HT>
 static made_seqw_kernel_t seqw_pick(int variant, bool logp, int nwv) {
     switch (nwv) {
         case 4: return seqw_pick_nwv<HT, 4>(variant, logp);
-        case 8: return seqw_pick_nwv<HT, 8>(variant, logp);
-        default: return seqw_pick_nwv<HT, 16>(variant, logp);
+        default: return seqw_pick_nwv<HT, 8>(variant, logp);
     }
 }
 
-// Waves (= samples) per workgroup: as many as keep at least one workgroup per CU (one fits a CU:
-// the two staged 64-step blocks take ~100 KB of LDS), at least 4.
+// Waves (= samples) per workgroup: 8 once that still gives every CU a workgroup (one fits a CU:
+// the two staged 64-step blocks take ~100 KB of LDS), else 4. Not 16: the kernel holds two
+// chunks' operands in registers (~150 VGPRs), more than 4 waves per SIMD leave room for.
 static int seqw_waves(int64_t B) {
     const int64_t cus = num_cus();
-    if ((B + 15) / 16 >= cus) return 16;
     if ((B + 7) / 8 >= cus) return 8;
     return 4;
 }
@@ -39,7 +38,7 @@ int made_seqw_launch(const float* packed, const float* in, float* out, float* lo
     if (rc) return rc;
     int64_t grid = (B + nwv - 1) / nwv;
     if (grid > kMaxPartials) grid = kMaxPartials;
-    k<<<(unsigned)grid, nwv * 64, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials,
+    k<<<(unsigned)grid, (nwv + 1) * 64, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials,
                                            gauss_const(d));
     *grid_out = (int)grid;
     return check_launch("made_seqw_kernel");

@@ -1,7 +1,7 @@
 """Stage clocks of the wave-per-sample sequential MADE kernel (IAF(784, 64) inverse), from a
 timing build:  NFX_BUILD_VARIANT=timing NFX_EXTRA_CFLAGS=-DNFX_SEQW_TIMING python
 normalizing-flows-study_amd/build.py, then  NFX_LIB=.../libnfx_timing.so python tools/seqw_timing.py [B]
-Workgroup 0 / wave 0 writes its accumulated clock64 ticks per stage into out[0, 0:7]."""
+Workgroup 0 / wave 0 writes its accumulated clock64 ticks per stage into out[0, 0:7] (stage names below)."""
 import json
 import os
 import sys
@@ -27,8 +27,8 @@ with torch.no_grad():
         z, _ = f.inverse(x)
     torch.cuda.synchronize()
 t = z[0, :9].double().cpu().tolist()
-names = ["dot+rowsum", "affine+ballot+stores", "bcast+rank1", "completion", "block sums+out", "dma wait+barrier",
-         "stage+x issue", "block tiles", "block end ballot"]
+names = ["operands+partials+dot+rowsum", "affine+ballot+stores", "bcast+rank1", "completion", "block end",
+         "dma wait+barrier", "block start", "-", "-"]
 tot = sum(t)
 print(json.dumps({"B": B, "total_ticks": tot, **{n: round(v / tot, 3) for n, v in zip(names, t)},
                   "ticks": dict(zip(names, t))}))
