@@ -226,7 +226,11 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     if (HT > 2) return NFX_OK;
     if (HT == 1) made_seqs_image_kernel<1><<<64, 256, 0, (hipStream_t)stream>>>(packed, d, H);
     else made_seqs_image_kernel<2><<<64, 256, 0, (hipStream_t)stream>>>(packed, d, H);
-    return check_launch("made_seqs_image_kernel");
+    rc = check_launch("made_seqs_image_kernel");
+    if (rc) return rc;
+    if (HT == 1) made_seqs_chunk_kernel<1><<<1, 64, 0, (hipStream_t)stream>>>(packed, d, H);
+    else made_seqs_chunk_kernel<2><<<1, 64, 0, (hipStream_t)stream>>>(packed, d, H);
+    return check_launch("made_seqs_chunk_kernel");
 }
 
 namespace nfx {

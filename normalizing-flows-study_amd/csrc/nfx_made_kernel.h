@@ -53,6 +53,7 @@ struct MadeLayout {
     int t4, t3, t2, t1;
     int rimg;  // made_seqs_kernel's LDS prologue image (HT <= 2): [w2 | w3 by rank][b1 | b2 | b3 | deg | gend]
     int sw1, sw4, sb4;  // made_seqs_kernel's block-ready step rows (HT <= 2), d + kSeqsPadRows rows each
+    int ctab;           // the sequential kernels' chunk schedule (HT <= 2): seqs_max_chunks x 8 words
     int total;
 };
 
@@ -63,6 +64,9 @@ __host__ __device__ constexpr int made_up4(int v) { return (v + 3) & ~3; }
 // 64-step block always be copied whole.
 __host__ __device__ constexpr int seqs_w4_stride(int Hp) { return 2 * Hp + 4; }
 constexpr int kSeqsPadRows = 64;
+// Chunks of the sequential schedule: each ends at 16 steps (<= d/16), at a completion (<= Hp) or
+// at a staged block's end (<= d/64 + Hp + 1); + 1 sentinel entry.
+__host__ __device__ constexpr int seqs_max_chunks(int d, int Hp) { return d / 8 + 2 * Hp + 8; }
 
 __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     MadeLayout L{};
@@ -106,6 +110,7 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     L.sw1 = o; o += made_up4(rows * L.Hp);
     L.sw4 = o; o += made_up4(rows * seqs_w4_stride(L.Hp));
     L.sb4 = o; o += made_up4(2 * rows);
+    L.ctab = o; o += HT <= 2 ? 8 * seqs_max_chunks(d, L.Hp) : 0;
     L.total = o;
     return L;
 }

@@ -555,6 +555,79 @@ __global__ __launch_bounds__(256) void made_seqs_image_kernel(float* __restrict_
     }
 }
 
+// The chunk schedule of the sequential directions, built once at pack time (one lane, serially,
+// over LDS copies of the rank tables). It depends only on the degrees, so the sequential kernels
+// read it instead of recomputing the bookkeeping per chunk. Entry k (8 words at P + L.ctab):
+//   [0] ii (block-relative first step) | nc << 8 | completes << 16 | one << 17 | last-in-block << 18
+//   [1] gc (= min(gi, Hp - 1)) | q (group end of gc) << 8 | h3 register slot << 16 | row << 24
+//   [2] pos(gc) (its W1t / W2 / W3 column)   [3] b2[gc]   [4] b3[gc]   [5] W2[gc][gc]   [6] W3[gc][gc]
+//   [7] i0 of the chunk's block
+// Blocks are made_seqs_kernel's (64 steps, or ending at the last segment end inside them).
+template <int HT>
+__global__ __launch_bounds__(64) void made_seqs_chunk_kernel(float* __restrict__ packed, int d, int H) {
+    constexpr int Hp = 32 * HT;
+    constexpr int UPL = Hp / 16;
+    const MadeLayout L = made_layout(d, HT);
+    const SeqsLds S = seqs_lds(Hp);
+    const float* img = packed + L.rimg;
+    __shared__ int deg[Hp], gend[Hp];
+    __shared__ float b2[Hp], b3[Hp], wd2[Hp], wd3[Hp];
+    for (int p = threadIdx.x; p < Hp; p += 64) {
+        deg[p] = p < H ? (int)img[S.tab + S.deg + p] : d;
+        gend[p] = (int)img[S.tab + S.gend + p];
+        b2[p] = img[S.tab + S.b2 + p];
+        b3[p] = img[S.tab + S.b3 + p];
+        const int pos = (p % 16) * UPL + p / 16;
+        wd2[p] = img[S.w2 + p * Hp + pos];
+        wd3[p] = img[S.w3 + p * Hp + pos];
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint32_t* tab = reinterpret_cast<uint32_t*>(packed + L.ctab);
+    const int cap = seqs_max_chunks(d, Hp) - 1;
+    int gi = 0, nextdeg = H > 0 ? deg[0] : d, k = 0;
+    for (int i0 = 0; i0 < d && k < cap;) {
+        int n = kSeqsStep;
+        if (i0 + kSeqsStep >= d) {
+            n = d - i0;
+        } else {
+            // the largest segment end (degree + 1) inside (i0, i0 + 64]
+            for (int g = 0; g < H; ++g) {
+                const int e = deg[g] + 1;
+                if (e > i0 && e <= i0 + kSeqsStep) n = e - i0;
+            }
+        }
+        for (int ii = 0; ii < n && k < cap;) {
+            const int i = i0 + ii;
+            int nc = n - ii < 16 ? n - ii : 16;
+            if (nextdeg - i + 1 < nc) nc = nextdeg - i + 1;
+            const bool completes = i + nc - 1 == nextdeg;
+            const int gc = gi < Hp ? gi : Hp - 1;
+            const int q = gend[gc];
+            const bool one = completes && q == gi + 1;
+            const bool last = ii + nc >= n;
+            uint32_t* e = tab + 8 * k;
+            e[0] = (uint32_t)ii | (uint32_t)nc << 8 | (uint32_t)completes << 16 | (uint32_t)one << 17 | (uint32_t)last << 18;
+            e[1] = (uint32_t)gc | (uint32_t)q << 8 | (uint32_t)(4 * (gc >> 4) + (gc & 3)) << 16 | (uint32_t)((gc >> 2) & 3) << 24;
+            e[2] = (uint32_t)((gc % 16) * UPL + gc / 16);
+            e[3] = __float_as_uint(b2[gc]);
+            e[4] = __float_as_uint(b3[gc]);
+            e[5] = __float_as_uint(wd2[gc]);
+            e[6] = __float_as_uint(wd3[gc]);
+            e[7] = (uint32_t)i0;
+            if (completes) {
+                gi = q;
+                nextdeg = gi < H ? deg[gi] : d;
+            }
+            ii += nc;
+            ++k;
+        }
+        i0 += n;
+    }
+    uint32_t* e = tab + 8 * k;  // sentinel: a valid, never-consumed prefetch target
+    for (int j = 0; j < 8; ++j) e[j] = 0u;
+}
+
 typedef void (*made_seqs_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int, float*,
                                    double*, float);
 

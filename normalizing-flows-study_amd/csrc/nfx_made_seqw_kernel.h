@@ -16,11 +16,12 @@
 //      directly and the lanes keep per-lane log-det partials;
 //   3. lane u owns the unit of completion rank u: its layer-1 pre-activation takes the chunk's
 //      new inputs (DPP row broadcasts) as rank-1 updates;
-//   4. the unit of degree D_{g+1} completes: its layer-2 and layer-3 sums over the units that
-//      completed BEFORE it (final h1 / h2) are all-reduced off the chain while steps 1-3 run, so
-//      on the chain only the diagonal terms remain: h1 = relu(pre1), h2 = relu(P2 + W2_gg h1 +
-//      b2), h3 = relu(P3 + W3_gg h2 + b3). (Several units of one degree take the general path:
-//      64-lane products + wave all-reduces, every lane gets the bit-identical sum.)
+//   4. the unit of degree D_{g+1} completes. Lane p also keeps unit p's layer-2 and layer-3 sums
+//      over the units completed so far (acc2, acc3: one FMA each per completion, with the
+//      completing unit's outgoing weights — W2 / W3 held transposed in LDS), so on the chain
+//      only the diagonal terms remain: h1 = relu(pre1), h2 = relu(acc2_g + W2_gg h1 + b2),
+//      h3 = relu(acc3_g + W3_gg h2 + b3) — no all-reduce. (Several units of one degree: the
+//      group's sums take every member first, MADE connecting equal degrees.)
 // Steps are staged as in made_seqs_kernel (64-step blocks of the block-ready image, 16-byte
 // LDS-DMA into a double buffer, the next block in flight) by a separate staging wave, which also
 // sums the fused Gaussian term's z^2 in step order (as nfx_gauss_logprob does) one block behind;
@@ -31,9 +32,9 @@
 
 namespace nfx {
 
-// per compute wave: the x block tile and two z block tiles (alternate blocks); then one z^2 sum
-// per sample slot
-constexpr int kSeqwTile = 3 * kSeqsStep;
+// per compute wave: the x block tile, two z block tiles (alternate blocks) and 64 floats where
+// masked lanes' stores land; then one z^2 sum per sample slot
+constexpr int kSeqwTile = 4 * kSeqsStep;
 
 __host__ __device__ inline int seqw_blkf(int Hp) { return kSeqsStep * Hp + kSeqsStep * seqs_w4_stride(Hp) + 2 * kSeqsStep; }
 // LDS: tables (5 Hp) | W2, W3 rank-ordered images (2 Hp^2) | two staged blocks | per-wave tiles | z^2 sums
@@ -56,9 +57,32 @@ __device__ __forceinline__ float rows4_sum(float v) {
     const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(t[0]) + __uint_as_float(t[1]);
 }
+// Row sums of two values at once (rows hold partials m_r, a_r): three lane swaps instead of four
+// (V_PERMLANE16_SWAP: odd rows of the first operand <-> even rows of the second; V_PERMLANE32_SWAP:
+// upper half of the first <-> lower half of the second); every lane ends with both sums.
+__device__ __forceinline__ void rows4_sum2(float m, float a, float& ms, float& as) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(a), false, false);
+    const float c = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows: m0+m1, a0+a1, m2+m3, a2+a3
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(c), false, false);
+    const float e = __uint_as_float(t[0]) + __uint_as_float(t[1]);  // rows: m, a, m, a
+    const auto u = __builtin_amdgcn_permlane16_swap(__float_as_uint(e), __float_as_uint(e), false, false);
+    ms = __uint_as_float(u[0]);
+    as = __uint_as_float(u[1]);
+}
 // Workgroup barrier over LDS only: unlike __syncthreads() it does not wait for the wave's global
 // stores (vmcnt), which the compute waves leave in flight.
 __device__ __forceinline__ void seqw_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A chunk's schedule entry (made_seqs_chunk_kernel), scalar-loaded (s_load_dwordx8) one chunk
+// ahead. Inline asm: the compiler would not use a scalar load here (the kernel's stores and asm
+// memory clobbers make every global read "clobberable" for it) and would read the entry with
+// vector loads + 8 v_readfirstlane instead. seqw_desc_wait is the matching wait; taking the entry
+// as an operand, it orders every use after it.
+typedef uint32_t SeqwDesc __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void seqw_desc_load(const uint32_t* p, SeqwDesc& o) {
+    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(o) : "s"(p) : "memory");
+}
+__device__ __forceinline__ void seqw_desc_wait(SeqwDesc& o) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(o)); }
 
 // The next chunk's W4 rows, biases and inputs, read one chunk ahead.
 template <int NM>
@@ -98,15 +122,19 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
     {
         const f32x4* src = reinterpret_cast<const f32x4*>(img + S.tab);
         for (int i = threadIdx.x; i < 5 * Hp / 4; i += (NWV + 1) * 64) lds4[i] = src[i];
-        // W2 / W3 rows by completion rank (columns by position)
-        const f32x4* sw = reinterpret_cast<const f32x4*>(img + S.w2);
-        for (int i = threadIdx.x; i < 2 * Hp * Hp / 4; i += (NWV + 1) * 64) lds4[5 * Hp / 4 + i] = sw[i];
+        // W2 / W3 TRANSPOSED by completion rank: wt[l][u][p] = W_l[rank p][rank u] (the image holds
+        // rows by rank p, columns by position), so lane p reads unit u's outgoing weights as one row
+        const float* sw = img + S.w2;
+        for (int e = threadIdx.x; e < 2 * Hp * Hp; e += (NWV + 1) * 64) {
+            const int l = e / (Hp * Hp), r = e % (Hp * Hp), u = r / Hp, pr = r % Hp;
+            lds[5 * Hp + e] = sw[l * Hp * Hp + pr * Hp + (u % 16) * UPL + u / 16];
+        }
     }
     __syncthreads();
-    const float* w23 = lds + 5 * Hp;  // [W2 rank rows | W3 rank rows]
+    const float* w2t = lds + 5 * Hp;  // [u][p]: W2[p][u]
+    const float* w3t = w2t + Hp * Hp;  // [u][p]: W3[p][u]
     const int tl = lane & (Hp - 1);
     const int degv = (int)lds[S.deg + tl];
-    const int gendv = (int)lds[S.gend + tl];
     const int b2v = __float_as_int(lds[S.b2 + tl]);
     const int b3v = __float_as_int(lds[S.b3 + tl]);
     float* blk0 = lds + 5 * Hp + 2 * Hp * Hp;
@@ -188,6 +216,8 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
         };
         // operands of the chunk at block position ii (rows past the block clamp to its last row:
         // their steps are masked out)
+        const uint32_t* ctab = reinterpret_cast<const uint32_t*>(P + L.ctab);
+        auto load_desc = [&](int k, SeqwDesc& o) { seqw_desc_load(ctab + 8 * k, o); };
         auto load_ops = [&](const float* blk, int ii, SeqwOps<NM>& o) {
             const int rj = ii + jl < kSeqsStep ? ii + jl : kSeqsStep - 1;
             const float* wr = blk + W4F + rj * RS4 + 8 * rq;
@@ -210,15 +240,17 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
         for (int64_t gb = (int64_t)blockIdx.x * NWV; gb < B; gb += (int64_t)gridDim.x * NWV) {
             const int64_t s = gb + wave;
             const bool valid = s < B;
-            float* orow = out + (valid ? s : 0) * d;
-            float pre1 = b1u, h1 = 0.f, h2 = 0.f;
+            const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(out + (valid ? s : 0) * d, 0, valid ? d * 4 : 0,
+                                                                  0x00020000);
+            // pre1: the owned unit's layer-1 pre-activation; acc2 / acc3: its layer-2 / layer-3 sums
+            // over the units completed so far (in completion order)
+            float pre1 = b1u, acc2 = 0.f, acc3 = 0.f;
             float h3r[4 * NM];
 #pragma unroll
             for (int k = 0; k < 4 * NM; ++k) h3r[k] = 0.f;
             float ldl = 0.f;  // per-lane log-det partial (steps ii + jl of every chunk)
             bool poisoned = false;
-            int gi = 0;
-            int nextdeg = H > 0 ? __builtin_amdgcn_readlane(degv, 0) : d;
+            int kc = 0;  // chunk index into the schedule
 
             int i0 = 0, n = blk_end(0), buf = 0, par = 0;
             float xr = x_load(s, 0, n);
@@ -226,7 +258,8 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             seqw_lds_barrier();  // B
             while (i0 < d) {
                 const float* blk = blk0 + buf * BLKF;
-                float* zt = xin_t + kSeqsStep * (1 + par);
+                const int zoff = kSeqsStep * (1 + par);
+                float* zt = xin_t + zoff;
                 xin_t[lane] = xr;
                 if (LOGP && lane >= n) zt[lane] = 0.f;
                 const int i0n = i0 + n;
@@ -234,26 +267,40 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                 if (nn > 0) xr = x_load(s, i0n, nn);
                 seqs_lds_order();
                 SeqwOps<NM> opa, opb;
+                SeqwDesc da, db;
+                load_desc(kc, da);
                 load_ops(blk, 0, opa);
                 NFX_WMARK(6);  // block start
-                int ii = 0;
-                auto chunk = [&](SeqwOps<NM>& c, SeqwOps<NM>& nx) {
-                    const int i = i0 + ii;
-                    int nc = n - ii < 16 ? n - ii : 16;
-                    if (nextdeg - i + 1 < nc) nc = nextdeg - i + 1;
-                    const bool completes = i + nc - 1 == nextdeg;
-                    const int ii2 = ii + nc;
-                    const int rj = ii + jl;
-                    // this chunk's LDS reads: unit gi's W2 / W3 rows and diagonal, the W1t rows
-                    const int gc = gi < Hp ? gi : Hp - 1;
-                    const int pg = (gc % 16) * UPL + gc / 16;
-                    const float w2n = own ? w23[gc * Hp + posu] : 0.f;
-                    const float w3n = own ? w23[Hp * Hp + gc * Hp + posu] : 0.f;
-                    const float wd2 = w23[gc * Hp + pg], wd3 = w23[Hp * Hp + gc * Hp + pg];
+                bool done = false;
+                auto chunk = [&](SeqwOps<NM>& c, SeqwOps<NM>& nx, SeqwDesc& dc, SeqwDesc& dn) {
+                    seqw_desc_wait(dc);
+                    load_desc(kc + 1, dn);
+                    // the chunk's schedule (made_seqs_chunk_kernel): no per-chunk bookkeeping
+                    const int ii = dc[0] & 0xff, nc = (dc[0] >> 8) & 0xff;
+                    const bool completes = (dc[0] >> 16) & 1u, one = (dc[0] >> 17) & 1u;
+                    done = (dc[0] >> 18) & 1u;
+                    const int gc = dc[1] & 0xff, q = (dc[1] >> 8) & 0xff, slot = (dc[1] >> 16) & 0xff;
+                    const int pg = (int)dc[2];
+                    const float b2g = __uint_as_float(dc[3]), b3g = __uint_as_float(dc[4]);
+                    const float wd2 = __uint_as_float(dc[5]), wd3 = __uint_as_float(dc[6]);
+                    const int i = i0 + ii, ii2 = ii + nc, rj = ii + jl;
+                    const unsigned rowm = one && rq == (int)(dc[1] >> 24) ? ~0u : 0u;  // lanes holding h3 of gc
+                    // this chunk's LDS reads: unit gc's outgoing W2 / W3 weights, the W1t rows (all
+                    // units' for the rank-1 updates; unit gc's for its own pre-activation)
+                    const float w2o = w2t[gc * Hp + tl], w3o = w3t[gc * Hp + tl];
+                    const float w1g = blk[rj * Hp + pg];
                     float w1v[16];
 #pragma unroll
                     for (int j = 0; j < 16; ++j) w1v[j] = own ? blk[(ii + j) * Hp + posu] : 0.f;  // rows past
                     // the block (ii + j < 80) read the finite W4 part of the same buffer; their steps are masked
+                    // unit gc's layer-1 pre-activation before this chunk, its layer-2 / layer-3 sums over
+                    // the units completed before it, its own (diagonal) weights
+                    const float p1g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre1), gc));
+                    const float P2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc2), gc));
+                    const float P3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc3), gc));
+                    // a poisoned sample's biases are NaN: every later step is NaN
+                    const float bmu = poisoned ? __builtin_nanf("") : c.bmu;
+                    const float bal = poisoned ? __builtin_nanf("") : c.bal;
                     // 1. step rj's mu/alpha over the lane's ranks, then the 4 rows meet
                     f32x2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f}, a2 = {0.f, 0.f}, a3 = {0.f, 0.f};
 #pragma unroll
@@ -265,17 +312,14 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                         a3 = pk_fma(f32x2{w1[2], w1[3]}, h3r[4 * m + 3], a3);
                     }
                     const f32x2 at = (a0 + a1) + (a2 + a3);
-                    float mu = rows4_sum(at[0]) + c.bmu;
-                    float al = rows4_sum(at[1]) + c.bal;
-                    // unit gi's layer-2 / layer-3 sums over the units completed before it
-                    const float P2 = wave_allsum(w2n * h1);
-                    const float P3 = wave_allsum(w3n * h2);
-                    NFX_WMARK(0);  // loads, dot products + row reduction, partial sums
+                    float mu, al;
+                    rows4_sum2(at[0], at[1], mu, al);
+                    mu = mu + bmu;
+                    al = al + bal;
+                    NFX_WMARK(0);  // loads, dot products + row reduction
                     // 2. step rj's affine map (every row)
                     const bool vj = jl < nc;
-                    mu = poisoned ? __builtin_nanf("") : mu;
-                    al = poisoned ? __builtin_nanf("") : al;
-                    float vi, vo, a;
+                    float vi, a;
                     if constexpr (VAR == NFX_MAF_FORWARD) {
                         a = tclamp(al, -3.f, 3.f);
                         vi = c.xin * exp_fast(a) + mu;
@@ -284,83 +328,84 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                         const float m = tclamp(mu, -10.f, 10.f);
                         vi = (c.xin - m) * exp_fast(-a);
                     }
-                    const uint64_t bad = __ballot(vj && nonfinite(vi));
+                    const float vz = vj ? vi : 0.f;
+                    // 3. the chain: unit gc completes. Its pre-activation takes the chunk's inputs as one
+                    // row sum; then only the diagonal terms of layers 2 and 3 are left. (A non-finite
+                    // step poisons the sample below; what it leaves in the sums reaches only steps that
+                    // the poison turns to NaN anyway.)
+                    {
+                        const float h1g = trelu(p1g + row16_allsum(vz * w1g));
+                        const float h2g = trelu(fmaf(wd2, h1g, P2) + b2g);
+                        const float h3g = trelu(fmaf(wd3, h2g, P3) + b3g);
+                        // select by bit mask (v_bfi_b32): one instruction, no exec-mask branch
+                        h3r[slot] = __uint_as_float((__float_as_uint(h3g) & rowm) | (__float_as_uint(h3r[slot]) & ~rowm));
+                        // every unit's running sums take unit gc's outputs
+                        acc2 = one ? fmaf(w2o, h1g, acc2) : acc2;
+                        acc3 = one ? fmaf(w3o, h2g, acc3) : acc3;
+                    }
+                    NFX_WMARK(1);  // affine map + completion
+                    // 4. off the chain: the poison rule, outputs, log-det
+                    const uint64_t bad = __builtin_amdgcn_ballot_w64(vj && nonfinite(vi));
                     const unsigned rowbad = (unsigned)bad & 0xFFFFu;  // every row holds the same steps
                     const bool kill = rowbad != 0u && jl > __builtin_ctz(rowbad | 0x10000u);
-                    vi = kill ? __builtin_nanf("") : vi;
+                    const float vk = kill ? __builtin_nanf("") : vi;
                     a = kill ? __builtin_nanf("") : a;
                     poisoned = poisoned || rowbad != 0u;
-                    if constexpr (VAR == NFX_MAF_FORWARD) vo = nonfinite(vi) ? 0.f : vi;
-                    else vo = nonfinite(vi) ? c.xin : vi;
+                    float vo;
+                    if constexpr (VAR == NFX_MAF_FORWARD) vo = nonfinite(vk) ? 0.f : vk;
+                    else vo = nonfinite(vk) ? c.xin : vk;
                     if constexpr (VAR == NFX_MAF_FORWARD) ldl = vj ? ldl + a : ldl;
                     else ldl = vj ? ldl - a : ldl;
-                    if (vj && rq == 0) {
-                        if (valid) orow[i + jl] = vo;
-                        if constexpr (LOGP) zt[rj] = vo;
-                    }
-                    NFX_WMARK(1);  // affine map, poison ballot, stores
-                    // 3. rank-1 updates of the owned unit's layer-1 pre-activation
-                    float cv[16];
-                    seqs_row_bcast16(vj ? vi : 0.f, cv);
                     {
-                        float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+                        // branch-free stores (a branch here would split the chunk's scheduling region):
+                        // out of range for the other lanes, which the buffer store drops
+                        const bool st = vj && rq == 0;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), orsrc, st ? (i + jl) * 4 : (int)0x7FFFFFF0,
+                                                              0, 0);
+                        if constexpr (LOGP) xin_t[st ? zoff + rj : 3 * kSeqsStep + lane] = vo;
+                    }
+                    // 5. rank-1 updates of every owned unit's layer-1 pre-activation
+                    float cv[16];
+                    seqs_row_bcast16(vz, cv);
+                    {
+                        // step pairs as packed FMAs: lanes (2j, 2j + 1) of the pair accumulators
+                        f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
 #pragma unroll
                         for (int j = 0; j < 16; j += 4) {
-                            t0 = fmaf(w1v[j], cv[j], t0);
-                            t1 = fmaf(w1v[j + 1], cv[j + 1], t1);
-                            t2 = fmaf(w1v[j + 2], cv[j + 2], t2);
-                            t3 = fmaf(w1v[j + 3], cv[j + 3], t3);
+                            t0 = __builtin_elementwise_fma(f32x2{w1v[j], w1v[j + 1]}, f32x2{cv[j], cv[j + 1]}, t0);
+                            t1 = __builtin_elementwise_fma(f32x2{w1v[j + 2], w1v[j + 3]}, f32x2{cv[j + 2], cv[j + 3]}, t1);
                         }
-                        pre1 = pre1 + ((t0 + t1) + (t2 + t3));
+                        const f32x2 tt = t0 + t1;
+                        pre1 = pre1 + (tt[0] + tt[1]);
                     }
-                    // the next chunk's W4 rows, biases and inputs (the completion reads no LDS)
-                    load_ops(blk, ii2 < n ? ii2 : ii, nx);
-                    NFX_WMARK(2);  // broadcasts + rank-1 updates
-                    // 4. the units of degree nextdeg (ranks gi .. q-1) complete
-                    const int q = __builtin_amdgcn_readlane(gendv, gc);
-                    const bool one = completes && q == gi + 1;
-                    {
-                        // one unit completes (branch-free): only the diagonal terms are left on the chain
-                        const float h1g = trelu(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre1), gc)));
-                        const float h2g = trelu(fmaf(wd2, h1g, P2) + __int_as_float(__builtin_amdgcn_readlane(b2v, gc)));
-                        const float h3g = trelu(fmaf(wd3, h2g, P3) + __int_as_float(__builtin_amdgcn_readlane(b3v, gc)));
-                        const bool mine = one && lane == gi;
-                        h1 = mine ? h1g : h1;
-                        h2 = mine ? h2g : h2;
-                        // h3r slot 4 (gc >> 4) + (gc & 3) of the lanes of row (gc >> 2) & 3: a uniform
-                        // register index
-                        const int slot = __builtin_amdgcn_readfirstlane(4 * (gc >> 4) + (gc & 3));
-                        const bool row = one && rq == ((gc >> 2) & 3);
-                        h3r[slot] = row ? h3g : h3r[slot];
-                    }
+                    // the next chunk's W4 rows, biases and inputs
+                    load_ops(blk, done ? ii : ii2, nx);
+                    NFX_WMARK(2);  // poison, stores, broadcasts + rank-1 updates
                     if (completes && !one) {
-                        // several units of one degree: 64-lane products + wave all-reduces
-                        if (lane >= gi && lane < q) h1 = trelu(pre1);
-                        for (int p = gi; p < q; ++p) {
-                            const float w = own ? w23[p * Hp + posu] : 0.f;
-                            const float h2p = trelu(wave_allsum(w * h1) + __int_as_float(__builtin_amdgcn_readlane(b2v, p)));
-                            if (lane == p) h2 = h2p;
-                        }
-                        for (int p = gi; p < q; ++p) {
-                            const float w = own ? w23[Hp * Hp + p * Hp + posu] : 0.f;
-                            const float h3p = trelu(wave_allsum(w * h2) + __int_as_float(__builtin_amdgcn_readlane(b3v, p)));
+                        // several units of one degree (MADE connects equal degrees): h1 of the group,
+                        // then its layer-2 sums, then layer 3
+                        const float h1v = trelu(pre1);
+                        for (int p = gc; p < q; ++p)
+                            acc2 = fmaf(w2t[p * Hp + tl], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h1v), p)), acc2);
+                        const float h2v = trelu(acc2 + __int_as_float(b2v));
+                        for (int p = gc; p < q; ++p)
+                            acc3 = fmaf(w3t[p * Hp + tl], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h2v), p)), acc3);
+                        const float h3v = trelu(acc3 + __int_as_float(b3v));
+                        for (int p = gc; p < q; ++p) {
+                            const float h3p = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h3v), p));
                             const int slot = __builtin_amdgcn_readfirstlane(4 * (p >> 4) + (p & 3));
                             const bool row = rq == ((p >> 2) & 3);
                             h3r[slot] = row ? h3p : h3r[slot];
                         }
                     }
-                    if (completes) {
-                        gi = q;
-                        nextdeg = gi < H ? __builtin_amdgcn_readlane(degv, gi) : d;
-                    }
                     NFX_WMARK(3);  // completion
-                    ii = ii2;
+                    ++kc;
                 };
-                for (;;) {  // two operand sets alternate: no register copies of loads in flight
-                    chunk(opa, opb);
-                    if (ii >= n) break;
-                    chunk(opb, opa);
-                    if (ii >= n) break;
+                for (;;) {  // two operand / schedule sets alternate: no register copies of loads in flight
+                    chunk(opa, opb, da, db);
+                    if (done) break;
+                    chunk(opb, opa, db, da);
+                    if (done) break;
                 }
                 seqw_lds_barrier();  // C
                 NFX_WMARK(5);  // barrier
