@@ -343,9 +343,10 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         const size_t lds = (size_t)seqs_lds(L.Hp).total * sizeof(float);
         int rc = prepare_lds((const void*)k, lds);
         if (rc) return rc;
-        int grid = resident_grid((const void*)k, 512, lds, (B + 4 * kSeqsWaves - 1) / (4 * kSeqsWaves));
+        const int threads = kSeqsThreads;
+        int grid = resident_grid((const void*)k, threads, lds, (B + 4 * kSeqsWaves - 1) / (4 * kSeqsWaves));
         if (grid > kMaxPartials) grid = kMaxPartials;
-        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials, gauss_const(d));
+        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials, gauss_const(d));
         rc = check_launch("made_seqs_kernel");
         if (rc || !fused) return rc;
         return gauss_finish(partials, grid, sums, B, s);

@@ -38,7 +38,10 @@
 
 namespace nfx {
 
-constexpr int kSeqsWaves = 8;  // 512-thread workgroups, 4 samples per wave
+constexpr int kSeqsWaves = 8;  // compute waves per workgroup (4 samples each)
+// + one staging wave that issues the blocks' LDS-DMA (else the compute waves share it)
+constexpr bool kSeqsStager = true;
+constexpr int kSeqsThreads = 64 * (kSeqsWaves + (kSeqsStager ? 1 : 0));
 constexpr int kSeqsStep = 64;  // steps per staged block
 constexpr int kSeqsH3 = 68;  // per-sample h3 row (by rank, Hp <= 64) + 4 pad floats
 // per wave: x, z, alpha block tiles; h3 rows; 64 floats where the lanes past a chunk store
@@ -111,6 +114,21 @@ __device__ __forceinline__ void seqs_dma_x4(const float* src, float* lds_dst) {
         : "v"(src), "s"(__builtin_amdgcn_readfirstlane(m))
         : "memory");
 }
+
+// Workgroup barrier over LDS only: unlike __syncthreads() it does not wait for the wave's global
+// stores (vmcnt), which the compute waves leave in flight.
+__device__ __forceinline__ void seqs_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A chunk's schedule entry (made_seqs_chunk_kernel), scalar-loaded (s_load_dwordx8) one chunk
+// ahead. Inline asm: the compiler would not use a scalar load here (the kernel's stores and asm
+// memory clobbers make every global read "clobberable" for it) and would read the entry with
+// vector loads + 8 v_readfirstlane instead. seqs_desc_wait is the matching wait; taking the entry
+// as an operand, it orders every use after it.
+typedef uint32_t SeqsDesc __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void seqs_desc_load(const uint32_t* p, SeqsDesc& o) {
+    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(o) : "s"(p) : "memory");
+}
+__device__ __forceinline__ void seqs_desc_wait(SeqsDesc& o) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(o)); }
 
 // Keeps the compiler from moving LDS accesses across this point. A wave's DS operations execute
 // in order, so wave-private tiles need nothing more -- and, unlike a fence, this emits no
@@ -200,7 +218,7 @@ __device__ __forceinline__ void seqs_unit(int p, int sub, const float (&w)[UPL],
 }
 
 template <int HT, int VAR, bool LOGP>
-__global__ __launch_bounds__(512) void made_seqs_kernel(
+__global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int H, int accumulate, float* __restrict__ logp,
     double* __restrict__ partials, float cgauss) {
@@ -222,14 +240,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
     const float* img = P + L.rimg;
     {
         const f32x4* src = reinterpret_cast<const f32x4*>(img + S.tab);
-        for (int i = threadIdx.x; i < S.blk / 4; i += 512) lds4[i] = src[i];
+        for (int i = threadIdx.x; i < S.blk / 4; i += kSeqsThreads) lds4[i] = src[i];
     }
     __syncthreads();
     // Per-rank tables held one entry per lane (Hp <= 64) and read with v_readlane at a uniform
     // rank: the completion chain (next degree, group end, layer-2/3 biases) has no LDS round trip.
     const int tl = lane & (Hp - 1);
     const int degv = (int)lds[S.deg + tl];
-    const int gendv = (int)lds[S.gend + tl];
     const int b2v = __float_as_int(lds[S.b2 + tl]);
     const int b3v = __float_as_int(lds[S.b3 + tl]);
     float* xin_t = lds + S.wv + wave * kSeqsTile;  // [4][64] inputs of the block
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         float* dst = lds + S.blk + buf * S.blkf;
         const float* sw1 = P + L.sw1 + (size_t)i0 * Hp;
         const float* sw4 = P + L.sw4 + (size_t)i0 * RS4;
-        for (int j = wave; j < N1 + N4 + 2; j += kSeqsWaves) {
+        for (int j = kSeqsStager ? 0 : wave; j < N1 + N4 + 2; j += kSeqsStager ? 1 : kSeqsWaves) {
             if (j < N1) {
                 seqs_dma_x4(sw1 + 256 * j + 4 * lane, dst + 256 * j);
             } else if (j < N1 + N4) {
@@ -293,6 +310,27 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
 #define NFX_TMARK(k) do { } while (0)
 #endif
     double lpacc = 0.0;
+    if (kSeqsStager && wave == kSeqsWaves) {
+        // staging wave: the LDS-DMA of every block (the compute waves never wait for it)
+        for (int64_t gb = (int64_t)blockIdx.x * kSeqsWaves * 4; gb < B; gb += (int64_t)gridDim.x * kSeqsWaves * 4) {
+            int i0 = 0, n = blk_end(0), buf = 0;
+            seqs_lds_barrier();  // A: the previous group is done with the staging buffers
+            blk_stage(0, 0);
+            seqs_dma_wait();
+            seqs_lds_barrier();  // B: block 0 is in LDS
+            while (i0 < d) {
+                const int i0n = i0 + n;
+                const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
+                if (nn > 0) blk_stage(i0n, buf ^ 1);
+                seqs_dma_wait();
+                seqs_lds_barrier();  // C: every compute wave is done with the block; the next is in
+                i0 = i0n;
+                n = nn;
+                buf ^= 1;
+            }
+        }
+    } else {
+    const uint32_t* ctab = reinterpret_cast<const uint32_t*>(P + L.ctab);
     for (int64_t gb = (int64_t)blockIdx.x * kSeqsWaves * 4; gb < B; gb += (int64_t)gridDim.x * kSeqsWaves * 4) {
         const int64_t s = gb + wave * 4 + slot;  // this row's sample
         const bool valid = s < B;
@@ -306,16 +344,20 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
         for (int e = lane; e < 4 * kSeqsH3; e += 64) h3_t[e] = 0.f;
         float ld = 0.f, zsq = 0.f;
         bool poisoned = false;
-        int gi = 0;  // completed units (ranks < gi)
-        int nextdeg = H > 0 ? __builtin_amdgcn_readlane(degv, 0) : d;
+        int kc = 0;  // chunk index into the schedule (made_seqs_chunk_kernel)
 
         float xr[4];
         int i0 = 0, n = blk_end(0), buf = 0;
         x_load(gb, i0, n, xr);
-        __syncthreads();  // previous group's readers of the staging buffers are done
-        blk_stage(i0, 0);
-        seqs_dma_wait();
-        __syncthreads();
+        if constexpr (kSeqsStager) {
+            seqs_lds_barrier();  // A
+            seqs_lds_barrier();  // B
+        } else {
+            __syncthreads();  // previous group's readers of the staging buffers are done
+            blk_stage(i0, 0);
+            seqs_dma_wait();
+            __syncthreads();
+        }
 
         while (i0 < d) {
             const float* blk = lds + S.blk + buf * S.blkf;
@@ -331,16 +373,22 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             const int i0n = i0 + n;
             const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
             if (nn > 0) {
-                blk_stage(i0n, buf ^ 1);  // its readers finished the previous block
+                if constexpr (!kSeqsStager) blk_stage(i0n, buf ^ 1);  // its readers finished the previous block
                 x_load(gb, i0n, nn, xr);
             }
             seqs_lds_order();
+            SeqsDesc da, db;
+            seqs_desc_load(ctab + 8 * kc, da);
 
             NFX_TMARK(6);  // block start: input tile, block end, LDS-DMA and x issue
-            for (int ii = 0; ii < n;) {
+            auto chunk = [&](SeqsDesc& dc, SeqsDesc& dn) -> bool {
+                seqs_desc_wait(dc);
+                seqs_desc_load(ctab + 8 * (kc + 1), dn);
+                // the chunk's schedule: first step, size, completion, completed units before it
+                const int ii = dc[0] & 0xff, nc = (dc[0] >> 8) & 0xff;
+                const bool completes = (dc[0] >> 16) & 1u, last = (dc[0] >> 18) & 1u;
+                const int q = (dc[1] >> 8) & 0xff, gi = (int)(dc[2] >> 16);
                 const int i = i0 + ii;
-                int nc = n - ii < 16 ? n - ii : 16;
-                if (nextdeg - i + 1 < nc) nc = nextdeg - i + 1;
                 // 1. lane sub forms step ii + sub's mu/alpha dot products over the completed ranks
                 // (< gi; ranks past it hold h3 = 0): the step's W4 row pair (mu, alpha) by rank
                 // against the sample's h3 row (one broadcast read per 4 ranks), two chains
@@ -423,8 +471,7 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 seqs_lds_order();  // the chunk tile is rewritten by the next chunk
                 NFX_TMARK(2);  // broadcasts + rank-1 updates
                 // 4. the units of degree nextdeg (ranks gi .. q-1) complete: layer 1, 2, 3
-                if (i + nc - 1 == nextdeg) {
-                    const int q = __builtin_amdgcn_readlane(gendv, gi);
+                if (completes) {
 #pragma unroll
                     for (int k = 0; k < UPL; ++k) {
                         const int p = sub + 16 * k;
@@ -450,11 +497,15 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                         const float v = seqs_unit_value<UPL>(p, w, h2v, b3v);
                         if (sub == 0) h3r[p] = v;
                     }
-                    gi = q;
-                    nextdeg = gi < H ? __builtin_amdgcn_readlane(degv, gi) : d;
                 }
                 NFX_TMARK(3);  // completion
-                ii += nc;
+                (void)i;
+                ++kc;
+                return last;
+            };
+            for (;;) {  // two schedule entries alternate: no copy of a scalar load in flight
+                if (chunk(da, db)) break;
+                if (chunk(db, da)) break;
             }
             seqs_lds_order();
             // log-det and z^2 of the block in step order (steps past d hold exact zeros)
@@ -476,9 +527,13 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
                 if (so < B && lane < n) out[so * d + i0 + lane] = zout_t[q * kSeqsStep + lane];
             }
             NFX_TMARK(4);  // log-det / z^2 sums of the block, output rows
-            seqs_dma_wait();  // the next block's LDS-DMA has landed
-            __syncthreads();  // ... for every wave; and every wave is done with this block
-            NFX_TMARK(5);  // vmcnt(0) + barrier
+            if constexpr (kSeqsStager) {
+                seqs_lds_barrier();  // C: the next block is in LDS, every wave is done with this one
+            } else {
+                seqs_dma_wait();  // the next block's LDS-DMA has landed
+                __syncthreads();  // ... for every wave; and every wave is done with this block
+            }
+            NFX_TMARK(5);  // barrier
             i0 = i0n;
             n = nn;
             buf ^= 1;
@@ -495,13 +550,14 @@ __global__ __launch_bounds__(512) void made_seqs_kernel(
             }
         }
     }
+    }
 #ifdef NFX_SEQS_TIMING
     // timing build only: workgroup 0's first lane overwrites sample 0's first outputs
     if (blockIdx.x == 0 && threadIdx.x == 0)
         for (int k = 0; k < 7; ++k) out[k] = (float)tacc[k];
 #endif
     if constexpr (LOGP) {
-        const double t = block_sum_f64<512>(lpacc);
+        const double t = block_sum_f64<kSeqsThreads>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
     }
 }
@@ -560,7 +616,7 @@ __global__ __launch_bounds__(256) void made_seqs_image_kernel(float* __restrict_
 // read it instead of recomputing the bookkeeping per chunk. Entry k (8 words at P + L.ctab):
 //   [0] ii (block-relative first step) | nc << 8 | completes << 16 | one << 17 | last-in-block << 18
 //   [1] gc (= min(gi, Hp - 1)) | q (group end of gc) << 8 | h3 register slot << 16 | row << 24
-//   [2] pos(gc) (its W1t / W2 / W3 column)   [3] b2[gc]   [4] b3[gc]   [5] W2[gc][gc]   [6] W3[gc][gc]
+//   [2] pos(gc) (its W1t / W2 / W3 column) | gi (completed units before the chunk) << 16   [3] b2[gc]   [4] b3[gc]   [5] W2[gc][gc]   [6] W3[gc][gc]
 //   [7] i0 of the chunk's block
 // Blocks are made_seqs_kernel's (64 steps, or ending at the last segment end inside them).
 template <int HT>
@@ -609,7 +665,7 @@ __global__ __launch_bounds__(64) void made_seqs_chunk_kernel(float* __restrict__
             uint32_t* e = tab + 8 * k;
             e[0] = (uint32_t)ii | (uint32_t)nc << 8 | (uint32_t)completes << 16 | (uint32_t)one << 17 | (uint32_t)last << 18;
             e[1] = (uint32_t)gc | (uint32_t)q << 8 | (uint32_t)(4 * (gc >> 4) + (gc & 3)) << 16 | (uint32_t)((gc >> 2) & 3) << 24;
-            e[2] = (uint32_t)((gc % 16) * UPL + gc / 16);
+            e[2] = (uint32_t)((gc % 16) * UPL + gc / 16) | (uint32_t)gi << 16;
             e[3] = __float_as_uint(b2[gc]);
             e[4] = __float_as_uint(b3[gc]);
             e[5] = __float_as_uint(wd2[gc]);

@@ -69,21 +69,6 @@ __device__ __forceinline__ void rows4_sum2(float m, float a, float& ms, float& a
     ms = __uint_as_float(u[0]);
     as = __uint_as_float(u[1]);
 }
-// Workgroup barrier over LDS only: unlike __syncthreads() it does not wait for the wave's global
-// stores (vmcnt), which the compute waves leave in flight.
-__device__ __forceinline__ void seqw_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// A chunk's schedule entry (made_seqs_chunk_kernel), scalar-loaded (s_load_dwordx8) one chunk
-// ahead. Inline asm: the compiler would not use a scalar load here (the kernel's stores and asm
-// memory clobbers make every global read "clobberable" for it) and would read the entry with
-// vector loads + 8 v_readfirstlane instead. seqw_desc_wait is the matching wait; taking the entry
-// as an operand, it orders every use after it.
-typedef uint32_t SeqwDesc __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ void seqw_desc_load(const uint32_t* p, SeqwDesc& o) {
-    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(o) : "s"(p) : "memory");
-}
-__device__ __forceinline__ void seqw_desc_wait(SeqwDesc& o) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(o)); }
-
 // The next chunk's W4 rows, biases and inputs, read one chunk ahead.
 template <int NM>
 struct SeqwOps {
@@ -180,10 +165,10 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
         for (int64_t gb = (int64_t)blockIdx.x * NWV; gb < B; gb += (int64_t)gridDim.x * NWV) {
             float z = 0.f;
             int i0 = 0, n = blk_end(0), buf = 0, par = 0;
-            seqw_lds_barrier();  // A: the previous group is done with the staging buffers
+            seqs_lds_barrier();  // A: the previous group is done with the staging buffers
             stage(0, 0);
             seqs_dma_wait();
-            seqw_lds_barrier();  // B: block 0 is in LDS
+            seqs_lds_barrier();  // B: block 0 is in LDS
             bool prev = false;
             while (i0 < d) {
                 const int i0n = i0 + n;
@@ -191,7 +176,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                 if (nn > 0) stage(i0n, buf ^ 1);
                 if (LOGP && prev) z = zsq_block(par ^ 1, z);  // the block before this one
                 seqs_dma_wait();
-                seqw_lds_barrier();  // C: block done by every compute wave; the next one is in LDS
+                seqs_lds_barrier();  // C: block done by every compute wave; the next one is in LDS
                 prev = true;
                 i0 = i0n;
                 n = nn;
@@ -201,7 +186,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             if constexpr (LOGP) {
                 z = zsq_block(par ^ 1, z);
                 if (lane < NWV) zsum_t[lane] = z;
-                seqw_lds_barrier();  // D: the sums are in LDS
+                seqs_lds_barrier();  // D: the sums are in LDS
             }
         }
     } else {
@@ -217,7 +202,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
         // operands of the chunk at block position ii (rows past the block clamp to its last row:
         // their steps are masked out)
         const uint32_t* ctab = reinterpret_cast<const uint32_t*>(P + L.ctab);
-        auto load_desc = [&](int k, SeqwDesc& o) { seqw_desc_load(ctab + 8 * k, o); };
+        auto load_desc = [&](int k, SeqsDesc& o) { seqs_desc_load(ctab + 8 * k, o); };
         auto load_ops = [&](const float* blk, int ii, SeqwOps<NM>& o) {
             const int rj = ii + jl < kSeqsStep ? ii + jl : kSeqsStep - 1;
             const float* wr = blk + W4F + rj * RS4 + 8 * rq;
@@ -254,8 +239,8 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
 
             int i0 = 0, n = blk_end(0), buf = 0, par = 0;
             float xr = x_load(s, 0, n);
-            seqw_lds_barrier();  // A
-            seqw_lds_barrier();  // B
+            seqs_lds_barrier();  // A
+            seqs_lds_barrier();  // B
             while (i0 < d) {
                 const float* blk = blk0 + buf * BLKF;
                 const int zoff = kSeqsStep * (1 + par);
@@ -267,20 +252,20 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                 if (nn > 0) xr = x_load(s, i0n, nn);
                 seqs_lds_order();
                 SeqwOps<NM> opa, opb;
-                SeqwDesc da, db;
+                SeqsDesc da, db;
                 load_desc(kc, da);
                 load_ops(blk, 0, opa);
                 NFX_WMARK(6);  // block start
                 bool done = false;
-                auto chunk = [&](SeqwOps<NM>& c, SeqwOps<NM>& nx, SeqwDesc& dc, SeqwDesc& dn) {
-                    seqw_desc_wait(dc);
+                auto chunk = [&](SeqwOps<NM>& c, SeqwOps<NM>& nx, SeqsDesc& dc, SeqsDesc& dn) {
+                    seqs_desc_wait(dc);
                     load_desc(kc + 1, dn);
                     // the chunk's schedule (made_seqs_chunk_kernel): no per-chunk bookkeeping
                     const int ii = dc[0] & 0xff, nc = (dc[0] >> 8) & 0xff;
                     const bool completes = (dc[0] >> 16) & 1u, one = (dc[0] >> 17) & 1u;
                     done = (dc[0] >> 18) & 1u;
                     const int gc = dc[1] & 0xff, q = (dc[1] >> 8) & 0xff, slot = (dc[1] >> 16) & 0xff;
-                    const int pg = (int)dc[2];
+                    const int pg = (int)(dc[2] & 0xffffu);
                     const float b2g = __uint_as_float(dc[3]), b3g = __uint_as_float(dc[4]);
                     const float wd2 = __uint_as_float(dc[5]), wd3 = __uint_as_float(dc[6]);
                     const int i = i0 + ii, ii2 = ii + nc, rj = ii + jl;
@@ -293,6 +278,9 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
 #pragma unroll
                     for (int j = 0; j < 16; ++j) w1v[j] = own ? blk[(ii + j) * Hp + posu] : 0.f;  // rows past
                     // the block (ii + j < 80) read the finite W4 part of the same buffer; their steps are masked
+                    // keep these reads at the chunk start (the scheduler would sink them next to their
+                    // uses, exposing their latency in the rank-1 updates and the running sums)
+                    __builtin_amdgcn_sched_barrier(0);
                     // unit gc's layer-1 pre-activation before this chunk, its layer-2 / layer-3 sums over
                     // the units completed before it, its own (diagonal) weights
                     const float p1g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pre1), gc));
@@ -407,7 +395,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                     chunk(opb, opa, db, da);
                     if (done) break;
                 }
-                seqw_lds_barrier();  // C
+                seqs_lds_barrier();  // C
                 NFX_WMARK(5);  // barrier
                 i0 = i0n;
                 n = nn;
@@ -417,7 +405,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             float ld = row16_allsum(ldl);
             float zsq = 0.f;
             if constexpr (LOGP) {
-                seqw_lds_barrier();  // D
+                seqs_lds_barrier();  // D
                 zsq = zsum_t[wave];
             }
             if (valid && lane == 0) {
