@@ -59,6 +59,10 @@ def perturb(model, sigma, seed):
                 mod.running_var.copy_(0.5 + torch.rand(mod.running_var.shape, generator=g))
 
 
+# the G16 figure-model training configs: fixture key prefix and Adam learning rate
+FIG_TRAIN = {"trainfig_spline": ("spline", 5e-4), "trainfig_maf": ("maf", 1e-3), "trainfig_iaf": ("iaf", 1e-3)}
+
+
 def build(config):
     """(model, d, flops_per_sample_per_layer, oracle spec, description)."""
     if config == "cfg2":
@@ -140,6 +144,26 @@ def build(config):
         return m, 2, f, oracle.realnvp_spec(10, training=True), \
             ("trainfig RealNVP(2,10,128) training step, full batch of 2,000 two-moons points "
              "(plots/_common.py:161,194-211: train-mode BatchNorm, Adam lr 1e-3, clip_grad_norm_ 5.0)")
+    if config in FIG_TRAIN:
+        # the reference's other benchmark-figure models in its training loop (plots/_common.py:
+        # 157-169, 178-183, 194-211), weights + data from the G16 fixture
+        import oracle
+        if config == "trainfig_spline":
+            m, H, K = nfs_amd.RealNVPSpline(2, 8, 64), 64, 10
+            P = 3 * K - 1
+            f = 2 * (3 * H * H + 3 * H + 3 * H * P)  # fused spline backward, as cfg3t
+            return m, 2, f, oracle.spline_model_spec(8), \
+                ("trainfig_spline RealNVPSpline(2,8,64) K=10 training step, full batch of 2,000 two-moons "
+                 "points (plots/_common.py:163,194-211: Adam lr 5e-4, clip_grad_norm_ 5.0)")
+        kind = "maf" if config == "trainfig_maf" else "iaf"
+        cls = nfs_amd.MaskedAutoregressiveFlow if kind == "maf" else nfs_amd.InverseAutoregressiveFlow
+        m = nfs_amd.NormalizingFlowModel([cls(2, 64) for _ in range(6)])
+        d, H = 2, 64
+        f = 2 * 2 * (d * H + 2 * H * H + 2 * d * H)  # forward recompute + data-gradient chain
+        spec = [(kind, f"flows.{i}.", {}) for i in range(6)]
+        return m, d, f, spec, \
+            (f"{config} 6x{kind.upper()}(2,64) training step, full batch of 2,000 two-moons points "
+             f"(plots/_common.py:165-167,194-211: Adam lr 1e-3, clip_grad_norm_ 5.0)")
     if config in ("cfg2t", "train5k"):
         torch.manual_seed(0)
         m = nfs_amd.RealNVP(2, 8, 64)
@@ -183,11 +207,12 @@ def build(config):
         return m, d, f, spec, "cfg5i IAF(784, 64) log_prob (sequential inverse), eval"
     raise ValueError(config)
 
-TRAIN_CONFIGS = ("cfg4t", "cfg2t", "train5k", "cfg3t", "trainfig")
+TRAIN_CONFIGS = ("cfg4t", "cfg2t", "train5k", "cfg3t", "trainfig", "trainfig_spline", "trainfig_maf", "trainfig_iaf")
 
 # Batch of each config: the BASELINE global batch (strong scaling splits it over the ranks,
 # --weak gives every rank all of it).
-DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "trainfig": 2_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
+DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "trainfig": 2_000, "trainfig_spline": 2_000,
+                 "trainfig_maf": 2_000, "trainfig_iaf": 2_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
                  "cfg4": 4_000_000, "cfg4t": 500_000, "cfg5f": 524_288, "cfg5i": 8_192,
                  "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000, "sample4k_iaf": 4_000}
 # The reference's only published throughput (assets/benchmark.png via
@@ -223,11 +248,11 @@ def load_reference_weights(model, config):
     model.load_state_dict(sd)
 
 
-def figure_batch():
-    """G15: the figure model's initial weights and its 2,000 standardized two-moons points
+def figure_batch(name="g15_fig_train.npz"):
+    """G15 / G16: the figure models' initial weights and the 2,000 standardized two-moons points
     (plots/_common.py:103-112), as the reference generated them."""
     import numpy as np
-    with np.load(os.path.join(GOLDEN, "g15_fig_train.npz"), allow_pickle=False) as z:
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
         arrs = {k: z[k] for k in z.files}
     return arrs
 
@@ -368,8 +393,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     model, d, f_layer, spec, desc = build(config)
     training = config in TRAIN_CONFIGS
     coupling_train = config in ("cfg2t", "train5k", "trainfig")
-    clip = 5.0 if config == "trainfig" else None
-    lr = 1e-3 if config == "trainfig" else 1e-5
+    clip = 5.0 if (config == "trainfig" or config in FIG_TRAIN) else None
+    lr = 1e-3 if config == "trainfig" else (FIG_TRAIN[config][1] if config in FIG_TRAIN else 1e-5)
     sampling = config == "cfg5f" or config.startswith("sample4k")
     pinned = config in REFERENCE_RUN
     if pinned:
@@ -379,6 +404,12 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         fig = figure_batch()
         model.load_state_dict({k: (torch.from_numpy(fig["fig.init." + k].copy()) if "fig.init." + k in fig else v)
                                for k, v in model.state_dict().items()})
+    elif config in FIG_TRAIN:
+        g16 = figure_batch("g16_fig_models.npz")
+        pre = FIG_TRAIN[config][0] + ".init."
+        model.load_state_dict({k: (torch.from_numpy(g16[pre + k].copy()) if pre + k in g16 else v)
+                               for k, v in model.state_dict().items()})
+        fig = {"fig.x": g16["x"]}
     if coupling_train and world > 1:
         from nfs_amd.distributed import enable_sync_batchnorm
         enable_sync_batchnorm(True)  # batch statistics over all ranks = the full-batch step
@@ -447,7 +478,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
 
     from nfs_amd.flows import autoregressive as _ar
     from nfs_amd.flows import spline as _sp
-    bwd_mod = _sp if config == "cfg3t" else _ar
+    bwd_mod = _sp if config in ("cfg3t", "trainfig_spline") else _ar
     with torch.set_grad_enabled(training):
         for _ in range(a.warmup):
             step()
@@ -623,6 +654,15 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         if world > 1:
             result["config"]["parallelism"] = (f"dp{world} (sample shards, SyncBN: 4 all-gathers/all-reduces "
                                                f"of <= 3 KB per layer + 1 bucketed gradient all-reduce)")
+    elif config in FIG_TRAIN:
+        result["metric"] = f"training samples/sec/GPU ({desc.split(' training')[0].split(' ', 1)[1]} figure-model step)"
+        result["data"] = ("the reference's own initial weights and 2,000 standardized two-moons points "
+                          "(tests/golden/g16_fig_models.npz, written by importing the reference)")
+        result["nll_f64"] = None
+        result["roofline"]["note"] = ("dominant kernel = the layer's fused backward (spline: MLP recompute, "
+                                      "spline adjoint, data-gradient chain and weight contractions; MADE: "
+                                      "forward recompute + data-gradient chain); at 2,000 samples the step "
+                                      "is launch-bound, frac is small by construction")
     elif config == "cfg3t":
         result["metric"] = "training samples/sec/GPU (8x RQ-spline coupling d=2 density step)"
         result["nll_f64"] = None
@@ -670,7 +710,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg2", "cfg2t", "train5k", "trainfig", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i",
+                    choices=["cfg2", "cfg2t", "train5k", "trainfig", "trainfig_spline", "trainfig_maf", "trainfig_iaf", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i",
                              "sample4k",
                              "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
     ap.add_argument("--batch", type=int, default=None,

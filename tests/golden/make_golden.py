@@ -33,6 +33,9 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
   g15_fig_train.npz   the benchmark-figure model RealNVP(2,10,128) (plots/_common.py:161) trained as
                       plots/_common.py:194-211: train-mode step on 2,000 two-moons points (z, ld, loss,
                       gradients, running stats) and 5 Adam + clip steps (losses, final state)
+  g16_fig_models.npz  the other benchmark-figure models (plots/_common.py:157-169): RealNVPSpline(2,8,64),
+                      6x MAF(2,64), 6x IAF(2,64): first train step (z, ld, loss, gradients) and 3 Adam +
+                      clip steps (losses, final state) on 2,000 two-moons points
   g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes (+ cfg5: IAF(784,64)
                       inverse NLL at B=8192 and forward checksums at B=524288)
 
@@ -578,6 +581,54 @@ def g15(models):
     np.savez_compressed(os.path.join(HERE, "g15_fig_train.npz"), **out)
 
 
+def g16(flows, models):
+    """The reference's other benchmark-figure models in training (plots/_common.py:157-169,
+    179-183, 194-211): RealNVPSpline(2, 8, 64) (lr 5e-4), 6x MaskedAutoregressiveFlow(2, 64) and
+    6x InverseAutoregressiveFlow(2, 64) in a NormalizingFlowModel (lr 1e-3), full batch on 2,000
+    two-moons points. Per model: the first step's z, ld, loss and raw gradients, then the losses
+    and final state of 3 Adam + clip_grad_norm_(5.0) steps."""
+    from torch.distributions import MultivariateNormal
+    out = {}
+    x = figure_moons(2000, 0)
+    out["x"] = x.numpy()
+    base = MultivariateNormal(torch.zeros(2), torch.eye(2))
+    builders = {
+        "spline": (lambda: models.RealNVPSpline(2, 8, 64), 5e-4),
+        "maf": (lambda: models.NormalizingFlowModel([flows.MaskedAutoregressiveFlow(2, 64) for _ in range(6)]), 1e-3),
+        "iaf": (lambda: models.NormalizingFlowModel([flows.InverseAutoregressiveFlow(2, 64) for _ in range(6)]), 1e-3),
+    }
+    for seed, (name, (build, lr)) in enumerate(builders.items()):
+        def fresh():
+            torch.manual_seed(160 + seed)
+            m = build()
+            perturb(m, 0.03, 170 + seed)
+            return m.train()
+
+        m = fresh()
+        out.update(sd_arrays(m, name + ".init."))
+        z, ld = m.inverse(x)
+        loss = -(base.log_prob(z) + ld).mean()
+        loss.backward()
+        out.update({name + ".z": z.detach().numpy(), name + ".ld": ld.detach().numpy(),
+                    name + ".loss": np.float64(loss.item())})
+        for k, p in m.named_parameters():
+            out[name + ".grad." + k] = p.grad.numpy()
+        m = fresh()
+        opt = torch.optim.Adam(m.parameters(), lr=lr)
+        losses = []
+        for _ in range(3):
+            z, ld = m.inverse(x)
+            loss = -(base.log_prob(z) + ld).mean()
+            opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(m.parameters(), 5.0)
+            opt.step()
+            losses.append(loss.item())
+        out[name + ".losses3"] = np.asarray(losses, dtype=np.float64)
+        out.update(sd_arrays(m, name + ".step3."))
+    np.savez_compressed(os.path.join(HERE, "g16_fig_models.npz"), **out)
+
+
 def g8_cfg5(f6):
     """cfg5 IAF(784,64) (G6 weights): inverse NLL at B=8192 (seed 1237) and forward checksums at
     B=524288 (seed 1238); merged into g8_full_nll.json."""
@@ -672,6 +723,9 @@ def main():
     if a.only == "g15":
         g15(models)
         return
+    if a.only == "g16":
+        g16(flows, models)
+        return
     if a.only == "g8_cfg5":
         g8_cfg5(g6(flows))
         return
@@ -689,6 +743,7 @@ def main():
     g13(flows)
     g14(flows)
     g15(models)
+    g16(flows, models)
     if not a.skip_full:
         g8(m2, m3, m5)
         g8_cfg5(f6)

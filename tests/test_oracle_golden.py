@@ -292,3 +292,28 @@ def test_gradients_g14(name, dname):
         assert np.abs(p.grad.numpy() - ref).max() <= 1e-5 * (1 + np.abs(ref).max()), k
         n += 1
     assert n >= 6
+
+
+@pytest.mark.parametrize("name", ["spline", "maf", "iaf"])
+def test_figure_models_g16(name):
+    """The oracle's training step of the reference's other benchmark-figure models
+    (plots/_common.py:157-169, 194-211) reproduces the reference's own z, log-det, loss and raw
+    gradients (G16) in float32 on 2,000 two-moons points."""
+    g = load_golden("g16_fig_models.npz")
+    spec = oracle.spline_model_spec(8) if name == "spline" else [(name, f"flows.{i}.", {}) for i in range(6)]
+    sd = oracle_sd(g, name + ".init.")
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items() if not k.endswith("mask")}
+    sd.update(params)
+    x = torch.from_numpy(g["x"])
+    z, ld = oracle.flow_model(sd, spec, x, -1)
+    loss = -oracle.gauss_log_prob(z, ld).mean()
+    loss.backward()
+    close(z.detach(), g[name + ".z"], rtol=2e-5, atol=2e-5)
+    close(ld.detach(), g[name + ".ld"], rtol=2e-5, atol=2e-5)
+    assert abs(loss.item() - float(g[name + ".loss"])) <= 1e-5
+    n = 0
+    for k, p in params.items():
+        ref = g[name + ".grad." + k]
+        assert np.abs(p.grad.numpy() - ref).max() <= 1e-4 * (1 + np.abs(ref).max()), k
+        n += 1
+    assert n == 48
