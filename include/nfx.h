@@ -374,6 +374,44 @@ int nfx_flowbn_backward(const float* in, const float* grad_out, const float* gra
                         const float* running_var, float eps, float* grad_gamma, float* grad_beta,
                         int64_t B, int d, int direction, void* workspace, void* stream);
 
+
+/* ---------------------------------------------------------------------------------------
+ * Any-shape path (csrc/nfx_generic.hip): the conditioner MLP of a layer whose shape is beyond
+ * the fused kernel families, one nn.Linear at a time on fp32 MFMA, plus the spline coupling's
+ * element math. Row-major fp32 device buffers; w is an nn.Linear weight [N][K] (out x in).
+ * ------------------------------------------------------------------------------------- */
+/* y[M][N] = act((x[M][K] o in_scale[K]) w^T + b): one nn.Linear (+ ReLU when relu = 1);
+ * in_scale (e.g. the coupling mask: Linear(x * mask)) and b may be NULL. Replaces
+ * torch.nn.functional.linear (+ relu) inside the reference's conditioner nn.Sequential. */
+int nfx_linear_forward(const float* x, const float* w, const float* b, const float* in_scale, float* y,
+                       int64_t M, int K, int N, int relu, void* stream);
+/* gx[M][K] (+)= ((gy[M][N] w) o out_scale[K]), kept only where act[M][K] > 0 when act is given
+ * (the ReLU backward of the layer feeding this Linear): autograd's input gradient of
+ * nn.Linear. accumulate = 1 adds into gx. */
+int nfx_linear_backward_data(const float* gy, const float* w, const float* act, const float* out_scale,
+                             float* gx, int64_t M, int N, int K, int accumulate, void* stream);
+/* gw[N][K] = gy^T (x o in_scale), gb[N] = sum over rows of gy (gb may be NULL): autograd's
+ * weight and bias gradients of nn.Linear, split over the batch into a workspace of
+ * nfx_linear_workspace_bytes(M, N, K) bytes and summed in a fixed order (deterministic). */
+size_t nfx_linear_workspace_bytes(int64_t M, int N, int K);
+int nfx_linear_backward_weight(const float* gy, const float* x, const float* in_scale, float* gw, float* gb,
+                               int64_t M, int N, int K, void* workspace, void* stream);
+/* SplineCouplingLayer element math for any d (spline_coupling_layer.py:96-180 with the spline
+ * of :182-309): params [B][d][3K-1] = param_net output; dims with mask == 0 go through the RQ
+ * spline (forward: direction +1, inverse: -1), the rest pass through; layer guards and the
+ * log-det (sum over transformed dims, guarded; written or added with accumulate). 2 <= K <= 11,
+ * data_min/data_max None. */
+int nfx_spline_elem_forward(const float* x, const float* params, const float* mask, float* y, float* log_det,
+                            int64_t B, int d, int K, float bound, float min_bin_width, float min_bin_height,
+                            float min_derivative, int direction, int accumulate, void* stream);
+/* Its adjoint: gparams [B][d][3K-1] = dL/dparams (zero for conditioning dims) and gx [B][d] =
+ * the direct dL/dx term (the conditioner's contribution is added by nfx_linear_backward_data
+ * with out_scale = mask). gy / gld (dL/dy, dL/dlog_det) may be NULL (zero). */
+int nfx_spline_elem_backward(const float* x, const float* params, const float* mask, const float* gy,
+                             const float* gld, float* gparams, float* gx, int64_t B, int d, int K, float bound,
+                             float min_bin_width, float min_bin_height, float min_derivative, int direction,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,396 @@
+// Any-shape path for the conditioner MLPs and the spline coupling element math (gfx950).
+//
+// The fused layer kernels (nfx_spline*.hip, nfx_affine*.hip, nfx_made*.hip) hold a whole
+// conditioner in registers and LDS and therefore cover bounded shape families. Shapes beyond
+// them — e.g. SplineCouplingLayer with H = 128 or several transformed dims under autograd, or
+// d > 64 — run the same math as a short sequence of launches over HBM-resident activations:
+//
+//   nfx_linear_forward        Y = act((X o s_k) W^T + b)          one nn.Linear (+ ReLU)
+//   nfx_linear_backward_data  G = ((D W) o s_k) [relu'(A)] (+ G)   dL/dinput of one nn.Linear
+//   nfx_linear_backward_weight dW = D^T (X o s_k), db = sum_rows D  split-K, fixed-order reduce
+//   nfx_spline_elem_forward   the coupling's RQ spline per (sample, transformed dim), guards,
+//                             log-det sum (spline_coupling_layer.py:96-180, :182-309)
+//   nfx_spline_elem_backward  its adjoint: dL/dparams, the direct dL/dx term
+//
+// GEMM: one kernel template for the three operand layouts an nn.Linear needs (NT forward, NN
+// data gradient, TN weight gradient), fp32 v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32
+// accumulation), 64 x 64 output tile per 256-thread workgroup (2 x 2 waves of 32 x 32), K staged
+// through LDS 32 at a time with the next K tile's global loads in flight during the current
+// tile's MFMAs. The weight gradient contracts over the batch: split-K over workgroups into a
+// [split][M][N] float workspace summed in a fixed order (deterministic, no atomics).
+#include <cstdlib>
+
+#include "nfx_common.h"
+#include "nfx_spline_bwd_kernel.h"  // rq_spline_adjoint
+#include "nfx_spline_kernel.h"      // rq_spline_elem, SplineConsts
+
+namespace nfx {
+
+constexpr int kGBM = 64, kGBN = 64, kGBK = 32;
+
+struct GemmArgs {
+    const float* a;          // A(m, k): TA = 0 -> a[m * lda + k], TA = 1 -> a[k * lda + m]
+    const float* b;          // B(k, n): TB = 0 -> b[k * ldb + n], TB = 1 -> b[n * ldb + k]
+    float* c;                // C(m, n) = c[m * ldc + n] (+ z * M * N for split-K partials)
+    int64_t M, N, K, lda, ldb, ldc;
+    const float* kscale;     // optional, length K: A(m, k) *= kscale[k]   (x * mask inputs)
+    const float* bias;       // optional, length N
+    const float* act;        // optional [M][ldact]: keep C(m, n) where act(m, n) > 0 (ReLU backward)
+    int64_t ldact;
+    const float* nscale;     // optional, length N: C(m, n) *= nscale[n]
+    int relu, accumulate;
+    int64_t kchunk;          // split-K: workgroup z covers k in [z * kchunk, (z + 1) * kchunk)
+};
+
+template <int TA, int TB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+    __shared__ float As[kGBM][kGBK + 1];
+    __shared__ float Bs[kGBK][kGBN + 1];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, h = lane >> 5, col = lane & 31;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int64_t m0 = (int64_t)blockIdx.x * kGBM, n0 = (int64_t)blockIdx.y * kGBN;
+    const int64_t kb = (int64_t)blockIdx.z * g.kchunk;
+    const int64_t ke = kb + g.kchunk < g.K ? kb + g.kchunk : g.K;
+    float ra[8], rb[8];
+    // global -> registers for the K tile at k0 (coalesced along the contiguous index)
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int idx = e * 256 + t;
+            int mi, ki;
+            if (TA == 0) { mi = idx >> 5; ki = idx & 31; } else { ki = idx >> 6; mi = idx & 63; }
+            const int64_t m = m0 + mi, k = k0 + ki;
+            float v = 0.f;
+            if (m < g.M && k < ke) {
+                v = TA == 0 ? g.a[m * g.lda + k] : g.a[k * g.lda + m];
+                if (g.kscale) v *= g.kscale[k];
+            }
+            ra[e] = v;
+            int ni, kj;
+            if (TB == 0) { kj = idx >> 6; ni = idx & 63; } else { ni = idx >> 5; kj = idx & 31; }
+            const int64_t n = n0 + ni, k2 = k0 + kj;
+            float w = 0.f;
+            if (n < g.N && k2 < ke) w = TB == 0 ? g.b[k2 * g.ldb + n] : g.b[n * g.ldb + k2];
+            rb[e] = w;
+        }
+    };
+    auto park = [&]() {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int idx = e * 256 + t;
+            if (TA == 0) As[idx >> 5][idx & 31] = ra[e]; else As[idx & 63][idx >> 6] = ra[e];
+            if (TB == 0) Bs[idx >> 6][idx & 63] = rb[e]; else Bs[idx & 31][idx >> 5] = rb[e];
+        }
+    };
+    f32x16 acc = {};
+    if (kb < ke) load(kb);
+    for (int64_t k0 = kb; k0 < ke; k0 += kGBK) {
+        __syncthreads();  // previous tile's readers are done
+        park();
+        __syncthreads();
+        if (k0 + kGBK < ke) load(k0 + kGBK);  // in flight during this tile's MFMAs
+#pragma unroll
+        for (int s = 0; s < kGBK / 2; ++s)
+            acc = mfma32(As[wm * 32 + col][2 * s + h], Bs[2 * s + h][wn * 32 + col], acc);
+    }
+    float* c = g.c + (int64_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm * 32 + crow(r, h), n = n0 + wn * 32 + col;
+        if (m < g.M && n < g.N) {
+            float v = acc[r];
+            if (g.bias) v += g.bias[n];
+            if (g.relu) v = trelu(v);
+            if (g.act) v = g.act[m * g.ldact + n] > 0.f ? v : 0.f;
+            if (g.nscale) v *= g.nscale[n];
+            float* p = c + m * g.ldc + n;
+            if (g.accumulate) v += *p;
+            *p = v;
+        }
+    }
+}
+
+static int gemm_launch(const GemmArgs& g, int ta, int tb, int64_t splits, hipStream_t s) {
+    // M tiles on x (the batch: up to 2^31 - 1 tiles), N tiles and split-K slices on y / z (< 65536)
+    const int64_t gm = (g.M + kGBM - 1) / kGBM, gn = (g.N + kGBN - 1) / kGBN;
+    if (gm > 0x7fffffff || gn > 65535 || splits > 65535)
+        return set_error(NFX_EUNSUPPORTED, "linear: grid %lld x %lld x %lld out of range", (long long)gm,
+                         (long long)gn, (long long)splits);
+    dim3 grid((unsigned)gm, (unsigned)gn, (unsigned)splits);
+    if (ta == 0 && tb == 1) gemm_kernel<0, 1><<<grid, 256, 0, s>>>(g);
+    else if (ta == 0 && tb == 0) gemm_kernel<0, 0><<<grid, 256, 0, s>>>(g);
+    else if (ta == 1 && tb == 0) gemm_kernel<1, 0><<<grid, 256, 0, s>>>(g);
+    else return set_error(NFX_EINVAL, "linear: unsupported layout");
+    return check_launch("gemm_kernel");
+}
+
+// out[i] (+)= sum_z part[z * n + i], z = 0 .. nz-1 in order
+__global__ void split_reduce_kernel(const float* __restrict__ part, int64_t nz, int64_t n, float* __restrict__ out,
+                                    int accumulate) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.f;
+        for (int64_t z = 0; z < nz; ++z) v += part[z * n + i];
+        out[i] = accumulate ? out[i] + v : v;
+    }
+}
+
+// Column sums of D [M][N] over row range z: part[z][n] (8 row groups x 32 columns per block,
+// the 8 group sums combined in a fixed order)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ d, int64_t M, int64_t N,
+                                                     int64_t rchunk, float* __restrict__ part) {
+    __shared__ float red[8][33];
+    const int cx = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    const int64_t n = (int64_t)blockIdx.x * 32 + cx;
+    const int64_t rb = (int64_t)blockIdx.y * rchunk, re = rb + rchunk < M ? rb + rchunk : M;
+    float v = 0.f;
+    if (n < N)
+        for (int64_t m = rb + rg; m < re; m += 8) v += d[m * N + n];
+    red[rg][cx] = v;
+    __syncthreads();
+    if (rg == 0 && n < N) {
+        float s = 0.f;
+        for (int q = 0; q < 8; ++q) s += red[q][cx];
+        part[(int64_t)blockIdx.y * N + n] = s;
+    }
+}
+
+static int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) {
+    const int64_t tiles = ((M + kGBM - 1) / kGBM) * ((N + kGBN - 1) / kGBN);
+    const int64_t want = (4 * (int64_t)num_cus() + tiles - 1) / tiles;
+    const int64_t maxs = (K + 1023) / 1024;  // at least 1024 rows per split
+    int64_t s = want < maxs ? want : maxs;
+    if (s < 1) s = 1;
+    if (s > 1024) s = 1024;
+    return s;
+}
+
+// ---- RQ spline coupling, element math ------------------------------------------------------
+static SplineConsts spline_consts(int K, float bound, float min_w, float min_h, float min_d) {
+    SplineConsts C{};
+    C.bound = bound;
+    C.two_bound = (float)(2.0 * (double)bound);
+    C.min_w = min_w;
+    C.cw = (float)(1.0 - (double)min_w * K);
+    C.min_h = min_h;
+    C.ch = (float)(1.0 - (double)min_h * K);
+    C.min_d = min_d;
+    C.rescale = 0;
+    return C;
+}
+
+// one lane per sample: every dim in order, spline on the transformed ones (mask == 0), the
+// layer guards (spline_coupling_layer.py:130-135 / :173-178) and the log-det (sum over the
+// transformed dims in order, then accumulate)
+template <int K, bool INV>
+__global__ __launch_bounds__(256) void spline_elem_fwd_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ prm,
+                                                              const float* __restrict__ mask, float* __restrict__ y,
+                                                              float* __restrict__ log_det, int64_t B, int d,
+                                                              int accumulate, const SplineConsts C) {
+    constexpr int P = 3 * K - 1;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    float ld = 0.f;
+    bool first = true;
+    for (int j = 0; j < d; ++j) {
+        const float v = x[s * d + j];
+        float o = v;
+        if (mask[j] == 0.f) {
+            float p[32];
+            const float* pr = prm + (s * d + j) * P;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) p[i] = i < P ? pr[i] : 0.f;
+            float lad;
+            rq_spline_elem<K, INV>(v, p, C, o, lad);
+            ld = first ? lad : ld + lad;
+            first = false;
+        }
+        y[s * d + j] = nonfinite(o) ? 0.f : o;
+    }
+    if (nonfinite(ld)) ld = 0.f;
+    log_det[s] = accumulate ? log_det[s] + ld : ld;
+}
+
+// two lanes per (sample, dim) element — lane half h = 0 owns the width side, h = 1 the heights
+// (rq_spline_adjoint); a wave covers 32 samples, walking the dims. gprm gets dL/dparams of every
+// dim (zeros for conditioning dims), gx the direct dL/dx term (the spline's own input gradient
+// for transformed dims, gy through the layer guard for conditioning dims).
+template <int K, bool INV>
+__global__ __launch_bounds__(256) void spline_elem_bwd_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ prm,
+                                                              const float* __restrict__ mask,
+                                                              const float* __restrict__ gy,
+                                                              const float* __restrict__ gld,
+                                                              float* __restrict__ gprm, float* __restrict__ gx,
+                                                              int64_t B, int d, const SplineConsts C) {
+    constexpr int P = 3 * K - 1;
+    const int lane = lane_id(), h = lane >> 5, col = lane & 31;
+    const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + col;
+    const bool ok = s < B;
+    const int64_t sc = ok ? s : 0;
+    const float gl = gld ? gld[sc] : 0.f;
+    for (int j = 0; j < d; ++j) {
+        const float v = x[sc * d + j];
+        const float g = gy ? gy[sc * d + j] : 0.f;
+        float* gp = gprm + (sc * d + j) * P;
+        if (mask[j] == 0.f) {
+            float p[32];
+            const float* pr = prm + (sc * d + j) * P;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) p[i] = i < P ? pr[i] : 0.f;
+            float o, gs[K], gd[K / 2], gv;
+            // the layer guard zeroes a non-finite output, which only a non-finite input gives
+            rq_spline_adjoint<K, INV>(v, p, C, nonfinite(v) ? 0.f : g, gl, o, gs, gd, gv);
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) gp[h * K + k] = gs[k];
+#pragma unroll
+                for (int q = 0; q < K / 2; ++q)
+                    if (2 * q + h < K - 1) gp[2 * K + 2 * q + h] = gd[q];
+                if (h == 0) gx[s * d + j] = gv;
+            }
+        } else if (ok) {
+            for (int i = h; i < P; i += 2) gp[i] = 0.f;
+            if (h == 0) gx[s * d + j] = nonfinite(v) ? 0.f : g;
+        }
+    }
+}
+
+template <bool BWD>
+static const void* spline_elem_pick(int K, bool inv) {
+#define NFX_SE(k)                                                                                         \
+    case k:                                                                                               \
+        if (BWD) return inv ? (const void*)spline_elem_bwd_kernel<k, true> : (const void*)spline_elem_bwd_kernel<k, false>; \
+        return inv ? (const void*)spline_elem_fwd_kernel<k, true> : (const void*)spline_elem_fwd_kernel<k, false>;
+    switch (K) {
+        NFX_SE(2) NFX_SE(3) NFX_SE(4) NFX_SE(5) NFX_SE(6) NFX_SE(7) NFX_SE(8) NFX_SE(9) NFX_SE(10) NFX_SE(11)
+    }
+#undef NFX_SE
+    return nullptr;
+}
+
+}  // namespace nfx
+
+using namespace nfx;
+
+extern "C" int nfx_linear_forward(const float* x, const float* w, const float* b, const float* in_scale, float* y,
+                                  int64_t M, int K, int N, int relu, void* stream) {
+    if (M < 0 || K <= 0 || N <= 0) return set_error(NFX_EINVAL, "linear_forward: bad shape M=%lld K=%d N=%d", (long long)M, K, N);
+    if (M == 0) return NFX_OK;
+    if (!x || !w || !y) return set_error(NFX_EINVAL, "linear_forward: null pointer");
+    GemmArgs g{};
+    g.a = x; g.lda = K;
+    g.b = w; g.ldb = K;
+    g.c = y; g.ldc = N;
+    g.M = M; g.N = N; g.K = K;
+    g.kscale = in_scale;
+    g.bias = b;
+    g.relu = relu;
+    g.kchunk = K;
+    return gemm_launch(g, 0, 1, 1, (hipStream_t)stream);
+}
+
+extern "C" int nfx_linear_backward_data(const float* gy, const float* w, const float* act, const float* out_scale,
+                                        float* gx, int64_t M, int N, int K, int accumulate, void* stream) {
+    if (M < 0 || K <= 0 || N <= 0) return set_error(NFX_EINVAL, "linear_backward_data: bad shape M=%lld N=%d K=%d", (long long)M, N, K);
+    if (M == 0) return NFX_OK;
+    if (!gy || !w || !gx) return set_error(NFX_EINVAL, "linear_backward_data: null pointer");
+    GemmArgs g{};
+    g.a = gy; g.lda = N;
+    g.b = w; g.ldb = K;
+    g.c = gx; g.ldc = K;
+    g.M = M; g.N = K; g.K = N;
+    g.act = act; g.ldact = K;
+    g.nscale = out_scale;
+    g.accumulate = accumulate;
+    g.kchunk = N;
+    return gemm_launch(g, 0, 0, 1, (hipStream_t)stream);
+}
+
+extern "C" size_t nfx_linear_workspace_bytes(int64_t M, int N, int K) {
+    if (M <= 0 || N <= 0 || K <= 0) return 0;
+    const int64_t s = wgrad_splits(N, K, M);
+    const int64_t cs = (M + 4095) / 4096 < 1024 ? (M + 4095) / 4096 : 1024;
+    const int64_t a = s * (int64_t)N * K, b = (cs < 1 ? 1 : cs) * (int64_t)N;
+    return (size_t)((a > b ? a : b) * sizeof(float));
+}
+
+extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const float* in_scale, float* gw,
+                                          float* gb, int64_t M, int N, int K, void* workspace, void* stream) {
+    if (M < 0 || K <= 0 || N <= 0) return set_error(NFX_EINVAL, "linear_backward_weight: bad shape M=%lld N=%d K=%d", (long long)M, N, K);
+    if (!gw || (M > 0 && (!gy || !x || !workspace))) return set_error(NFX_EINVAL, "linear_backward_weight: null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    float* ws = reinterpret_cast<float*>(workspace);
+    if (M == 0) {
+        (void)hipMemsetAsync(gw, 0, (size_t)N * K * sizeof(float), s);
+        if (gb) (void)hipMemsetAsync(gb, 0, (size_t)N * sizeof(float), s);
+        return check_launch("linear_backward_weight(memset)");
+    }
+    // gw [N][K] = sum_m gy[m][n] x[m][k] s[k]: A(n, m) = gy[m * N + n] (TA = 1), B(m, k) = x[m * K + k]
+    const int64_t splits = wgrad_splits(N, K, M);
+    int64_t kchunk = (M + splits - 1) / splits;
+    kchunk = (kchunk + kGBK - 1) / kGBK * kGBK;
+    const int64_t nz = (M + kchunk - 1) / kchunk;
+    GemmArgs g{};
+    g.a = gy; g.lda = N;
+    g.b = x; g.ldb = K;
+    g.c = ws; g.ldc = K;
+    g.M = N; g.N = K; g.K = M;
+    g.kchunk = kchunk;
+    // x * in_scale applies to B's n index here (the input features): scale after the sum
+    g.nscale = in_scale;
+    int rc = gemm_launch(g, 1, 0, nz, s);
+    if (rc) return rc;
+    const int64_t n = (int64_t)N * K;
+    split_reduce_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, n, gw, 0);
+    rc = check_launch("split_reduce_kernel");
+    if (rc || !gb) return rc;
+    int64_t cs = (M + 4095) / 4096;
+    if (cs > 1024) cs = 1024;
+    if (cs < 1) cs = 1;
+    const int64_t rchunk = (M + cs - 1) / cs;
+    const int64_t ncs = (M + rchunk - 1) / rchunk;
+    colsum_kernel<<<dim3((unsigned)((N + 31) / 32), (unsigned)ncs), 256, 0, s>>>(gy, M, N, rchunk, ws);
+    rc = check_launch("colsum_kernel");
+    if (rc) return rc;
+    split_reduce_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(ws, ncs, N, gb, 0);
+    return check_launch("split_reduce_kernel");
+}
+
+extern "C" int nfx_spline_elem_forward(const float* x, const float* params, const float* mask, float* y,
+                                       float* log_det, int64_t B, int d, int K, float bound, float min_bin_width,
+                                       float min_bin_height, float min_derivative, int direction, int accumulate,
+                                       void* stream) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "spline_elem_forward: bad shape B=%lld d=%d", (long long)B, d);
+    if (K < 2 || K > 11) return set_error(NFX_EUNSUPPORTED, "spline_elem_forward: K=%d outside 2..11", K);
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "spline_elem_forward: direction");
+    if (B == 0) return NFX_OK;
+    if (!x || !params || !mask || !y || !log_det) return set_error(NFX_EINVAL, "spline_elem_forward: null pointer");
+    if (x == y) return set_error(NFX_EINVAL, "spline_elem_forward: x and y must not alias");
+    typedef void (*fk)(const float*, const float*, const float*, float*, float*, int64_t, int, int, const SplineConsts);
+    fk k = (fk)spline_elem_pick<false>(K, direction < 0);
+    const SplineConsts C = spline_consts(K, bound, min_bin_width, min_bin_height, min_derivative);
+    const int64_t blocks = (B + 255) / 256;
+    if (blocks > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "spline_elem_forward: B too large");
+    k<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, params, mask, y, log_det, B, d, accumulate, C);
+    return check_launch("spline_elem_fwd_kernel");
+}
+
+extern "C" int nfx_spline_elem_backward(const float* x, const float* params, const float* mask, const float* gy,
+                                        const float* gld, float* gparams, float* gx, int64_t B, int d, int K,
+                                        float bound, float min_bin_width, float min_bin_height, float min_derivative,
+                                        int direction, void* stream) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "spline_elem_backward: bad shape B=%lld d=%d", (long long)B, d);
+    if (K < 2 || K > 11) return set_error(NFX_EUNSUPPORTED, "spline_elem_backward: K=%d outside 2..11", K);
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "spline_elem_backward: direction");
+    if (B == 0) return NFX_OK;
+    if (!x || !params || !mask || !gparams || !gx) return set_error(NFX_EINVAL, "spline_elem_backward: null pointer");
+    typedef void (*bk)(const float*, const float*, const float*, const float*, const float*, float*, float*, int64_t,
+                       int, const SplineConsts);
+    bk k = (bk)spline_elem_pick<true>(K, direction < 0);
+    const SplineConsts C = spline_consts(K, bound, min_bin_width, min_bin_height, min_derivative);
+    const int64_t blocks = (B + 127) / 128;
+    if (blocks > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "spline_elem_backward: B too large");
+    k<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, params, mask, gy, gld, gparams, gx, B, d, C);
+    return check_launch("spline_elem_bwd_kernel");
+}

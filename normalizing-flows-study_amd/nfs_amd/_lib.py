@@ -50,6 +50,8 @@ EXPORTED_SYMBOLS = (
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob",
     "nfx_flowbn_workspace_bytes", "nfx_flowbn_apply", "nfx_flowbn_moments", "nfx_flowbn_update_running",
     "nfx_flowbn_backward",
+    "nfx_linear_forward", "nfx_linear_backward_data", "nfx_linear_workspace_bytes", "nfx_linear_backward_weight",
+    "nfx_spline_elem_forward", "nfx_spline_elem_backward",
 )
 
 
@@ -91,6 +93,13 @@ _SIGNATURES = {
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_affine_kernel_policy": (_int, [_int]),
+    "nfx_linear_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_linear_backward_data": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_linear_workspace_bytes": (_sz, [_i64, _int, _int]),
+    "nfx_linear_backward_weight": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp, _vp]),
+    "nfx_spline_elem_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int, _int, _vp]),
+    "nfx_spline_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int,
+                                        _vp]),
     "nfx_affine_chain": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,
                                         _int, _vp]),

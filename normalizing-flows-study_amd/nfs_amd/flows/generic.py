@@ -1,0 +1,70 @@
+"""Any-shape path for conditioner MLPs (csrc/nfx_generic.hip).
+
+The fused layer kernels cover bounded shape families (a whole conditioner held in registers and
+LDS). A layer beyond them runs its conditioner one nn.Linear at a time through the gfx950 GEMM
+kernels (`nfx_linear_*`, fp32 MFMA) with HBM-resident activations, plus the layer's element
+kernel. These helpers are the host side of that sequence; every call is a HIP launch.
+"""
+import torch
+
+from .. import _lib
+
+
+def linear_forward(x, lin, in_scale=None, relu=False):
+    """relu?((x * in_scale) @ lin.weight.T + lin.bias) — one nn.Linear (+ ReLU) on MFMA."""
+    M, K = x.shape
+    N = lin.out_features
+    y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    w = lin.weight.detach()
+    b = None if lin.bias is None else lin.bias.detach()
+    _lib.check(_lib.lib().nfx_linear_forward(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(in_scale), _lib.ptr(y),
+                                             M, K, N, int(bool(relu)), _lib.stream_of(x)), "nfx_linear_forward")
+    return y
+
+
+def linear_backward_data(gy, lin, act=None, out_scale=None, out=None):
+    """(gy @ lin.weight) * out_scale, masked where act <= 0 (the ReLU feeding this Linear);
+    added into `out` when given."""
+    M, N = gy.shape
+    K = lin.in_features
+    acc = out is not None
+    if out is None:
+        out = torch.empty(M, K, device=gy.device, dtype=torch.float32)
+    _lib.check(_lib.lib().nfx_linear_backward_data(_lib.ptr(gy), _lib.ptr(lin.weight.detach()), _lib.ptr(act),
+                                                   _lib.ptr(out_scale), _lib.ptr(out), M, N, K, int(acc),
+                                                   _lib.stream_of(gy)), "nfx_linear_backward_data")
+    return out
+
+
+def linear_backward_weight(gy, x, lin, in_scale=None):
+    """(dL/dweight, dL/dbias) of one nn.Linear: gy^T (x * in_scale), column sums of gy."""
+    M, N = gy.shape
+    K = lin.in_features
+    L = _lib.lib()
+    gw = torch.empty(N, K, device=gy.device, dtype=torch.float32)
+    gb = None if lin.bias is None else torch.empty(N, device=gy.device, dtype=torch.float32)
+    ws = torch.empty(max(1, L.nfx_linear_workspace_bytes(M, N, K)), device=gy.device, dtype=torch.uint8)
+    _lib.check(L.nfx_linear_backward_weight(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(in_scale), _lib.ptr(gw),
+                                            _lib.ptr(gb), M, N, K, _lib.ptr(ws), _lib.stream_of(gy)),
+               "nfx_linear_backward_weight")
+    return gw, gb
+
+
+def mlp3_forward(x, l1, l2, l3, in_scale):
+    """Linear -> ReLU -> Linear -> ReLU -> Linear on (x * in_scale): (h1, h2, out)."""
+    h1 = linear_forward(x, l1, in_scale, relu=True)
+    h2 = linear_forward(h1, l2, relu=True)
+    return h1, h2, linear_forward(h2, l3)
+
+
+def mlp3_backward(x, l1, l2, l3, in_scale, h1, h2, g3, gx):
+    """Backward of mlp3_forward given dL/dout = g3: parameter gradients in parameters() order
+    (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias); dL/dx (times in_scale) is
+    added into gx."""
+    gw3, gb3 = linear_backward_weight(g3, h2, l3)
+    g2 = linear_backward_data(g3, l3, act=h2)
+    gw2, gb2 = linear_backward_weight(g2, h1, l2)
+    g1 = linear_backward_data(g2, l2, act=h1)
+    gw1, gb1 = linear_backward_weight(g1, x, l1, in_scale)
+    linear_backward_data(g1, l1, out_scale=in_scale, out=gx)
+    return [gw1, gb1, gw2, gb2, gw3, gb3]

@@ -14,6 +14,7 @@ import torch.nn as nn
 from torch.nn import functional as F
 
 from .. import _lib
+from . import generic as _generic
 from .flow import HipFlow, STATS
 
 MAX_K = 11        # 3K-1 <= 32: one MFMA row tile of spline parameters per transformed dim
@@ -21,6 +22,9 @@ MAX_D = 64        # spline_coupling_kernel (d <= 8) / spline_wide_kernel (d <= 6
 MAX_D_BWD = 8     # fused backward
 MAX_H = 128
 MAX_H_BWD = 64    # fused backward: dW accumulators of <= 2 (H <= 32) / 1 (H <= 64) transformed dims
+# Tests: route every call through the any-shape path (GEMM conditioner + element kernels,
+# csrc/nfx_generic.hip) even where a fused kernel exists, to pin it against the same fixtures.
+FORCE_GENERIC = False
 # (kernel-name, start-event, end-event) of every fused backward while a list is installed here
 # (bench.py roofline timing); None = no events.
 BACKWARD_EVENTS = None
@@ -189,11 +193,60 @@ class SplineCouplingLayer(HipFlow):
         d, H, K = self.data_dim, self._hidden(), self.num_bins
         if x.dim() != 2 or x.shape[1] != d:
             return False, f"input shape {tuple(x.shape)} vs data_dim={d}"
-        if d > MAX_D or H > MAX_H or K > MAX_K or K < 1:
-            return False, f"d={d} (<= {MAX_D}) H={H} (<= {MAX_H}) K={K} (<= {MAX_K})"
-        if self._rescale_scalars() is None:
-            return False, "per-dimension data_min/data_max tensors"
-        return True, ""
+        if self._fused_family():
+            if self._rescale_scalars() is None:
+                return False, "per-dimension data_min/data_max tensors"
+            return True, ""
+        if self._generic_ok():
+            return True, ""
+        return False, (f"d={d} H={H} K={K}: fused kernels need d <= {MAX_D}, H <= {MAX_H}, K <= {MAX_K}; "
+                       f"the any-shape path needs 2 <= K <= {MAX_K} and data_min/data_max None")
+
+    def _fused_family(self):
+        """Shapes of the fused eval kernels (spline_coupling_kernel / spline_wide_kernel)."""
+        return (not FORCE_GENERIC and self.data_dim <= MAX_D and self._hidden() <= MAX_H
+                and 1 <= self.num_bins <= MAX_K)
+
+    def _generic_ok(self):
+        """The any-shape path (csrc/nfx_generic.hip): GEMM conditioner + spline element kernels."""
+        return 2 <= self.num_bins <= MAX_K and (self.data_min is None or self.data_max is None)
+
+    def _mask_dev(self, device):
+        m = self.mask
+        return m.detach().to(device=device, dtype=torch.float32).contiguous()
+
+    def _generic_params(self, x):
+        """Conditioner recompute on the any-shape path: (mask, h1, h2, params [B, d(3K-1)])."""
+        mask = self._mask_dev(x.device)
+        h1, h2, prm = _generic.mlp3_forward(x, self.param_net[0], self.param_net[2], self.param_net[4], mask)
+        return mask, h1, h2, prm
+
+    def _spline_scalars(self):
+        return (float(self.bound), float(self.min_bin_width), float(self.min_bin_height),
+                float(self.min_derivative))
+
+    def _generic_launch(self, x, out, log_det, direction, accumulate):
+        mask, _, _, prm = self._generic_params(x)
+        _lib.check(_lib.lib().nfx_spline_elem_forward(
+            _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(out), _lib.ptr(log_det), x.shape[0],
+            self.data_dim, self.num_bins, *self._spline_scalars(), int(direction), int(bool(accumulate)),
+            _lib.stream_of(x)), "nfx_spline_elem_forward")
+
+    def _generic_backward(self, x, gy, gld, direction):
+        """dL/dx and parameter gradients on the any-shape path: conditioner recompute (GEMMs),
+        the spline adjoint per element (nfx_spline_elem_backward), then the conditioner's
+        backward GEMMs (data gradient into dL/dx, weight gradients split over the batch)."""
+        B, d = x.shape
+        mask, h1, h2, prm = self._generic_params(x)
+        gprm = torch.empty_like(prm)
+        gx = torch.empty_like(x)
+        _lib.check(_lib.lib().nfx_spline_elem_backward(
+            _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(gy), _lib.ptr(gld), _lib.ptr(gprm), _lib.ptr(gx),
+            B, d, self.num_bins, *self._spline_scalars(), int(direction), _lib.stream_of(x)),
+            "nfx_spline_elem_backward")
+        grads = _generic.mlp3_backward(x, self.param_net[0], self.param_net[2], self.param_net[4], mask, h1, h2,
+                                       gprm, gx)
+        return gx, grads
 
     def _build_pack(self, device):
         d, H, K = self.data_dim, self._hidden(), self.num_bins
@@ -208,11 +261,16 @@ class SplineCouplingLayer(HipFlow):
 
     # -- fused backward (training) ---------------------------------------
     def _hip_backward_ok(self, x, direction):
+        return x.dtype == torch.float32 and (self._fused_backward_ok() or self._generic_ok())
+
+    def _fused_backward_ok(self):
+        """Shapes of the fused backward kernel (spline_bwd_kernel); others take the any-shape
+        path (_generic_backward)."""
         d, H, K = self.data_dim, self._hidden(), self.num_bins
         nt = self._n_transformed()
         ntmax = 2 if H <= 32 else 1
-        return (x.dtype == torch.float32 and d <= MAX_D_BWD and H <= MAX_H_BWD and 2 <= K <= MAX_K
-                and nt <= ntmax and (self.data_min is None or self.data_max is None))
+        return (not FORCE_GENERIC and d <= MAX_D_BWD and H <= MAX_H_BWD and 2 <= K <= MAX_K and nt <= ntmax
+                and (self.data_min is None or self.data_max is None))
 
     def _n_transformed(self):
         """Number of transformed (mask == 0) dimensions, cached per mask version (no sync)."""
@@ -244,6 +302,8 @@ class SplineCouplingLayer(HipFlow):
         H, K = self._hidden(), self.num_bins
         gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
         gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
+        if not self._fused_backward_ok():
+            return self._generic_backward(x, gy, gld, direction)
         packed, mask = self._packed(x.device, self._build_bwd_pack, slot="_nfx_bwd_pack_cache")
         L = _lib.lib()
         gx = torch.empty_like(x)
@@ -271,6 +331,8 @@ class SplineCouplingLayer(HipFlow):
         return gx, out
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
+        if not self._fused_family():
+            return self._generic_launch(x, out, log_det, direction, accumulate)
         packed = self._packed(x.device, self._build_pack)
         rescale, lo, hi = self._rescale_scalars()
         _lib.check(_lib.lib().nfx_spline_coupling(
@@ -281,6 +343,8 @@ class SplineCouplingLayer(HipFlow):
             "nfx_spline_coupling")
 
     def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
+        if not self._fused_family():
+            return False
         packed = self._packed(x.device, self._build_pack)
         rescale, lo, hi = self._rescale_scalars()
         _lib.check(_lib.lib().nfx_spline_coupling_logprob(

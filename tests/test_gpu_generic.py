@@ -1,0 +1,221 @@
+"""GPU: the any-shape path (csrc/nfx_generic.hip) — nn.Linear on fp32 MFMA and the spline
+coupling's element kernels, for layers beyond the fused kernel families.
+
+* nfx_linear_*: forward (x * scale) W^T + b (+ ReLU), data gradient (masked by the ReLU feeding
+  the layer, times a scale, accumulated) and weight/bias gradients (split over the batch, fixed
+  order) against float64 torch on the same inputs. Tolerance: an fp32 dot product of length n
+  carries at most ~n ulp of sum |a_i b_i|; checked as |C - C64| <= 1e-5 (|A||B|) + 1e-30 per
+  element (|A||B| = the absolute-value product, the conditioning of each entry).
+* SplineCouplingLayer on the any-shape path — eval beyond the fused eval family (H = 256,
+  d = 80) against the CPU oracle with the fp32 parity model of conftest; gradients beyond the
+  fused backward family (H = 128, several transformed dims at H = 64, d = 12) against float64
+  autograd with the error model of test_gpu_spline_backward.py; and forced onto the fused shapes
+  (spline.FORCE_GENERIC) against the reference's own gradients (G14) and the fused kernels.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import nfs_amd
+import oracle
+from conftest import assert_fp32_parity, fp32_jitter, load_golden, oracle_sd, state_dict_from
+from nfs_amd.flows import generic as G
+from nfs_amd.flows import spline as _sp
+from nfs_amd.flows.flow import STATS
+from test_gpu_spline_backward import _check, _grads, _ill_rows_checked, _layer
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(c, c64, conditioning, what):
+    c = c.double().cpu()
+    err = (c - c64).abs()
+    bound = 1e-5 * conditioning + 1e-30
+    worst = (err - bound).max().item()
+    assert worst <= 0, f"{what}: max excess {worst:.3g} (max err {err.max().item():.3g})"
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 2, 64), (4097, 64, 64), (300, 128, 232), (70001, 128, 128),
+                                   (5, 3, 1), (1, 96, 33), (2048, 784, 64)])
+def test_linear_kernels_vs_float64(cuda_device, M, K, N):
+    g = torch.Generator().manual_seed(M + K + N)
+    lin = nn.Linear(K, N)
+    x = torch.randn(M, K, generator=g)
+    s = (torch.rand(K, generator=g) > 0.3).float()
+    gy = torch.randn(M, N, generator=g)
+    act = torch.relu(torch.randn(M, K, generator=g))
+    base = torch.randn(M, K, generator=g)
+    w64, b64, x64, s64 = lin.weight.double(), lin.bias.double(), x.double(), s.double()
+    linc = copy.deepcopy(lin).to(cuda_device)
+    dx, ds, dgy, dact = (t.to(cuda_device) for t in (x, s, gy, act))
+    # forward, with and without the ReLU and the input scale
+    for relu, scale in ((False, None), (True, ds)):
+        y = G.linear_forward(dx, linc, scale, relu=relu)
+        xs = x64 * s64 if scale is not None else x64
+        y64 = xs @ w64.T + b64
+        if relu:
+            y64 = torch.relu(y64)
+        _close(y, y64, xs.abs() @ w64.abs().T + b64.abs(), f"forward relu={relu}")
+    # data gradient: masked by act > 0, times s, accumulated into `base`
+    out = base.to(cuda_device).clone()
+    G.linear_backward_data(dgy, linc, act=dact, out_scale=ds, out=out)
+    gx64 = base.double() + torch.where(act.double() > 0, (gy.double() @ w64) * s64, torch.zeros(()))
+    _close(out, gx64, base.double().abs() + (gy.double().abs() @ w64.abs()), "backward data")
+    gx = G.linear_backward_data(dgy, linc)
+    _close(gx, gy.double() @ w64, gy.double().abs() @ w64.abs(), "backward data (plain)")
+    # weight and bias gradients (input scaled by s)
+    gw, gb = G.linear_backward_weight(dgy, dx, linc, ds)
+    xs = x64 * s64
+    _close(gw, gy.double().T @ xs, gy.double().abs().T @ xs.abs(), "weight grad")
+    _close(gb, gy.double().sum(0), gy.double().abs().sum(0), "bias grad")
+
+
+def test_linear_weight_grad_deterministic(cuda_device):
+    """Split-K partials are summed in a fixed order: bitwise identical on repeat."""
+    lin = nn.Linear(128, 128).to(cuda_device)
+    x = torch.randn(300000, 128, device=cuda_device)
+    gy = torch.randn(300000, 128, device=cuda_device)
+    a = G.linear_backward_weight(gy, x, lin)
+    b = G.linear_backward_weight(gy, x, lin)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def sd64(sd):
+    return {k: v.double() for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("d,H,K,mask", [(2, 256, 8, [1, 0]), (4, 320, 5, [0, 1, 0, 1]),
+                                        (80, 32, 4, [(i % 3 == 0) * 1.0 for i in range(80)])])
+def test_generic_spline_eval_vs_oracle(cuda_device, d, H, K, mask):
+    """Eval beyond the fused eval family (H > 128 or d > 64) runs the any-shape path."""
+    torch.manual_seed(d * 100 + H + K)
+    layer = nfs_amd.SplineCouplingLayer(d, H, torch.tensor(mask, dtype=torch.float32), num_bins=K)
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(0.1 * torch.randn_like(p))
+    x = torch.randn(1000, d) * 2.5
+    x[0, 0] = float("nan")
+    sd = {k: v.clone() for k, v in layer.state_dict().items()}
+    layer = layer.to(cuda_device).eval()
+    assert not layer._fused_family()
+    for direction in (1, -1):
+        STATS["hip"] = STATS["torch"] = 0
+        with torch.no_grad():
+            yg, lg = (layer.forward if direction > 0 else layer.inverse)(x.to(cuda_device))
+        assert STATS["hip"] == 1 and STATS["torch"] == 0, STATS
+        with torch.no_grad():
+            yr, lr = oracle.spline_coupling(sd, "", x, direction, K=K)
+            y64, l64 = oracle.spline_coupling(sd64(sd), "", x.double(), direction, K=K)
+        sy, sl = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, direction, K=K), x, sd=sd, k=4,
+                             n_perm=4, n_wjit=4)
+        assert_fp32_parity(yg.cpu(), yr, y64, what=f"y dir={direction}", sens=sy)
+        assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}", sens=sl)
+
+
+GRAD_CASES = [
+    # d, H, K, mask, B — all beyond the fused backward (H > 64, or > 1 transformed dim at H = 64,
+    # or d > 8)
+    (2, 128, 10, [1, 0], 4096),        # RealNVPSpline(2, *, 128)
+    (4, 64, 8, [1, 0, 1, 0], 2000),    # two transformed dims at H = 64
+    (3, 128, 5, [0, 1, 0], 777),
+    (12, 48, 4, [(i % 2) * 1.0 for i in range(12)], 513),
+    (2, 256, 8, [0, 1], 300),
+]
+
+
+@pytest.mark.parametrize("direction", [1, -1])
+@pytest.mark.parametrize("d,H,K,mask,B", GRAD_CASES)
+def test_generic_spline_backward_vs_float64_autograd(cuda_device, d, H, K, mask, B, direction):
+    f = _layer(d, H, K, mask, d * 1000 + H * 10 + K, scale=0.1)
+    assert not f._fused_backward_ok()
+    f64 = copy.deepcopy(f).double()
+    g = torch.Generator().manual_seed(B + K)
+    x = 2.0 * torch.randn(B, d, generator=g)
+    if B >= 8:
+        x[:4] *= 4.0
+    gy = torch.randn(B, d, generator=g)
+    gld = torch.randn(B, generator=g)
+    fg = copy.deepcopy(f).to(cuda_device)
+    ill = _ill_rows_checked(f, f64, fg, x, gy, gld, direction, cuda_device)
+    gy[ill] = 0.0
+    gld[ill] = 0.0
+    gx64, gp64, _, _ = _grads(f64, x.double(), gy.double(), gld.double(), direction)
+    gx32, gp32, _, _ = _grads(f, x, gy, gld, direction)
+    STATS["hip"] = STATS["torch"] = 0
+    gx, gp, _, _ = _grads(fg, x.to(cuda_device), gy.to(cuda_device), gld.to(cuda_device), direction)
+    assert STATS["hip"] == 2 and STATS["torch"] == 0, STATS  # HIP forward + HIP backward
+    _check(gx, gx32, gx64, "dL/dx")
+    for (n, _), a, b, c in zip(f.named_parameters(), gp, gp32, gp64):
+        _check(a, b, c, n)
+
+
+@pytest.fixture
+def force_generic():
+    old = _sp.FORCE_GENERIC
+    _sp.FORCE_GENERIC = True
+    yield
+    _sp.FORCE_GENERIC = old
+
+
+@pytest.mark.parametrize("name", ["sp8", "sp10"])
+@pytest.mark.parametrize("dname", ["inv", "fwd"])
+def test_generic_spline_vs_reference_gradients_g14(cuda_device, force_generic, name, dname):
+    """The any-shape path forced onto G14's layers: the reference's own fp32 gradients."""
+    from test_gpu_grad_fixtures import _g14_module, _grad_close, _run
+    g = load_golden("g14_grads.npz")
+    m = _g14_module(name)
+    m.load_state_dict(state_dict_from(g, name + ".init.", m))
+    m.eval()
+    m64 = copy.deepcopy(m).double()
+    x, wy, wl = (torch.from_numpy(g[f"{name}.{k}"]) for k in ("x", "wy", "wl"))
+    _, _, gx64, gp64 = _run(m64, x.double(), wy.double(), wl.double(), dname)
+    mg = m.to(cuda_device)
+    STATS["hip"] = STATS["torch"] = 0
+    y, ld, gx, gp = _run(mg, x.to(cuda_device), wy.to(cuda_device), wl.to(cuda_device), dname)
+    assert STATS["torch"] == 0 and STATS["hip"] == 2, STATS
+    K = 8 if name == "sp8" else 10
+    sd = oracle_sd(g, name + ".init.")
+    direction = -1 if dname == "inv" else 1
+    with torch.no_grad():
+        y64, l64 = oracle.spline_coupling(sd64(sd), "", x.double(), direction, K=K)
+    ens = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, direction, K=K), x, sd=sd)
+    assert_fp32_parity(y.cpu(), g[f"{name}.{dname}.y"], y64, what=f"{name} {dname} y", sens=ens[0])
+    assert_fp32_parity(ld.cpu(), g[f"{name}.{dname}.ld"], l64, what=f"{name} {dname} ld", sens=ens[1])
+    _grad_close(gx, g[f"{name}.{dname}.gx"], gx64, "dL/dx")
+    for k in gp64:
+        _grad_close(gp[k], g[f"{name}.{dname}.grad.{k}"], gp64[k], k)
+
+
+def test_realnvp_spline_h128_training_step(cuda_device):
+    """loss = -log_prob(x).mean(); backward through RealNVPSpline(2, 6, 128) (K = 10): every
+    layer's forward and backward on HIP (fused eval kernel forward, any-shape backward), loss
+    and gradients vs the float64 model."""
+    from test_gpu_spline_backward import _ill_rows, _model_grads
+    torch.manual_seed(5)
+    model = nfs_amd.RealNVPSpline(2, 6, 128)
+    g = torch.Generator().manual_seed(6)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(0.1 * torch.randn(p.shape, generator=g))
+    ref64 = copy.deepcopy(model).double()
+    ref32 = copy.deepcopy(model)
+    data = torch.randn(2000, 2, generator=g) * torch.tensor([1.5, 0.7])
+    model = model.to(cuda_device).train()
+    w = torch.ones(2000)
+    loss64, gx64, _ = _model_grads(ref64, data.double(), w.double())
+    _, gx32, _ = _model_grads(ref32, data, w)
+    STATS["hip"] = STATS["torch"] = 0
+    loss, gx, _ = _model_grads(model, data.to(cuda_device), w.to(cuda_device))
+    assert STATS["torch"] == 0 and STATS["hip"] >= 12, STATS
+    assert abs(loss.item() - loss64.item()) <= 1e-5 * (1 + abs(loss64.item()))
+    ill = _ill_rows(gx, gx32, gx64, data.shape[0])
+    w[ill] = 0.0
+    _, gx64, gp64 = _model_grads(ref64, data.double(), w.double())
+    _, gx32, gp32 = _model_grads(ref32, data, w)
+    _, gx, gp = _model_grads(model, data.to(cuda_device), w.to(cuda_device))
+    _check(gx, gx32, gx64, "dL/dx")
+    for (n, _), a, b, c in zip(model.named_parameters(), gp, gp32, gp64):
+        _check(a, b, c, n)
