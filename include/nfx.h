@@ -380,22 +380,43 @@ int nfx_flowbn_backward(const float* in, const float* grad_out, const float* gra
  * the fused kernel families, one nn.Linear at a time on fp32 MFMA, plus the spline coupling's
  * element math. Row-major fp32 device buffers; w is an nn.Linear weight [N][K] (out x in).
  * ------------------------------------------------------------------------------------- */
-/* y[M][N] = act((x[M][K] o in_scale[K]) w^T + b): one nn.Linear (+ ReLU when relu = 1);
- * in_scale (e.g. the coupling mask: Linear(x * mask)) and b may be NULL. Replaces
- * torch.nn.functional.linear (+ relu) inside the reference's conditioner nn.Sequential. */
-int nfx_linear_forward(const float* x, const float* w, const float* b, const float* in_scale, float* y,
-                       int64_t M, int K, int N, int relu, void* stream);
-/* gx[M][K] (+)= ((gy[M][N] w) o out_scale[K]), kept only where act[M][K] > 0 when act is given
- * (the ReLU backward of the layer feeding this Linear): autograd's input gradient of
+/* y[M][N] = act(((x[M][K] o in_scale[K]) (w o wmask)^T + b) o post_scale + post_shift): one
+ * nn.Linear / MaskedLinear (wmask: its 0/1 mask, weight * mask as masked_linear.py:17) with an
+ * optional per-feature affine after it (an eval-mode BatchNorm1d: post_scale = gamma/sqrt(rv+eps),
+ * post_shift = beta - rm * post_scale) and ReLU when relu = 1. in_scale (e.g. the coupling mask:
+ * Linear(x * mask)), wmask, b and the post affine may be NULL. Replaces the reference's
+ * conditioner nn.Sequential one Linear (+ BatchNorm + ReLU) at a time. */
+int nfx_linear_forward(const float* x, const float* w, const float* wmask, const float* b, const float* in_scale,
+                       const float* post_scale, const float* post_shift, float* y, int64_t M, int K, int N,
+                       int relu, void* stream);
+/* gx[M][K] (+)= ((gy[M][N] (w o wmask)) o out_scale[K]), kept only where act[M][K] > 0 when act
+ * is given (the ReLU backward of the layer feeding this Linear): autograd's input gradient of
  * nn.Linear. accumulate = 1 adds into gx. */
-int nfx_linear_backward_data(const float* gy, const float* w, const float* act, const float* out_scale,
-                             float* gx, int64_t M, int N, int K, int accumulate, void* stream);
-/* gw[N][K] = gy^T (x o in_scale), gb[N] = sum over rows of gy (gb may be NULL): autograd's
- * weight and bias gradients of nn.Linear, split over the batch into a workspace of
- * nfx_linear_workspace_bytes(M, N, K) bytes and summed in a fixed order (deterministic). */
+int nfx_linear_backward_data(const float* gy, const float* w, const float* wmask, const float* act,
+                             const float* out_scale, float* gx, int64_t M, int N, int K, int accumulate, void* stream);
+/* gw[N][K] = (gy^T (x o in_scale)) o wmask, gb[N] = sum over rows of gy (gb may be NULL):
+ * autograd's weight and bias gradients of nn.Linear / MaskedLinear, split over the batch into a
+ * workspace of nfx_linear_workspace_bytes(M, N, K) bytes and summed in a fixed order. */
 size_t nfx_linear_workspace_bytes(int64_t M, int N, int K);
-int nfx_linear_backward_weight(const float* gy, const float* x, const float* in_scale, float* gw, float* gb,
-                               int64_t M, int N, int K, void* workspace, void* stream);
+int nfx_linear_backward_weight(const float* gy, const float* x, const float* in_scale, const float* wmask, float* gw,
+                               float* gb, int64_t M, int N, int K, void* workspace, void* stream);
+/* MADE affine flows' element math for any (d, H) (the conditioner output params [B][2d] =
+ * [mu | alpha] from nfx_linear_*): nfx_made_elem_forward — the parallel directions
+ * (NFX_MAF_INVERSE: masked_autoregressive_flow.py:18-44, NFX_IAF_FORWARD:
+ * inverse_autoregressive_flow.py:30-63) incl. guards and log-det clamp; nfx_made_elem_step —
+ * step i of a sequential direction (NFX_MAF_FORWARD :46-78, NFX_IAF_INVERSE :65-103) on the
+ * running vector `work` [B][d] (zeros at i = 0) and log-det `work_ld` [B] (zeros), then
+ * nfx_made_elem_finish — the final guards and clamp into y / log_det (written or accumulated);
+ * nfx_made_elem_backward — the adjoint of the parallel element map: gparams [B][2d] =
+ * (dL/dmu, dL/dalpha) and gx the direct dL/dx term (gy / gld may be NULL). */
+int nfx_made_elem_forward(const float* x, const float* params, float* y, float* log_det, int64_t B, int d,
+                          int variant, int accumulate, void* stream);
+int nfx_made_elem_step(const float* x, const float* params, float* work, float* work_ld, int64_t B, int d, int i,
+                       int variant, void* stream);
+int nfx_made_elem_finish(const float* x, const float* work, const float* work_ld, float* y, float* log_det,
+                         int64_t B, int d, int variant, int accumulate, void* stream);
+int nfx_made_elem_backward(const float* x, const float* params, const float* gy, const float* gld, float* gparams,
+                           float* gx, int64_t B, int d, int variant, void* stream);
 /* SplineCouplingLayer element math for any d (spline_coupling_layer.py:96-180 with the spline
  * of :182-309): params [B][d][3K-1] = param_net output; dims with mask == 0 go through the RQ
  * spline (forward: direction +1, inverse: -1), the rest pass through; layer guards and the

@@ -34,7 +34,10 @@ struct GemmArgs {
     float* c;                // C(m, n) = c[m * ldc + n] (+ z * M * N for split-K partials)
     int64_t M, N, K, lda, ldb, ldc;
     const float* kscale;     // optional, length K: A(m, k) *= kscale[k]   (x * mask inputs)
+    const float* bmask;      // optional, indexed like b: B(k, n) *= bmask (MaskedLinear weight * mask)
     const float* bias;       // optional, length N
+    const float* pscale;     // optional, length N: C = C * pscale[n] + pshift[n] after the bias
+    const float* pshift;     //   (an eval-mode BatchNorm1d folded per output feature)
     const float* act;        // optional [M][ldact]: keep C(m, n) where act(m, n) > 0 (ReLU backward)
     int64_t ldact;
     const float* nscale;     // optional, length N: C(m, n) *= nscale[n]
@@ -70,7 +73,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
             if (TB == 0) { kj = idx >> 6; ni = idx & 63; } else { ni = idx >> 5; kj = idx & 31; }
             const int64_t n = n0 + ni, k2 = k0 + kj;
             float w = 0.f;
-            if (n < g.N && k2 < ke) w = TB == 0 ? g.b[k2 * g.ldb + n] : g.b[n * g.ldb + k2];
+            if (n < g.N && k2 < ke) {
+                const int64_t o = TB == 0 ? k2 * g.ldb + n : n * g.ldb + k2;
+                w = g.b[o];
+                if (g.bmask) w *= g.bmask[o];
+            }
             rb[e] = w;
         }
     };
@@ -100,6 +107,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         if (m < g.M && n < g.N) {
             float v = acc[r];
             if (g.bias) v += g.bias[n];
+            if (g.pscale) v = v * g.pscale[n] + g.pshift[n];
             if (g.relu) v = trelu(v);
             if (g.act) v = g.act[m * g.ldact + n] > 0.f ? v : 0.f;
             if (g.nscale) v *= g.nscale[n];
@@ -124,12 +132,13 @@ static int gemm_launch(const GemmArgs& g, int ta, int tb, int64_t splits, hipStr
     return check_launch("gemm_kernel");
 }
 
-// out[i] (+)= sum_z part[z * n + i], z = 0 .. nz-1 in order
+// out[i] (+)= (sum_z part[z * n + i], z = 0 .. nz-1 in order) * mask[i] (mask optional)
 __global__ void split_reduce_kernel(const float* __restrict__ part, int64_t nz, int64_t n, float* __restrict__ out,
-                                    int accumulate) {
+                                    int accumulate, const float* __restrict__ mask) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         float v = 0.f;
         for (int64_t z = 0; z < nz; ++z) v += part[z * n + i];
+        if (mask) v *= mask[i];
         out[i] = accumulate ? out[i] + v : v;
     }
 }
@@ -269,11 +278,133 @@ static const void* spline_elem_pick(int K, bool inv) {
     return nullptr;
 }
 
+// ---- MADE affine flows, element math -----------------------------------------------------
+// params [B][2d] = the MADE output, mu = params[:, :d], alpha = params[:, d:] (chunk(2, dim=1)).
+// Parallel directions (one thread per sample, dims in order, log-det summed in dim order):
+//   MAF inverse  masked_autoregressive_flow.py:18-44   z = (x - mu) exp(clamp(-clamp(a,-3,3),-5,5))
+//   IAF forward  inverse_autoregressive_flow.py:30-63  y = x exp(clamp(clamp(a,-2,2),-3,3)) + clamp(mu,-10,10)
+__global__ __launch_bounds__(256) void made_elem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ prm,
+                                                            float* __restrict__ y, float* __restrict__ log_det,
+                                                            int64_t B, int d, int variant, int accumulate) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const float* mu = prm + s * 2 * d;
+    const float* al = mu + d;
+    float ld = 0.f;
+    if (variant == NFX_MAF_INVERSE) {
+        for (int j = 0; j < d; ++j) {
+            const float a = tclamp(al[j], -3.f, 3.f);
+            const float z = (x[s * d + j] - mu[j]) * exp_fast(tclamp(-a, -5.f, 5.f));
+            y[s * d + j] = nonfinite(z) ? 0.f : z;
+            ld = ld + a;
+        }
+        ld = -ld;
+        ld = nonfinite(ld) ? 0.f : tclamp(ld, -100.f, 100.f);
+    } else {
+        for (int j = 0; j < d; ++j) {
+            const float a = tclamp(al[j], -2.f, 2.f);
+            const float xv = x[s * d + j];
+            const float v = xv * exp_fast(tclamp(a, -3.f, 3.f)) + tclamp(mu[j], -10.f, 10.f);
+            y[s * d + j] = nonfinite(v) ? xv : v;
+            ld = ld + a;
+        }
+        ld = nonfinite(ld) ? 0.f : tclamp(ld, -50.f, 50.f);
+    }
+    log_det[s] = accumulate ? log_det[s] + ld : ld;
+}
+
+// One step i of a sequential direction on the running vector w [B][d] (the conditioner input of
+// the next step) and the running log-det ld [B] (starts at 0):
+//   MAF forward  masked_autoregressive_flow.py:55-74   w_i = x_i exp(clamp(a_i,-5,5)) + mu_i, ld += a_i
+//   IAF inverse  inverse_autoregressive_flow.py:80-99  w_i = (x_i - clamp(mu_i,-10,10)) exp(clamp(-a_i,-3,3)), ld -= a_i
+__global__ __launch_bounds__(256) void made_elem_step_kernel(const float* __restrict__ x, const float* __restrict__ prm,
+                                                             float* __restrict__ w, float* __restrict__ ld, int64_t B,
+                                                             int d, int i, int variant) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const float mu = prm[s * 2 * d + i], al = prm[s * 2 * d + d + i], xv = x[s * d + i];
+    if (variant == NFX_MAF_FORWARD) {
+        const float a = tclamp(al, -3.f, 3.f);
+        w[s * d + i] = xv * exp_fast(tclamp(a, -5.f, 5.f)) + mu;
+        ld[s] = ld[s] + a;
+    } else {
+        const float a = tclamp(al, -2.f, 2.f);
+        w[s * d + i] = (xv - tclamp(mu, -10.f, 10.f)) * exp_fast(tclamp(-a, -3.f, 3.f));
+        ld[s] = ld[s] - a;
+    }
+}
+
+// The sequential directions' final guards (:75-77 / :100-102), then write or accumulate the log-det.
+__global__ __launch_bounds__(256) void made_elem_finish_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ ldw, float* __restrict__ y,
+                                                               float* __restrict__ log_det, int64_t B, int d, int variant,
+                                                               int accumulate) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const bool maf = variant == NFX_MAF_FORWARD;
+    for (int j = 0; j < d; ++j) {
+        const float v = w[s * d + j];
+        y[s * d + j] = nonfinite(v) ? (maf ? 0.f : x[s * d + j]) : v;
+    }
+    float ld = ldw[s];
+    ld = nonfinite(ld) ? 0.f : (maf ? tclamp(ld, -100.f, 100.f) : tclamp(ld, -50.f, 50.f));
+    log_det[s] = accumulate ? log_det[s] + ld : ld;
+}
+
+// Adjoint of made_elem_fwd_kernel (autograd of the reference's ops, guards and clamps included):
+// gprm [B][2d] = (dL/dmu, dL/dalpha), gx [B][d] = the direct dL/dx term.
+__global__ __launch_bounds__(256) void made_elem_bwd_kernel(const float* __restrict__ x, const float* __restrict__ prm,
+                                                            const float* __restrict__ gy, const float* __restrict__ gld,
+                                                            float* __restrict__ gprm, float* __restrict__ gx, int64_t B,
+                                                            int d, int variant) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const float* mu = prm + s * 2 * d;
+    const float* al = mu + d;
+    float* gmu = gprm + s * 2 * d;
+    float* gal = gmu + d;
+    const bool maf = variant == NFX_MAF_INVERSE;
+    const float lo = maf ? -3.f : -2.f, hi = maf ? 3.f : 2.f, lim = maf ? 100.f : 50.f;
+    float asum = 0.f;
+    for (int j = 0; j < d; ++j) asum = asum + tclamp(al[j], lo, hi);
+    const float ldraw = maf ? -asum : asum;
+    const float ld1 = nonfinite(ldraw) ? 0.f : ldraw;
+    const float g0 = gld ? gld[s] : 0.f;
+    const float gl = (nonfinite(ldraw) || !(ld1 >= -lim && ld1 <= lim)) ? 0.f : g0;
+    for (int j = 0; j < d; ++j) {
+        const float xv = x[s * d + j], alpha = al[j], m = mu[j];
+        const float g = gy ? gy[s * d + j] : 0.f;
+        const float a = tclamp(alpha, lo, hi);
+        const bool ain = alpha >= lo && alpha <= hi;
+        if (maf) {
+            const float e = exp_fast(tclamp(-a, -5.f, 5.f));
+            const float xm = xv - m;
+            const float gz = nonfinite(xm * e) ? 0.f : g;
+            const float ge = gz * e;
+            gx[s * d + j] = ge;
+            gmu[j] = -ge;
+            gal[j] = ain ? -(gz * xm * e) - gl : 0.f;
+        } else {
+            const float e = exp_fast(tclamp(a, -3.f, 3.f));
+            const float yr = xv * e + tclamp(m, -10.f, 10.f);
+            const bool bad = nonfinite(yr);
+            const float gyr = bad ? 0.f : g;
+            gx[s * d + j] = bad ? g : gyr * e;
+            gmu[j] = (m >= -10.f && m <= 10.f) ? gyr : 0.f;
+            gal[j] = ain ? gyr * xv * e + gl : 0.f;
+        }
+    }
+}
+
 }  // namespace nfx
 
 using namespace nfx;
 
-extern "C" int nfx_linear_forward(const float* x, const float* w, const float* b, const float* in_scale, float* y,
+extern "C" int nfx_linear_forward(const float* x, const float* w, const float* wmask, const float* b,
+                                  const float* in_scale, const float* post_scale, const float* post_shift, float* y,
                                   int64_t M, int K, int N, int relu, void* stream) {
     if (M < 0 || K <= 0 || N <= 0) return set_error(NFX_EINVAL, "linear_forward: bad shape M=%lld K=%d N=%d", (long long)M, K, N);
     if (M == 0) return NFX_OK;
@@ -284,20 +415,27 @@ extern "C" int nfx_linear_forward(const float* x, const float* w, const float* b
     g.c = y; g.ldc = N;
     g.M = M; g.N = N; g.K = K;
     g.kscale = in_scale;
+    g.bmask = wmask;
     g.bias = b;
+    if ((post_scale == nullptr) != (post_shift == nullptr))
+        return set_error(NFX_EINVAL, "linear_forward: post_scale and post_shift go together");
+    g.pscale = post_scale;
+    g.pshift = post_shift;
     g.relu = relu;
     g.kchunk = K;
     return gemm_launch(g, 0, 1, 1, (hipStream_t)stream);
 }
 
-extern "C" int nfx_linear_backward_data(const float* gy, const float* w, const float* act, const float* out_scale,
-                                        float* gx, int64_t M, int N, int K, int accumulate, void* stream) {
+extern "C" int nfx_linear_backward_data(const float* gy, const float* w, const float* wmask, const float* act,
+                                        const float* out_scale, float* gx, int64_t M, int N, int K, int accumulate,
+                                        void* stream) {
     if (M < 0 || K <= 0 || N <= 0) return set_error(NFX_EINVAL, "linear_backward_data: bad shape M=%lld N=%d K=%d", (long long)M, N, K);
     if (M == 0) return NFX_OK;
     if (!gy || !w || !gx) return set_error(NFX_EINVAL, "linear_backward_data: null pointer");
     GemmArgs g{};
     g.a = gy; g.lda = N;
     g.b = w; g.ldb = K;
+    g.bmask = wmask;
     g.c = gx; g.ldc = K;
     g.M = M; g.N = K; g.K = N;
     g.act = act; g.ldact = K;
@@ -315,13 +453,15 @@ extern "C" size_t nfx_linear_workspace_bytes(int64_t M, int N, int K) {
     return (size_t)((a > b ? a : b) * sizeof(float));
 }
 
-extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const float* in_scale, float* gw,
-                                          float* gb, int64_t M, int N, int K, void* workspace, void* stream) {
+extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const float* in_scale, const float* wmask,
+                                          float* gw, float* gb, int64_t M, int N, int K, void* workspace,
+                                          void* stream) {
     if (M < 0 || K <= 0 || N <= 0) return set_error(NFX_EINVAL, "linear_backward_weight: bad shape M=%lld N=%d K=%d", (long long)M, N, K);
     if (!gw || (M > 0 && (!gy || !x || !workspace))) return set_error(NFX_EINVAL, "linear_backward_weight: null pointer");
     hipStream_t s = (hipStream_t)stream;
     float* ws = reinterpret_cast<float*>(workspace);
     if (M == 0) {
+        (void)wmask;
         (void)hipMemsetAsync(gw, 0, (size_t)N * K * sizeof(float), s);
         if (gb) (void)hipMemsetAsync(gb, 0, (size_t)N * sizeof(float), s);
         return check_launch("linear_backward_weight(memset)");
@@ -342,7 +482,7 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
     int rc = gemm_launch(g, 1, 0, nz, s);
     if (rc) return rc;
     const int64_t n = (int64_t)N * K;
-    split_reduce_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, n, gw, 0);
+    split_reduce_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, n, gw, 0, wmask);
     rc = check_launch("split_reduce_kernel");
     if (rc || !gb) return rc;
     int64_t cs = (M + 4095) / 4096;
@@ -353,7 +493,7 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
     colsum_kernel<<<dim3((unsigned)((N + 31) / 32), (unsigned)ncs), 256, 0, s>>>(gy, M, N, rchunk, ws);
     rc = check_launch("colsum_kernel");
     if (rc) return rc;
-    split_reduce_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(ws, ncs, N, gb, 0);
+    split_reduce_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(ws, ncs, N, gb, 0, nullptr);
     return check_launch("split_reduce_kernel");
 }
 
@@ -393,4 +533,63 @@ extern "C" int nfx_spline_elem_backward(const float* x, const float* params, con
     if (blocks > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "spline_elem_backward: B too large");
     k<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, params, mask, gy, gld, gparams, gx, B, d, C);
     return check_launch("spline_elem_bwd_kernel");
+}
+
+static int made_elem_check(int64_t B, int d, const char* what) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "%s: bad shape B=%lld d=%d", what, (long long)B, d);
+    if ((B + 255) / 256 > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "%s: B too large", what);
+    return NFX_OK;
+}
+
+extern "C" int nfx_made_elem_forward(const float* x, const float* params, float* y, float* log_det, int64_t B, int d,
+                                     int variant, int accumulate, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_forward");
+    if (rc) return rc;
+    if (variant != NFX_MAF_INVERSE && variant != NFX_IAF_FORWARD)
+        return set_error(NFX_EINVAL, "made_elem_forward: parallel variants only (MAF inverse / IAF forward)");
+    if (B == 0) return NFX_OK;
+    if (!x || !params || !y || !log_det) return set_error(NFX_EINVAL, "made_elem_forward: null pointer");
+    made_elem_fwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, y, log_det, B, d,
+                                                                                      variant, accumulate);
+    return check_launch("made_elem_fwd_kernel");
+}
+
+extern "C" int nfx_made_elem_step(const float* x, const float* params, float* work, float* work_ld, int64_t B, int d,
+                                  int i, int variant, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_step");
+    if (rc) return rc;
+    if (variant != NFX_MAF_FORWARD && variant != NFX_IAF_INVERSE)
+        return set_error(NFX_EINVAL, "made_elem_step: sequential variants only (MAF forward / IAF inverse)");
+    if (i < 0 || i >= d) return set_error(NFX_EINVAL, "made_elem_step: step %d outside 0..%d", i, d - 1);
+    if (B == 0) return NFX_OK;
+    if (!x || !params || !work || !work_ld) return set_error(NFX_EINVAL, "made_elem_step: null pointer");
+    made_elem_step_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, work, work_ld, B, d,
+                                                                                       i, variant);
+    return check_launch("made_elem_step_kernel");
+}
+
+extern "C" int nfx_made_elem_finish(const float* x, const float* work, const float* work_ld, float* y, float* log_det,
+                                    int64_t B, int d, int variant, int accumulate, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_finish");
+    if (rc) return rc;
+    if (variant != NFX_MAF_FORWARD && variant != NFX_IAF_INVERSE)
+        return set_error(NFX_EINVAL, "made_elem_finish: sequential variants only");
+    if (B == 0) return NFX_OK;
+    if (!x || !work || !work_ld || !y || !log_det) return set_error(NFX_EINVAL, "made_elem_finish: null pointer");
+    made_elem_finish_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, work, work_ld, y, log_det,
+                                                                                         B, d, variant, accumulate);
+    return check_launch("made_elem_finish_kernel");
+}
+
+extern "C" int nfx_made_elem_backward(const float* x, const float* params, const float* gy, const float* gld,
+                                      float* gparams, float* gx, int64_t B, int d, int variant, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_backward");
+    if (rc) return rc;
+    if (variant != NFX_MAF_INVERSE && variant != NFX_IAF_FORWARD)
+        return set_error(NFX_EINVAL, "made_elem_backward: parallel variants only");
+    if (B == 0) return NFX_OK;
+    if (!x || !params || !gparams || !gx) return set_error(NFX_EINVAL, "made_elem_backward: null pointer");
+    made_elem_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, gy, gld, gparams, gx,
+                                                                                      B, d, variant);
+    return check_launch("made_elem_bwd_kernel");
 }

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "nfx_flowbn_backward",
     "nfx_linear_forward", "nfx_linear_backward_data", "nfx_linear_workspace_bytes", "nfx_linear_backward_weight",
     "nfx_spline_elem_forward", "nfx_spline_elem_backward",
+    "nfx_made_elem_forward", "nfx_made_elem_step", "nfx_made_elem_finish", "nfx_made_elem_backward",
 )
 
 
@@ -93,10 +94,14 @@ _SIGNATURES = {
     "nfx_affine_coupling": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_affine_kernel_policy": (_int, [_int]),
-    "nfx_linear_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
-    "nfx_linear_backward_data": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_linear_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_linear_backward_data": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_linear_workspace_bytes": (_sz, [_i64, _int, _int]),
-    "nfx_linear_backward_weight": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp, _vp]),
+    "nfx_linear_backward_weight": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp, _vp]),
+    "nfx_made_elem_forward": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_made_elem_step": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_made_elem_finish": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_made_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp]),
     "nfx_spline_elem_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int, _int, _vp]),
     "nfx_spline_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int,
                                         _vp]),

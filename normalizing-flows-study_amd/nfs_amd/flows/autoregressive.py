@@ -23,11 +23,15 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
+from . import generic as _generic
 from .flow import HipFlow
 
 MAX_H = 256       # eval kernels (H > 128: nfx_made_big.hip)
 MAX_H_BWD = 128   # fused backward kernels; wider layers differentiate through the composite
 MAX_D = 4096
+# Tests: route every call through the any-shape path (csrc/nfx_generic.hip) even where a fused
+# kernel exists, to pin it against the same fixtures.
+FORCE_GENERIC = False
 # Profiling hook (bench.py): when set to a list, every fused backward launch appends
 # (name, start, end) HIP events recorded on the launch stream around the kernel.
 BACKWARD_EVENTS = None
@@ -132,12 +136,66 @@ class _MadeAffineFlow(HipFlow):
         return any(bn.training or bn.running_mean is None for bn in self._batchnorms())
 
     def _hip_supported(self, x):
-        d, H = self.dim, self.conditioner.hidden_dim
+        d = self.dim
         if x.dim() != 2 or x.shape[1] != d:
             return False, f"input shape {tuple(x.shape)} vs dim={d}"
-        if d > MAX_D or H > MAX_H:
-            return False, f"d={d} (<= {MAX_D}) H={H} (<= {MAX_H})"
-        return True, ""
+        return True, ""  # beyond the fused family: the any-shape path (_generic_launch)
+
+    def _fused_family(self):
+        """Shapes of the fused eval kernels (nfx_made*.hip); wider ones run the any-shape path."""
+        return not FORCE_GENERIC and self.dim <= MAX_D and self.conditioner.hidden_dim <= MAX_H
+
+    # -- any-shape path (csrc/nfx_generic.hip): the MADE one MaskedLinear at a time on MFMA ------
+    def _generic_pack(self, device):
+        """(masks, eval-BatchNorm post affines) on the device, cached with the parameters."""
+        lins = self.conditioner.linears()
+        masks = [lin.mask.detach().to(device=device, dtype=torch.float32).contiguous() for lin in lins]
+        posts = [None, None, None]
+        bns = self.conditioner.batchnorms()
+        if bns:
+            for i, bn in enumerate(bns):
+                sc = (bn.weight.detach() / torch.sqrt(bn.running_var.detach() + bn.eps)).float().contiguous()
+                sh = (bn.bias.detach() - bn.running_mean.detach() * sc).float().contiguous()
+                posts[i] = (sc, sh)
+        return masks, posts
+
+    def _generic_made(self, x):
+        masks, posts = self._packed(x.device, self._generic_pack, slot="_nfx_generic_pack_cache")
+        return masks, _generic.made_forward(x, self.conditioner.linears(), masks, posts)
+
+    def _generic_launch(self, x, out, log_det, direction, accumulate):
+        variant = self._variant(direction)
+        L = _lib.lib()
+        B, d = x.shape
+        st = _lib.stream_of(x)
+        if variant in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD):
+            _, (_, _, _, prm) = self._generic_made(x)
+            _lib.check(L.nfx_made_elem_forward(_lib.ptr(x), _lib.ptr(prm), _lib.ptr(out), _lib.ptr(log_det), B, d,
+                                               variant, int(bool(accumulate)), st), "nfx_made_elem_forward")
+            return
+        # sequential direction: the reference's d MADE calls, one element step each
+        work = torch.zeros_like(x)
+        wld = torch.zeros(B, device=x.device, dtype=torch.float32)
+        for i in range(d):
+            _, (_, _, _, prm) = self._generic_made(work)
+            _lib.check(L.nfx_made_elem_step(_lib.ptr(x), _lib.ptr(prm), _lib.ptr(work), _lib.ptr(wld), B, d, i,
+                                            variant, st), "nfx_made_elem_step")
+        _lib.check(L.nfx_made_elem_finish(_lib.ptr(x), _lib.ptr(work), _lib.ptr(wld), _lib.ptr(out), _lib.ptr(log_det),
+                                          B, d, variant, int(bool(accumulate)), st), "nfx_made_elem_finish")
+
+    def _generic_backward(self, x, gz, gld, direction):
+        """Parallel directions beyond the fused backward: MADE recompute (GEMMs), the element
+        adjoint (nfx_made_elem_backward), then the MADE's backward GEMMs."""
+        variant = self._variant(direction)
+        B, d = x.shape
+        masks, (h1, h2, h3, prm) = self._generic_made(x)
+        gprm = torch.empty_like(prm)
+        gx = torch.empty_like(x)
+        _lib.check(_lib.lib().nfx_made_elem_backward(_lib.ptr(x), _lib.ptr(prm), _lib.ptr(gz), _lib.ptr(gld),
+                                                     _lib.ptr(gprm), _lib.ptr(gx), B, d, variant, _lib.stream_of(x)),
+                   "nfx_made_elem_backward")
+        grads = _generic.made_backward(x, self.conditioner.linears(), masks, h1, h2, h3, gprm, gx)
+        return gx, grads
 
     def _build_pack(self, device):
         d, H = self.dim, self.conditioner.hidden_dim
@@ -156,10 +214,15 @@ class _MadeAffineFlow(HipFlow):
     def _hip_backward_ok(self, x, direction):
         if x.dtype != torch.float32 or self.conditioner.batchnorms():
             return False
-        d, H = self.dim, self.conditioner.hidden_dim
+        if self._fused_backward_ok():
+            return True
+        # the any-shape path differentiates the parallel directions
+        return self._variant(direction) in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD)
+
+    def _fused_backward_ok(self):
         # parallel directions: made_bwd_kernel (d, H <= 64) / made_bwdw_kernel; sequential
         # directions: made_seq_bwd_kernel
-        return d <= MAX_D and H <= MAX_H_BWD
+        return not FORCE_GENERIC and self.dim <= MAX_D and self.conditioner.hidden_dim <= MAX_H_BWD
 
     def _hip_backward(self, x, gz, gld, direction):
         """dL/dx and the parameter gradients (in self.parameters() order) of one call. Batches
@@ -170,6 +233,8 @@ class _MadeAffineFlow(HipFlow):
         H = self.conditioner.hidden_dim
         gz = torch.zeros_like(x) if gz is None else gz.contiguous().float()
         gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
+        if not self._fused_backward_ok():
+            return self._generic_backward(x, gz, gld, direction)
         cap = int(_lib.lib().nfx_made_backward_max_batch(d, H))
         if B > cap:
             gxs, acc = [], None
@@ -230,6 +295,8 @@ class _MadeAffineFlow(HipFlow):
         return out
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
+        if not self._fused_family():
+            return self._generic_launch(x, out, log_det, direction, accumulate)
         packed = self._packed(x.device, self._build_pack)
         _lib.check(_lib.lib().nfx_made_affine(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), x.shape[0], self.dim,
@@ -237,6 +304,8 @@ class _MadeAffineFlow(HipFlow):
             _lib.stream_of(x)), "nfx_made_affine")
 
     def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
+        if not self._fused_family():
+            return False
         variant = self._variant(-1)
         packed = self._packed(x.device, self._build_pack)
         rc = _lib.lib().nfx_made_affine_logprob(

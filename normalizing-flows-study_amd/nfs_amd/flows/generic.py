@@ -10,42 +10,46 @@ import torch
 from .. import _lib
 
 
-def linear_forward(x, lin, in_scale=None, relu=False):
-    """relu?((x * in_scale) @ lin.weight.T + lin.bias) — one nn.Linear (+ ReLU) on MFMA."""
+def linear_forward(x, lin, in_scale=None, relu=False, wmask=None, post=None):
+    """relu?(((x * in_scale) @ (lin.weight * wmask).T + lin.bias) * post[0] + post[1]) — one
+    nn.Linear / MaskedLinear (+ folded eval BatchNorm, + ReLU) on MFMA."""
     M, K = x.shape
     N = lin.out_features
     y = torch.empty(M, N, device=x.device, dtype=torch.float32)
     w = lin.weight.detach()
     b = None if lin.bias is None else lin.bias.detach()
-    _lib.check(_lib.lib().nfx_linear_forward(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(in_scale), _lib.ptr(y),
+    ps, pt = (None, None) if post is None else post
+    _lib.check(_lib.lib().nfx_linear_forward(_lib.ptr(x), _lib.ptr(w), _lib.ptr(wmask), _lib.ptr(b),
+                                             _lib.ptr(in_scale), _lib.ptr(ps), _lib.ptr(pt), _lib.ptr(y),
                                              M, K, N, int(bool(relu)), _lib.stream_of(x)), "nfx_linear_forward")
     return y
 
 
-def linear_backward_data(gy, lin, act=None, out_scale=None, out=None):
-    """(gy @ lin.weight) * out_scale, masked where act <= 0 (the ReLU feeding this Linear);
-    added into `out` when given."""
+def linear_backward_data(gy, lin, act=None, out_scale=None, out=None, wmask=None):
+    """(gy @ (lin.weight * wmask)) * out_scale, masked where act <= 0 (the ReLU feeding this
+    Linear); added into `out` when given."""
     M, N = gy.shape
     K = lin.in_features
     acc = out is not None
     if out is None:
         out = torch.empty(M, K, device=gy.device, dtype=torch.float32)
-    _lib.check(_lib.lib().nfx_linear_backward_data(_lib.ptr(gy), _lib.ptr(lin.weight.detach()), _lib.ptr(act),
-                                                   _lib.ptr(out_scale), _lib.ptr(out), M, N, K, int(acc),
-                                                   _lib.stream_of(gy)), "nfx_linear_backward_data")
+    _lib.check(_lib.lib().nfx_linear_backward_data(_lib.ptr(gy), _lib.ptr(lin.weight.detach()), _lib.ptr(wmask),
+                                                   _lib.ptr(act), _lib.ptr(out_scale), _lib.ptr(out), M, N, K,
+                                                   int(acc), _lib.stream_of(gy)), "nfx_linear_backward_data")
     return out
 
 
-def linear_backward_weight(gy, x, lin, in_scale=None):
-    """(dL/dweight, dL/dbias) of one nn.Linear: gy^T (x * in_scale), column sums of gy."""
+def linear_backward_weight(gy, x, lin, in_scale=None, wmask=None):
+    """(dL/dweight, dL/dbias) of one nn.Linear / MaskedLinear: (gy^T (x * in_scale)) * wmask,
+    column sums of gy."""
     M, N = gy.shape
     K = lin.in_features
     L = _lib.lib()
     gw = torch.empty(N, K, device=gy.device, dtype=torch.float32)
     gb = None if lin.bias is None else torch.empty(N, device=gy.device, dtype=torch.float32)
     ws = torch.empty(max(1, L.nfx_linear_workspace_bytes(M, N, K)), device=gy.device, dtype=torch.uint8)
-    _lib.check(L.nfx_linear_backward_weight(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(in_scale), _lib.ptr(gw),
-                                            _lib.ptr(gb), M, N, K, _lib.ptr(ws), _lib.stream_of(gy)),
+    _lib.check(L.nfx_linear_backward_weight(_lib.ptr(gy), _lib.ptr(x), _lib.ptr(in_scale), _lib.ptr(wmask),
+                                            _lib.ptr(gw), _lib.ptr(gb), M, N, K, _lib.ptr(ws), _lib.stream_of(gy)),
                "nfx_linear_backward_weight")
     return gw, gb
 
@@ -68,3 +72,26 @@ def mlp3_backward(x, l1, l2, l3, in_scale, h1, h2, g3, gx):
     gw1, gb1 = linear_backward_weight(g1, x, l1, in_scale)
     linear_backward_data(g1, l1, out_scale=in_scale, out=gx)
     return [gw1, gb1, gw2, gb2, gw3, gb3]
+
+
+def made_forward(x, lins, masks, posts):
+    """MADE conditioner (made.py:136-140): MaskedLinear (+ eval BatchNorm) + ReLU three times, then
+    the output MaskedLinear. Returns (h1, h2, h3, params [B, 2d])."""
+    h1 = linear_forward(x, lins[0], relu=True, wmask=masks[0], post=posts[0])
+    h2 = linear_forward(h1, lins[1], relu=True, wmask=masks[1], post=posts[1])
+    h3 = linear_forward(h2, lins[2], relu=True, wmask=masks[2], post=posts[2])
+    return h1, h2, h3, linear_forward(h3, lins[3], wmask=masks[3])
+
+
+def made_backward(x, lins, masks, h1, h2, h3, gp, gx):
+    """Backward of made_forward (no BatchNorm) given dL/dparams = gp: parameter gradients in
+    parameters() order; dL/dx is added into gx."""
+    g4 = linear_backward_weight(gp, h3, lins[3], wmask=masks[3])
+    g = linear_backward_data(gp, lins[3], act=h3, wmask=masks[3])
+    g3 = linear_backward_weight(g, h2, lins[2], wmask=masks[2])
+    g = linear_backward_data(g, lins[2], act=h2, wmask=masks[2])
+    g2 = linear_backward_weight(g, h1, lins[1], wmask=masks[1])
+    g = linear_backward_data(g, lins[1], act=h1, wmask=masks[1])
+    g1 = linear_backward_weight(g, x, lins[0], wmask=masks[0])
+    linear_backward_data(g, lins[0], wmask=masks[0], out=gx)
+    return [*g1, *g2, *g3, *g4]

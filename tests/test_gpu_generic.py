@@ -11,6 +11,11 @@ coupling's element kernels, for layers beyond the fused kernel families.
   fused backward family (H = 128, several transformed dims at H = 64, d = 12) against float64
   autograd with the error model of test_gpu_spline_backward.py; and forced onto the fused shapes
   (spline.FORCE_GENERIC) against the reference's own gradients (G14) and the fused kernels.
+* MAF / IAF on the any-shape path — forced onto the reference's fixtures (G5 both directions,
+  G9, the G14 gradients of the parallel directions), H > 256 against the oracle (both
+  directions; the sequential ones as the reference's d MADE calls), eval BatchNorm at H = 288,
+  and H = 320 gradients against float64 autograd (MADE tolerances of test_gpu_made.py /
+  test_gpu_grad_fixtures.py).
 """
 import copy
 
@@ -219,3 +224,153 @@ def test_realnvp_spline_h128_training_step(cuda_device):
     _check(gx, gx32, gx64, "dL/dx")
     for (n, _), a, b, c in zip(model.named_parameters(), gp, gp32, gp64):
         _check(a, b, c, n)
+
+
+# ---- MADE flows (MAF / IAF) on the any-shape path ---------------------------------------------
+from test_gpu_made import assert_ld, assert_y  # noqa: E402
+from nfs_amd.flows import autoregressive as _ar  # noqa: E402
+
+
+@pytest.fixture
+def force_generic_made():
+    old = _ar.FORCE_GENERIC
+    _ar.FORCE_GENERIC = True
+    yield
+    _ar.FORCE_GENERIC = old
+
+
+def test_generic_made_vs_reference_g5_g9(cuda_device, force_generic_made):
+    """Forced onto the reference's MAF(63, 64) x5 (G5, both directions — the sequential one as
+    the reference's d MADE calls) and its small MAF/IAF fixtures (G9)."""
+    g = load_golden("g5_maf63.npz")
+    m = nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(63, 64) for _ in range(5)])
+    m.load_state_dict(state_dict_from(g, "", m))
+    m = m.to(cuda_device).eval()
+    STATS["hip"] = STATS["torch"] = 0
+    with torch.no_grad():
+        z, ld = m.inverse(torch.from_numpy(g["x"]).to(cuda_device))
+        x, lf = m.forward(torch.from_numpy(g["z"][:256]).to(cuda_device))
+    assert STATS["torch"] == 0
+    assert_y(z.cpu(), g["inv_z"])
+    assert_ld(ld.cpu(), g["inv_ld"])
+    assert_y(x.cpu(), g["fwd_x"][:256])
+    assert_ld(lf.cpu(), g["fwd_ld"][:256])
+    g9 = load_golden("g9_small.npz")
+    for name, cls in (("maf4", nfs_amd.MaskedAutoregressiveFlow), ("iaf10", nfs_amd.InverseAutoregressiveFlow),
+                      ("maf2", nfs_amd.MaskedAutoregressiveFlow), ("iaf3", nfs_amd.InverseAutoregressiveFlow)):
+        sd = oracle_sd(g9, name + ".")
+        f = cls(sd["conditioner.net.0.weight"].shape[1], sd["conditioner.net.0.weight"].shape[0])
+        f.load_state_dict(state_dict_from(g9, name + ".", f))
+        f = f.to(cuda_device).eval()
+        xx = torch.from_numpy(g9[name + ".x"]).to(cuda_device)
+        with torch.no_grad():
+            yf, lf = f.forward(xx)
+            yi, li = f.inverse(xx)
+        assert_y(yf.cpu(), g9[name + ".fwd_y"])
+        assert_ld(lf.cpu(), g9[name + ".fwd_ld"])
+        assert_y(yi.cpu(), g9[name + ".inv_y"])
+        assert_ld(li.cpu(), g9[name + ".inv_ld"])
+
+
+@pytest.mark.parametrize("d,H,B", [(5, 320, 100), (40, 512, 257), (2, 300, 64), (300, 264, 33)])
+def test_generic_made_wide_vs_oracle(cuda_device, d, H, B):
+    """H > 256 (beyond nfx_made_big.hip): the any-shape path, both flows, both directions."""
+    torch.manual_seed(d * 31 + H)
+    for cls, fn in ((nfs_amd.MaskedAutoregressiveFlow, oracle.maf), (nfs_amd.InverseAutoregressiveFlow, oracle.iaf)):
+        f = cls(d, H)
+        with torch.no_grad():
+            for p in f.parameters():
+                p.add_(0.05 * torch.randn_like(p))
+        sd = {k: v.clone() for k, v in f.state_dict().items()}
+        f = f.to(cuda_device).eval()
+        assert not f._fused_family()
+        x = torch.randn(B, d)
+        x[0, 0] = float("inf")
+        for direction in (1, -1):
+            STATS["hip"] = STATS["torch"] = 0
+            with torch.no_grad():
+                yg, lg = (f.forward if direction > 0 else f.inverse)(x.to(cuda_device))
+                yr, lr = fn(sd, "", x, direction)
+            assert STATS["hip"] == 1 and STATS["torch"] == 0, STATS
+            yr = np.asarray(yr, np.float64)
+            assert np.array_equal(np.isnan(yg.cpu().numpy()), np.isnan(yr))
+            fin = np.isfinite(yr)
+            assert_y(yg.cpu().numpy()[fin], yr[fin])
+            assert_ld(lg.cpu(), lr, 5e-4)
+
+
+def test_generic_made_batchnorm_eval_wide(cuda_device):
+    """MADE(use_batch_norm=True), eval, H = 288: BatchNorm folded into the GEMM epilogue."""
+    torch.manual_seed(19)
+    f = nfs_amd.MaskedAutoregressiveFlow(12, 288, use_batch_norm=True)
+    with torch.no_grad():
+        for m in f.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.normal_(0, 0.1)
+                m.running_var.uniform_(0.5, 1.5)
+                m.weight.normal_(1, 0.1)
+                m.bias.normal_(0, 0.1)
+    f.eval()
+    x = torch.randn(300, 12)
+    with torch.no_grad():
+        zc, lc = f.inverse(x)
+        xc, lfc = f.forward(x)
+    f = f.to(cuda_device)
+    with torch.no_grad():
+        zg, lg = f.inverse(x.to(cuda_device))
+        xg, lfg = f.forward(x.to(cuda_device))
+    assert_y(zg.cpu(), zc)
+    assert_ld(lg.cpu(), lc)
+    assert_y(xg.cpu(), xc)
+    assert_ld(lfg.cpu(), lfc)
+
+
+@pytest.mark.parametrize("name", ["maf10", "iaf10", "maf63", "iaf784"])
+def test_generic_made_vs_reference_gradients_g14(cuda_device, force_generic_made, name):
+    """Parallel directions (MAF inverse / IAF forward) on the any-shape path: the reference's
+    own fp32 gradients (G14)."""
+    from test_gpu_grad_fixtures import _g14_module, _grad_close, _run
+    dname = "inv" if name.startswith("maf") else "fwd"
+    g = load_golden("g14_grads.npz")
+    m = _g14_module(name)
+    m.load_state_dict(state_dict_from(g, name + ".init.", m))
+    m.eval()
+    m64 = copy.deepcopy(m).double()
+    x, wy, wl = (torch.from_numpy(g[f"{name}.{k}"]) for k in ("x", "wy", "wl"))
+    _, _, gx64, gp64 = _run(m64, x.double(), wy.double(), wl.double(), dname)
+    mg = m.to(cuda_device)
+    STATS["hip"] = STATS["torch"] = 0
+    y, ld, gx, gp = _run(mg, x.to(cuda_device), wy.to(cuda_device), wl.to(cuda_device), dname)
+    assert STATS["torch"] == 0 and STATS["hip"] == 2, STATS
+    yr, ldr = g[f"{name}.{dname}.y"], g[f"{name}.{dname}.ld"]
+    assert (np.abs(y.cpu().numpy().astype(np.float64) - yr) <= 2e-5 * (1 + np.abs(yr))).all()
+    ltol = 1e-6 * np.abs(ldr).max() + 2e-4 if name == "iaf784" else 2e-4
+    assert np.abs(ld.cpu().numpy().astype(np.float64) - ldr).max() <= ltol
+    _grad_close(gx, g[f"{name}.{dname}.gx"], gx64, "dL/dx")
+    for k in gp64:
+        _grad_close(gp[k], g[f"{name}.{dname}.grad.{k}"], gp64[k], k)
+
+
+@pytest.mark.parametrize("cls", ["maf", "iaf"])
+def test_generic_made_wide_backward_vs_float64(cuda_device, cls):
+    """H = 320 (beyond the fused backward's H <= 128), parallel direction, vs float64 autograd."""
+    from test_gpu_grad_fixtures import _grad_close, _run
+    torch.manual_seed(23)
+    f = (nfs_amd.MaskedAutoregressiveFlow if cls == "maf" else nfs_amd.InverseAutoregressiveFlow)(24, 320)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.add_(0.03 * torch.randn_like(p))
+    dname = "inv" if cls == "maf" else "fwd"
+    g = torch.Generator().manual_seed(29)
+    x, wy, wl = torch.randn(3000, 24, generator=g), torch.randn(3000, 24, generator=g), torch.randn(3000, generator=g)
+    y32, l32, gx32, gp32 = _run(f, x, wy, wl, dname)
+    _, _, gx64, gp64 = _run(copy.deepcopy(f).double(), x.double(), wy.double(), wl.double(), dname)
+    fg = copy.deepcopy(f).to(cuda_device)
+    STATS["hip"] = STATS["torch"] = 0
+    y, ld, gx, gp = _run(fg, x.to(cuda_device), wy.to(cuda_device), wl.to(cuda_device), dname)
+    assert STATS["torch"] == 0 and STATS["hip"] == 2, STATS
+    assert_y(y.cpu(), y32)
+    assert_ld(ld.cpu(), l32)
+    _grad_close(gx, gx32, gx64, "dL/dx")
+    for k in gp64:
+        _grad_close(gp[k], gp32[k], gp64[k], k)
