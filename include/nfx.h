@@ -417,6 +417,14 @@ int nfx_made_elem_finish(const float* x, const float* work, const float* work_ld
                          int64_t B, int d, int variant, int accumulate, void* stream);
 int nfx_made_elem_backward(const float* x, const float* params, const float* gy, const float* gld, float* gparams,
                            float* gx, int64_t B, int d, int variant, void* stream);
+/* Adjoint pieces of a sequential direction (autograd through the reference's d MADE calls),
+ * at the finished raw vector `work` and params = MADE(work): mode 0 writes out [B][d] = the
+ * output guard's share of gy; mode 1 out [B][2d] = dL/dparams for the total adjoint lam [B][d];
+ * mode 2 out [B][d] = dL/dx. The caller iterates lam = (mode 0) + MADE-input-VJP(mode 1) d times
+ * (the Jacobian is strictly triangular), then takes the weight gradients from mode 1. */
+int nfx_made_elem_seq_backward(const float* x, const float* params, const float* work, const float* lam,
+                               const float* gy, const float* gld, float* out, int64_t B, int d, int variant, int mode,
+                               void* stream);
 /* SplineCouplingLayer element math for any d (spline_coupling_layer.py:96-180 with the spline
  * of :182-309): params [B][d][3K-1] = param_net output; dims with mask == 0 go through the RQ
  * spline (forward: direction +1, inverse: -1), the rest pass through; layer guards and the

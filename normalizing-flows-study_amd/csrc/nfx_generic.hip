@@ -399,6 +399,57 @@ __global__ __launch_bounds__(256) void made_elem_bwd_kernel(const float* __restr
     }
 }
 
+// Adjoint pieces of a sequential direction, differentiated at the finished vector w (the raw
+// conditioner input after the last step; params = MADE(w): column i of it equals step i's
+// params, the masks give mu_i, alpha_i no dependence on w_j, j >= i). With lam = the total
+// dL/dw (the upstream gradient through the output guard plus what later steps pass back through
+// the MADE), mode 0 writes g_w = the guard's share of gy, mode 1 dL/dparams [B][2d] of lam,
+// mode 2 dL/dx. The caller iterates lam = g_w + MADE-input-VJP(mode 1) d times (nilpotent:
+// the Jacobian is strictly triangular), which is autograd through the reference's d calls.
+//   MAF forward  w_i = x_i exp(clamp(a_i,-5,5)) + mu_i, a = clamp(alpha,-3,3), ld = sum a
+//   IAF inverse  w_i = (x_i - clamp(mu_i,-10,10)) exp(clamp(-a_i,-3,3)), a = clamp(alpha,-2,2), ld = -sum a
+__global__ __launch_bounds__(256) void made_elem_seq_bwd_kernel(const float* __restrict__ x, const float* __restrict__ prm,
+                                                                const float* __restrict__ w, const float* __restrict__ lam,
+                                                                const float* __restrict__ gy, const float* __restrict__ gld,
+                                                                float* __restrict__ out, int64_t B, int d, int variant,
+                                                                int mode) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const bool maf = variant == NFX_MAF_FORWARD;
+    if (mode == 0) {
+        for (int j = 0; j < d; ++j) out[s * d + j] = (gy && !nonfinite(w[s * d + j])) ? gy[s * d + j] : 0.f;
+        return;
+    }
+    const float* mu = prm + s * 2 * d;
+    const float* al = mu + d;
+    const float lo = maf ? -3.f : -2.f, hi = maf ? 3.f : 2.f, lim = maf ? 100.f : 50.f;
+    float gl = 0.f;
+    if (mode == 1) {
+        float ldr = 0.f;
+        for (int j = 0; j < d; ++j) ldr = maf ? ldr + tclamp(al[j], lo, hi) : ldr - tclamp(al[j], lo, hi);
+        const float g0 = gld ? gld[s] : 0.f;
+        gl = (nonfinite(ldr) || !(ldr >= -lim && ldr <= lim)) ? 0.f : g0;
+    }
+    for (int j = 0; j < d; ++j) {
+        const float alpha = al[j], m = mu[j], xv = x[s * d + j], l = lam[s * d + j];
+        const float a = tclamp(alpha, lo, hi);
+        const bool ain = alpha >= lo && alpha <= hi;
+        const float e = maf ? exp_fast(tclamp(a, -5.f, 5.f)) : exp_fast(tclamp(-a, -3.f, 3.f));
+        if (mode == 2) {
+            const float gd = (!maf && gy && nonfinite(w[s * d + j])) ? gy[s * d + j] : 0.f;  // IAF guard: y = x
+            out[s * d + j] = l * e + gd;
+        } else if (maf) {
+            out[s * 2 * d + j] = l;
+            out[s * 2 * d + d + j] = ain ? l * xv * e + gl : 0.f;
+        } else {
+            const float xm = xv - tclamp(m, -10.f, 10.f);
+            out[s * 2 * d + j] = (m >= -10.f && m <= 10.f) ? -(l * e) : 0.f;
+            out[s * 2 * d + d + j] = ain ? -(l * xm * e) - gl : 0.f;
+        }
+    }
+}
+
 }  // namespace nfx
 
 using namespace nfx;
@@ -592,4 +643,19 @@ extern "C" int nfx_made_elem_backward(const float* x, const float* params, const
     made_elem_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, gy, gld, gparams, gx,
                                                                                       B, d, variant);
     return check_launch("made_elem_bwd_kernel");
+}
+
+extern "C" int nfx_made_elem_seq_backward(const float* x, const float* params, const float* work, const float* lam,
+                                          const float* gy, const float* gld, float* out, int64_t B, int d, int variant,
+                                          int mode, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_seq_backward");
+    if (rc) return rc;
+    if (variant != NFX_MAF_FORWARD && variant != NFX_IAF_INVERSE)
+        return set_error(NFX_EINVAL, "made_elem_seq_backward: sequential variants only");
+    if (mode < 0 || mode > 2) return set_error(NFX_EINVAL, "made_elem_seq_backward: mode %d", mode);
+    if (B == 0) return NFX_OK;
+    if (!x || !work || !out || (mode > 0 && (!params || !lam))) return set_error(NFX_EINVAL, "made_elem_seq_backward: null pointer");
+    made_elem_seq_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, work, lam, gy, gld,
+                                                                                          out, B, d, variant, mode);
+    return check_launch("made_elem_seq_bwd_kernel");
 }

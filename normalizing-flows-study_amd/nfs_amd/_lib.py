@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "nfx_linear_forward", "nfx_linear_backward_data", "nfx_linear_workspace_bytes", "nfx_linear_backward_weight",
     "nfx_spline_elem_forward", "nfx_spline_elem_backward",
     "nfx_made_elem_forward", "nfx_made_elem_step", "nfx_made_elem_finish", "nfx_made_elem_backward",
+    "nfx_made_elem_seq_backward",
 )
 
 
@@ -102,6 +103,7 @@ _SIGNATURES = {
     "nfx_made_elem_step": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_made_elem_finish": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_made_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp]),
+    "nfx_made_elem_seq_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_spline_elem_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int, _int, _vp]),
     "nfx_spline_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int,
                                         _vp]),

@@ -173,20 +173,60 @@ class _MadeAffineFlow(HipFlow):
             _lib.check(L.nfx_made_elem_forward(_lib.ptr(x), _lib.ptr(prm), _lib.ptr(out), _lib.ptr(log_det), B, d,
                                                variant, int(bool(accumulate)), st), "nfx_made_elem_forward")
             return
-        # sequential direction: the reference's d MADE calls, one element step each
+        work, wld = self._generic_seq_work(x, variant)
+        _lib.check(L.nfx_made_elem_finish(_lib.ptr(x), _lib.ptr(work), _lib.ptr(wld), _lib.ptr(out), _lib.ptr(log_det),
+                                          B, d, variant, int(bool(accumulate)), st), "nfx_made_elem_finish")
+
+    def _generic_seq_work(self, x, variant):
+        """A sequential direction as the reference runs it: d MADE calls, one element step each
+        (nfx_made_elem_step); returns the raw vector and log-det before the final guards."""
+        B, d = x.shape
+        L = _lib.lib()
+        st = _lib.stream_of(x)
         work = torch.zeros_like(x)
         wld = torch.zeros(B, device=x.device, dtype=torch.float32)
         for i in range(d):
             _, (_, _, _, prm) = self._generic_made(work)
             _lib.check(L.nfx_made_elem_step(_lib.ptr(x), _lib.ptr(prm), _lib.ptr(work), _lib.ptr(wld), B, d, i,
                                             variant, st), "nfx_made_elem_step")
-        _lib.check(L.nfx_made_elem_finish(_lib.ptr(x), _lib.ptr(work), _lib.ptr(wld), _lib.ptr(out), _lib.ptr(log_det),
-                                          B, d, variant, int(bool(accumulate)), st), "nfx_made_elem_finish")
+        return work, wld
+
+    def _generic_seq_backward(self, x, gz, gld, variant):
+        """A sequential direction beyond the fused backward: autograd through the reference's d
+        MADE calls, computed at the finished vector w (params = MADE(w) equal every step's params,
+        masks): the total adjoint lam of w solves lam = g_w + VJP_w(dparams(lam)), a strictly
+        triangular system, by d - 1 substitution passes (each one MADE input-VJP, 4 GEMMs);
+        then the weight gradients for dparams(lam) and dL/dx."""
+        B, d = x.shape
+        L = _lib.lib()
+        st = _lib.stream_of(x)
+        p = _lib.ptr
+        work, _ = self._generic_seq_work(x, variant)
+        masks, (h1, h2, h3, prm) = self._generic_made(work)
+        lins = self.conditioner.linears()
+        gw = torch.empty_like(x)
+        _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), None, p(gz), p(gld), p(gw), B, d, variant, 0,
+                                                st), "nfx_made_elem_seq_backward")
+        lam = gw
+        dprm = torch.empty_like(prm)
+        for _ in range(d - 1):
+            _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), p(lam), p(gz), p(gld), p(dprm), B, d,
+                                                    variant, 1, st), "nfx_made_elem_seq_backward")
+            lam = _generic.made_input_vjp(dprm, lins, masks, h1, h2, h3, gw.clone())
+        _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), p(lam), p(gz), p(gld), p(dprm), B, d,
+                                                variant, 1, st), "nfx_made_elem_seq_backward")
+        gx = torch.empty_like(x)
+        _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), p(lam), p(gz), p(gld), p(gx), B, d,
+                                                variant, 2, st), "nfx_made_elem_seq_backward")
+        return gx, _generic.made_backward(work, lins, masks, h1, h2, h3, dprm, None)
 
     def _generic_backward(self, x, gz, gld, direction):
-        """Parallel directions beyond the fused backward: MADE recompute (GEMMs), the element
-        adjoint (nfx_made_elem_backward), then the MADE's backward GEMMs."""
+        """Beyond the fused backward: parallel directions — MADE recompute (GEMMs), the element
+        adjoint (nfx_made_elem_backward), then the MADE's backward GEMMs; sequential directions —
+        _generic_seq_backward."""
         variant = self._variant(direction)
+        if variant in (_lib.NFX_MAF_FORWARD, _lib.NFX_IAF_INVERSE):
+            return self._generic_seq_backward(x, gz, gld, variant)
         B, d = x.shape
         masks, (h1, h2, h3, prm) = self._generic_made(x)
         gprm = torch.empty_like(prm)
@@ -214,10 +254,7 @@ class _MadeAffineFlow(HipFlow):
     def _hip_backward_ok(self, x, direction):
         if x.dtype != torch.float32 or self.conditioner.batchnorms():
             return False
-        if self._fused_backward_ok():
-            return True
-        # the any-shape path differentiates the parallel directions
-        return self._variant(direction) in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD)
+        return True  # fused backward kernels, or the any-shape path (_generic_backward)
 
     def _fused_backward_ok(self):
         # parallel directions: made_bwd_kernel (d, H <= 64) / made_bwdw_kernel; sequential

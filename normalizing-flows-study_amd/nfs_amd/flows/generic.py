@@ -83,9 +83,17 @@ def made_forward(x, lins, masks, posts):
     return h1, h2, h3, linear_forward(h3, lins[3], wmask=masks[3])
 
 
+def made_input_vjp(gp, lins, masks, h1, h2, h3, out):
+    """dL/d(MADE input) for dL/dparams = gp (no BatchNorm), added into `out`."""
+    g = linear_backward_data(gp, lins[3], act=h3, wmask=masks[3])
+    g = linear_backward_data(g, lins[2], act=h2, wmask=masks[2])
+    g = linear_backward_data(g, lins[1], act=h1, wmask=masks[1])
+    return linear_backward_data(g, lins[0], wmask=masks[0], out=out)
+
+
 def made_backward(x, lins, masks, h1, h2, h3, gp, gx):
     """Backward of made_forward (no BatchNorm) given dL/dparams = gp: parameter gradients in
-    parameters() order; dL/dx is added into gx."""
+    parameters() order; dL/dx is added into gx (skipped when gx is None)."""
     g4 = linear_backward_weight(gp, h3, lins[3], wmask=masks[3])
     g = linear_backward_data(gp, lins[3], act=h3, wmask=masks[3])
     g3 = linear_backward_weight(g, h2, lins[2], wmask=masks[2])
@@ -93,5 +101,6 @@ def made_backward(x, lins, masks, h1, h2, h3, gp, gx):
     g2 = linear_backward_weight(g, h1, lins[1], wmask=masks[1])
     g = linear_backward_data(g, lins[1], act=h1, wmask=masks[1])
     g1 = linear_backward_weight(g, x, lins[0], wmask=masks[0])
-    linear_backward_data(g, lins[0], wmask=masks[0], out=gx)
+    if gx is not None:
+        linear_backward_data(g, lins[0], wmask=masks[0], out=gx)
     return [*g1, *g2, *g3, *g4]

@@ -326,11 +326,12 @@ def test_generic_made_batchnorm_eval_wide(cuda_device):
 
 
 @pytest.mark.parametrize("name", ["maf10", "iaf10", "maf63", "iaf784"])
-def test_generic_made_vs_reference_gradients_g14(cuda_device, force_generic_made, name):
-    """Parallel directions (MAF inverse / IAF forward) on the any-shape path: the reference's
-    own fp32 gradients (G14)."""
+@pytest.mark.parametrize("dname", ["inv", "fwd"])
+def test_generic_made_vs_reference_gradients_g14(cuda_device, force_generic_made, name, dname):
+    """Both directions on the any-shape path — parallel: element adjoint + MADE backward GEMMs;
+    sequential: the triangular adjoint solve through the MADE — against the reference's own fp32
+    gradients (G14; its sequential ones are autograd through all d MADE calls)."""
     from test_gpu_grad_fixtures import _g14_module, _grad_close, _run
-    dname = "inv" if name.startswith("maf") else "fwd"
     g = load_golden("g14_grads.npz")
     m = _g14_module(name)
     m.load_state_dict(state_dict_from(g, name + ".init.", m))
@@ -352,15 +353,15 @@ def test_generic_made_vs_reference_gradients_g14(cuda_device, force_generic_made
 
 
 @pytest.mark.parametrize("cls", ["maf", "iaf"])
-def test_generic_made_wide_backward_vs_float64(cuda_device, cls):
-    """H = 320 (beyond the fused backward's H <= 128), parallel direction, vs float64 autograd."""
+@pytest.mark.parametrize("dname", ["inv", "fwd"])
+def test_generic_made_wide_backward_vs_float64(cuda_device, cls, dname):
+    """H = 320 (beyond the fused backward's H <= 128), both directions, vs float64 autograd."""
     from test_gpu_grad_fixtures import _grad_close, _run
     torch.manual_seed(23)
     f = (nfs_amd.MaskedAutoregressiveFlow if cls == "maf" else nfs_amd.InverseAutoregressiveFlow)(24, 320)
     with torch.no_grad():
         for p in f.parameters():
             p.add_(0.03 * torch.randn_like(p))
-    dname = "inv" if cls == "maf" else "fwd"
     g = torch.Generator().manual_seed(29)
     x, wy, wl = torch.randn(3000, 24, generator=g), torch.randn(3000, 24, generator=g), torch.randn(3000, generator=g)
     y32, l32, gx32, gp32 = _run(f, x, wy, wl, dname)
