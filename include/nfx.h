@@ -425,6 +425,34 @@ int nfx_made_elem_backward(const float* x, const float* params, const float* gy,
 int nfx_made_elem_seq_backward(const float* x, const float* params, const float* work, const float* lam,
                                const float* gy, const float* gld, float* out, int64_t B, int d, int variant, int mode,
                                void* stream);
+/* CouplingLayer element math for any (d, H) (coupling_layer.py:40-96): s_raw, b_raw [B][d] are
+ * the raw s_net / b_net outputs; forward (+1) or inverse (-1) affine map with the clamps, guards
+ * and log-det; the backward gives dL/ds_raw, dL/db_raw and the direct dL/dx term. */
+int nfx_affine_elem_forward(const float* x, const float* s_raw, const float* b_raw, const float* mask, float* y,
+                            float* log_det, int64_t B, int d, int direction, int accumulate, void* stream);
+int nfx_affine_elem_backward(const float* x, const float* s_raw, const float* b_raw, const float* mask,
+                             const float* gy, const float* gld, float* gs, float* gb, float* gx, int64_t B, int d,
+                             int direction, void* stream);
+/* A conditioner BatchNorm1d at any width N: nfx_bn_prepare turns batch moments (stats: float64
+ * (n, mean, M2) per feature from nfx_flowbn_moments, SyncBN-merged; running statistics updated
+ * with the unbiased variance when update_running) or, with stats = NULL, the running statistics
+ * into mean / invstd / scale = gamma invstd / shift = beta - mean scale (BN(z) = z scale + shift);
+ * nfx_bn_apply_relu h = relu(z scale + shift); the backward takes g = dL/dBN-output (ReLU mask
+ * applied): nfx_bn_backward_sums sums [2][N] = (sum g = dL/dbeta, sum g xhat = dL/dgamma) in
+ * float64 (workspace nfx_bn_workspace_bytes(M, N)); nfx_bn_backward_apply dL/dz (train: the
+ * batch-statistics terms with the global sample count *count, a device float64 — the n of the
+ * merged moments triple). */
+int nfx_bn_prepare(const double* stats, const float* gamma, const float* beta, float* running_mean,
+                   float* running_var, double eps, double momentum, int update_running, int N, float* mean,
+                   float* invstd, float* scale, float* shift, void* stream);
+int nfx_bn_apply_relu(const float* z, const float* scale, const float* shift, float* h, int64_t M, int N,
+                      void* stream);
+size_t nfx_bn_workspace_bytes(int64_t M, int N);
+int nfx_bn_backward_sums(const float* g, const float* z, const float* mean, const float* invstd, double* sums,
+                         int64_t M, int N, void* workspace, void* stream);
+int nfx_bn_backward_apply(const float* g, const float* z, const float* mean, const float* invstd,
+                          const float* gamma, const double* sums, const double* count, int train, float* gz,
+                          int64_t M, int N, void* stream);
 /* SplineCouplingLayer element math for any d (spline_coupling_layer.py:96-180 with the spline
  * of :182-309): params [B][d][3K-1] = param_net output; dims with mask == 0 go through the RQ
  * spline (forward: direction +1, inverse: -1), the rest pass through; layer guards and the

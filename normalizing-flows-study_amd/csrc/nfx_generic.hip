@@ -450,6 +450,178 @@ __global__ __launch_bounds__(256) void made_elem_seq_bwd_kernel(const float* __r
     }
 }
 
+// ---- affine coupling element math (coupling_layer.py:40-96) ---------------------------------
+// s, b = clamp(raw, -10, 10); y = x m + (1 - m)(x exp(s) + b)  (forward) or
+// x m + (1 - m)((x - b) exp(-s)) (inverse); ld = sum_j (1 - m) (+-s); guards: y, ld non-finite -> 0.
+__global__ __launch_bounds__(256) void affine_elem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sr,
+                                                              const float* __restrict__ br, const float* __restrict__ mask,
+                                                              float* __restrict__ y, float* __restrict__ log_det,
+                                                              int64_t B, int d, int dir, int accumulate) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    float ld = 0.f;
+    for (int j = 0; j < d; ++j) {
+        const float m = mask[j], om = 1.f - m, xv = x[s * d + j];
+        const float sv = tclamp(sr[s * d + j], -10.f, 10.f), bv = tclamp(br[s * d + j], -10.f, 10.f);
+        float t;
+        if (dir > 0) {
+            t = xv * exp_fast(sv) + bv;
+            ld = ld + om * sv;
+        } else {
+            t = (xv - bv) * exp_fast(-sv);
+            ld = ld + om * (-sv);
+        }
+        const float v = xv * m + om * t;
+        y[s * d + j] = nonfinite(v) ? 0.f : v;
+    }
+    if (nonfinite(ld)) ld = 0.f;
+    log_det[s] = accumulate ? log_det[s] + ld : ld;
+}
+
+// Its adjoint: gs, gb = dL/d(raw net outputs), gx = the direct dL/dx term.
+__global__ __launch_bounds__(256) void affine_elem_bwd_kernel(const float* __restrict__ x, const float* __restrict__ sr,
+                                                              const float* __restrict__ br, const float* __restrict__ mask,
+                                                              const float* __restrict__ gy, const float* __restrict__ gld,
+                                                              float* __restrict__ gs, float* __restrict__ gb,
+                                                              float* __restrict__ gx, int64_t B, int d, int dir) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    float ld = 0.f;
+    for (int j = 0; j < d; ++j) {
+        const float om = 1.f - mask[j], sv = tclamp(sr[s * d + j], -10.f, 10.f);
+        ld = ld + om * (dir > 0 ? sv : -sv);
+    }
+    const float gl = (gld && !nonfinite(ld)) ? gld[s] : 0.f;
+    for (int j = 0; j < d; ++j) {
+        const float m = mask[j], om = 1.f - m, xv = x[s * d + j];
+        const float s0 = sr[s * d + j], b0 = br[s * d + j];
+        const float sv = tclamp(s0, -10.f, 10.f), bv = tclamp(b0, -10.f, 10.f);
+        const bool sin = s0 >= -10.f && s0 <= 10.f, bin = b0 >= -10.f && b0 <= 10.f;
+        const float g = gy ? gy[s * d + j] : 0.f;
+        float v, e, dts, dtb;
+        if (dir > 0) {
+            e = exp_fast(sv);
+            v = xv * m + om * (xv * e + bv);
+            dts = xv * e;
+            dtb = 1.f;
+        } else {
+            e = exp_fast(-sv);
+            v = xv * m + om * ((xv - bv) * e);
+            dts = -((xv - bv) * e);
+            dtb = -e;
+        }
+        const float gv = nonfinite(v) ? 0.f : g;
+        const float gvo = gv * om;
+        gs[s * d + j] = sin ? gvo * dts + (dir > 0 ? gl * om : -(gl * om)) : 0.f;
+        gb[s * d + j] = bin ? gvo * dtb : 0.f;
+        gx[s * d + j] = gv * m + gvo * e;
+    }
+}
+
+// ---- BatchNorm1d of a conditioner (coupling_layer.py:18-35), any H --------------------------
+// prepare: per-feature mean / invstd from the batch moments (train: float64 (n, mean, M2) triples
+// from nfx_flowbn_moments, SyncBN-merged; the running statistics updated with the unbiased
+// variance, as torch) or from the running statistics (eval); scale = gamma invstd,
+// shift = beta - mean scale, so BN(z) = z scale + shift.
+__global__ void bn_prepare_kernel(const double* __restrict__ stats, const float* __restrict__ gamma,
+                                  const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+                                  double eps, double momentum, int update, int N, float* __restrict__ mean_o,
+                                  float* __restrict__ invstd_o, float* __restrict__ scale_o, float* __restrict__ shift_o) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    double mean, var;
+    if (stats) {
+        const double cnt = stats[3 * n], m2 = stats[3 * n + 2];
+        mean = stats[3 * n + 1];
+        var = cnt > 0 ? m2 / cnt : 0.0;
+        if (update) {
+            const double unb = cnt > 1 ? m2 / (cnt - 1) : var;
+            rmean[n] = (float)((1.0 - momentum) * (double)rmean[n] + momentum * mean);
+            rvar[n] = (float)((1.0 - momentum) * (double)rvar[n] + momentum * unb);
+        }
+    } else {
+        mean = (double)rmean[n];
+        var = (double)rvar[n];
+    }
+    const float inv = (float)(1.0 / sqrt(var + eps));
+    const float mf = (float)mean;
+    const float sc = gamma[n] * inv;
+    mean_o[n] = mf;
+    invstd_o[n] = inv;
+    scale_o[n] = sc;
+    shift_o[n] = beta[n] - mf * sc;
+}
+
+// h = relu(z scale + shift) over [M][N]
+__global__ void bn_apply_relu_kernel(const float* __restrict__ z, const float* __restrict__ scale,
+                                     const float* __restrict__ shift, float* __restrict__ h, int64_t M, int N) {
+    const int64_t total = M * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int n = (int)(i % N);
+        h[i] = trelu(z[i] * scale[n] + shift[n]);
+    }
+}
+
+// Backward sums over rows z: part[z][0][n] = sum g, part[z][1][n] = sum g (zv - mean) invstd (float64)
+__global__ __launch_bounds__(256) void bn_bwd_sums_kernel(const float* __restrict__ g, const float* __restrict__ zv,
+                                                          const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                          int64_t M, int N, int64_t rchunk, double* __restrict__ part) {
+    __shared__ double red[2][8][33];
+    const int cx = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    const int n = blockIdx.x * 32 + cx;
+    const int64_t rb = (int64_t)blockIdx.y * rchunk, re = rb + rchunk < M ? rb + rchunk : M;
+    double a = 0.0, b = 0.0;
+    if (n < N) {
+        const float mu = mean[n], is = invstd[n];
+        for (int64_t m = rb + rg; m < re; m += 8) {
+            const float gv = g[m * N + n];
+            a += (double)gv;
+            b += (double)(gv * ((zv[m * N + n] - mu) * is));
+        }
+    }
+    red[0][rg][cx] = a;
+    red[1][rg][cx] = b;
+    __syncthreads();
+    if (rg == 0 && n < N) {
+        double sa = 0.0, sb = 0.0;
+        for (int q = 0; q < 8; ++q) {
+            sa += red[0][q][cx];
+            sb += red[1][q][cx];
+        }
+        part[((int64_t)blockIdx.y * 2 + 0) * N + n] = sa;
+        part[((int64_t)blockIdx.y * 2 + 1) * N + n] = sb;
+    }
+}
+
+__global__ void reduce_f64_kernel(const double* __restrict__ part, int64_t nz, int64_t n, double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double v = 0.0;
+        for (int64_t z = 0; z < nz; ++z) v += part[z * n + i];
+        out[i] = v;
+    }
+}
+
+// g_z = gamma invstd g (eval) or gamma invstd (g - sum g / cnt - xhat sum(g xhat) / cnt) (train)
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ zv,
+                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                    const float* __restrict__ gamma, const double* __restrict__ sums,
+                                    const double* __restrict__ count, int train, float* __restrict__ gz, int64_t M, int N) {
+    const int64_t total = M * N;
+    const double cnt = train ? *count : 1.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int n = (int)(i % N);
+        const float k = gamma[n] * invstd[n];
+        float v = g[i];
+        if (train) {
+            const float xh = (zv[i] - mean[n]) * invstd[n];
+            v = v - (float)(sums[n] / cnt) - xh * (float)(sums[N + n] / cnt);
+        }
+        gz[i] = v * k;
+    }
+}
+
 }  // namespace nfx
 
 using namespace nfx;
@@ -658,4 +830,96 @@ extern "C" int nfx_made_elem_seq_backward(const float* x, const float* params, c
     made_elem_seq_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, work, lam, gy, gld,
                                                                                           out, B, d, variant, mode);
     return check_launch("made_elem_seq_bwd_kernel");
+}
+
+static unsigned elem_grid(int64_t n) {
+    const int64_t b = (n + 255) / 256;
+    return (unsigned)(b < 65536 ? (b < 1 ? 1 : b) : 65536);
+}
+
+extern "C" int nfx_affine_elem_forward(const float* x, const float* s_raw, const float* b_raw, const float* mask,
+                                       float* y, float* log_det, int64_t B, int d, int direction, int accumulate,
+                                       void* stream) {
+    int rc = made_elem_check(B, d, "affine_elem_forward");
+    if (rc) return rc;
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "affine_elem_forward: direction");
+    if (B == 0) return NFX_OK;
+    if (!x || !s_raw || !b_raw || !mask || !y || !log_det) return set_error(NFX_EINVAL, "affine_elem_forward: null pointer");
+    affine_elem_fwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, s_raw, b_raw, mask, y, log_det,
+                                                                                        B, d, direction, accumulate);
+    return check_launch("affine_elem_fwd_kernel");
+}
+
+extern "C" int nfx_affine_elem_backward(const float* x, const float* s_raw, const float* b_raw, const float* mask,
+                                        const float* gy, const float* gld, float* gs, float* gb, float* gx, int64_t B,
+                                        int d, int direction, void* stream) {
+    int rc = made_elem_check(B, d, "affine_elem_backward");
+    if (rc) return rc;
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "affine_elem_backward: direction");
+    if (B == 0) return NFX_OK;
+    if (!x || !s_raw || !b_raw || !mask || !gs || !gb || !gx) return set_error(NFX_EINVAL, "affine_elem_backward: null pointer");
+    affine_elem_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, s_raw, b_raw, mask, gy, gld, gs,
+                                                                                        gb, gx, B, d, direction);
+    return check_launch("affine_elem_bwd_kernel");
+}
+
+extern "C" int nfx_bn_prepare(const double* stats, const float* gamma, const float* beta, float* running_mean,
+                              float* running_var, double eps, double momentum, int update_running, int N, float* mean,
+                              float* invstd, float* scale, float* shift, void* stream) {
+    if (N <= 0) return set_error(NFX_EINVAL, "bn_prepare: N=%d", N);
+    if (!gamma || !beta || !running_mean || !running_var || !mean || !invstd || !scale || !shift)
+        return set_error(NFX_EINVAL, "bn_prepare: null pointer");
+    bn_prepare_kernel<<<(N + 255) / 256, 256, 0, (hipStream_t)stream>>>(stats, gamma, beta, running_mean, running_var, eps,
+                                                                         momentum, stats ? update_running : 0, N, mean,
+                                                                         invstd, scale, shift);
+    return check_launch("bn_prepare_kernel");
+}
+
+extern "C" int nfx_bn_apply_relu(const float* z, const float* scale, const float* shift, float* h, int64_t M, int N,
+                                 void* stream) {
+    if (M < 0 || N <= 0) return set_error(NFX_EINVAL, "bn_apply_relu: bad shape");
+    if (M == 0) return NFX_OK;
+    if (!z || !scale || !shift || !h) return set_error(NFX_EINVAL, "bn_apply_relu: null pointer");
+    bn_apply_relu_kernel<<<elem_grid(M * N), 256, 0, (hipStream_t)stream>>>(z, scale, shift, h, M, N);
+    return check_launch("bn_apply_relu_kernel");
+}
+
+extern "C" size_t nfx_bn_workspace_bytes(int64_t M, int N) {
+    if (M <= 0 || N <= 0) return 0;
+    int64_t cs = (M + 4095) / 4096;
+    if (cs > 1024) cs = 1024;
+    return (size_t)(cs * 2 * (int64_t)N * sizeof(double));
+}
+
+extern "C" int nfx_bn_backward_sums(const float* g, const float* z, const float* mean, const float* invstd, double* sums,
+                                    int64_t M, int N, void* workspace, void* stream) {
+    if (M < 0 || N <= 0) return set_error(NFX_EINVAL, "bn_backward_sums: bad shape");
+    if (!sums) return set_error(NFX_EINVAL, "bn_backward_sums: null sums");
+    hipStream_t s = (hipStream_t)stream;
+    if (M == 0) {
+        (void)hipMemsetAsync(sums, 0, 2 * (size_t)N * sizeof(double), s);
+        return check_launch("bn_backward_sums(memset)");
+    }
+    if (!g || !z || !mean || !invstd || !workspace) return set_error(NFX_EINVAL, "bn_backward_sums: null pointer");
+    int64_t cs = (M + 4095) / 4096;
+    if (cs > 1024) cs = 1024;
+    const int64_t rchunk = (M + cs - 1) / cs, nz = (M + rchunk - 1) / rchunk;
+    double* part = reinterpret_cast<double*>(workspace);
+    bn_bwd_sums_kernel<<<dim3((unsigned)((N + 31) / 32), (unsigned)nz), 256, 0, s>>>(g, z, mean, invstd, M, N, rchunk, part);
+    int rc = check_launch("bn_bwd_sums_kernel");
+    if (rc) return rc;
+    reduce_f64_kernel<<<(unsigned)((2 * N + 255) / 256), 256, 0, s>>>(part, nz, 2 * (int64_t)N, sums);
+    return check_launch("reduce_f64_kernel");
+}
+
+extern "C" int nfx_bn_backward_apply(const float* g, const float* z, const float* mean, const float* invstd,
+                                     const float* gamma, const double* sums, const double* count, int train, float* gz,
+                                     int64_t M, int N, void* stream) {
+    if (M < 0 || N <= 0) return set_error(NFX_EINVAL, "bn_backward_apply: bad shape");
+    if (M == 0) return NFX_OK;
+    if (!g || !gamma || !invstd || !gz || (train && (!z || !mean || !sums || !count)))
+        return set_error(NFX_EINVAL, "bn_backward_apply: null pointer");
+    bn_bwd_apply_kernel<<<elem_grid(M * N), 256, 0, (hipStream_t)stream>>>(g, z, mean, invstd, gamma, sums, count, train,
+                                                                          gz, M, N);
+    return check_launch("bn_bwd_apply_kernel");
 }

@@ -26,6 +26,7 @@ import torch.nn as nn
 
 from .. import _lib
 from .. import distributed as _dist
+from . import generic as _generic
 from .flow import HipFlow, STATS
 
 MAX_D = 64          # eval kernels: affine_coupling_kernel (d <= 8) / affine_wide_kernel (d <= 64)
@@ -41,12 +42,16 @@ TRAIN_EVENTS = None
 # One-launch layer chains (nfx_affine_chain, csrc/nfx_affine_chain.hip) are used for batches up to
 # this many samples; above it the per-layer streaming kernels (higher MFMA efficiency) run.
 CHAIN_MAX_B = int(os.environ.get("NFX_CHAIN_MAX_B", str(1 << 16)))
+# Tests: route every call through the any-shape path (csrc/nfx_generic.hip) even where a fused
+# kernel exists, to pin it against the same fixtures.
+FORCE_GENERIC = False
+GENERIC_MAX_H = 1024  # conditioner BatchNorm moments (nfx_flowbn_moments): <= 1024 features
 
 
 def chain_ok(flows, x):
     """A run of eval-mode CouplingLayers with one (d, H), d in {2, 4, 8}, H <= 128, on fp32 ROCm
     rows, small enough for the one-launch chain kernel."""
-    if not flows or len(flows) > 64 or x.shape[0] > CHAIN_MAX_B or x.shape[0] == 0:
+    if FORCE_GENERIC or not flows or len(flows) > 64 or x.shape[0] > CHAIN_MAX_B or x.shape[0] == 0:
         return False
     f0 = flows[0]
     if not isinstance(f0, CouplingLayer):
@@ -170,8 +175,157 @@ class CouplingLayer(HipFlow):
         if any(not bn.affine or not bn.track_running_stats or bn.momentum is None or bn.running_mean is None
                for bn in bns):
             return False
-        d, H = self.data_dim, self._hidden()
-        return x.shape[1] == d and d <= MAX_D_TRAIN and H <= MAX_H_TRAIN and x.shape[0] >= 2
+        return x.shape[1] == self.data_dim and x.shape[0] >= 2 and (self._fused_train() or self._hidden() <= GENERIC_MAX_H)
+
+    def _fused_train(self):
+        """Shapes of the fused train-mode / backward kernels (affine_train*_kernel); others run the
+        any-shape path (GEMM conditioner, BatchNorm and affine element kernels)."""
+        return not FORCE_GENERIC and self.data_dim <= MAX_D_TRAIN and self._hidden() <= MAX_H_TRAIN
+
+    def _fused_family(self):
+        """Shapes of the fused eval kernels (affine_coupling_kernel / affine_wide_kernel)."""
+        return not FORCE_GENERIC and self.data_dim <= MAX_D and self._hidden() <= MAX_H
+
+    # -- any-shape path (csrc/nfx_generic.hip) ---------------------------------------------------
+    def _generic_nets(self):
+        return [(n[0], n[1], n[3], n[4], n[6]) for n in (self.s_net, self.b_net)]
+
+    def _generic_bn_eval(self, device):
+        """Per conditioner BatchNorm [4][H] = (mean, invstd, scale, shift) from the running
+        statistics (nfx_bn_prepare), cached with the parameters."""
+        L = _lib.lib()
+        H = self._hidden()
+        out = []
+        for _, bn1, _, bn2, _ in self._generic_nets():
+            for bn in (bn1, bn2):
+                t = torch.empty(4, H, device=device, dtype=torch.float32)
+                _lib.check(L.nfx_bn_prepare(None, _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()),
+                                            _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var), float(bn.eps), 0.0,
+                                            0, H, _lib.ptr(t[0]), _lib.ptr(t[1]), _lib.ptr(t[2]), _lib.ptr(t[3]),
+                                            _lib.stream_of(t)), "nfx_bn_prepare")
+                out.append(t)
+        return out
+
+    def _mask_dev(self, device):
+        return self.mask.detach().to(device=device, dtype=torch.float32).contiguous()
+
+    def _generic_launch(self, x, out, log_det, direction, accumulate):
+        mask = self._mask_dev(x.device)
+        bnp = self._packed(x.device, self._generic_bn_eval, slot="_nfx_generic_pack_cache")
+        raw = []
+        for i, (l1, _, l2, _, l3) in enumerate(self._generic_nets()):
+            p1, p2 = bnp[2 * i], bnp[2 * i + 1]
+            h1 = _generic.linear_forward(x, l1, in_scale=mask, relu=True, post=(p1[2], p1[3]))
+            h2 = _generic.linear_forward(h1, l2, relu=True, post=(p2[2], p2[3]))
+            raw.append(_generic.linear_forward(h2, l3))
+        _lib.check(_lib.lib().nfx_affine_elem_forward(
+            _lib.ptr(x), _lib.ptr(raw[0]), _lib.ptr(raw[1]), _lib.ptr(mask), _lib.ptr(out), _lib.ptr(log_det),
+            x.shape[0], self.data_dim, int(direction), int(bool(accumulate)), _lib.stream_of(x)),
+            "nfx_affine_elem_forward")
+
+    def _generic_acts(self, x, mask, bnp):
+        """Conditioner recompute with given BatchNorm (mean, invstd, scale, shift): per net
+        (z1, h1, z2, h2, raw output)."""
+        L = _lib.lib()
+        B, H = x.shape[0], self._hidden()
+        acts = []
+        for i, (l1, _, l2, _, l3) in enumerate(self._generic_nets()):
+            z1 = _generic.linear_forward(x, l1, in_scale=mask)
+            h1 = torch.empty_like(z1)
+            _lib.check(L.nfx_bn_apply_relu(_lib.ptr(z1), _lib.ptr(bnp[2 * i][2]), _lib.ptr(bnp[2 * i][3]),
+                                           _lib.ptr(h1), B, H, _lib.stream_of(x)), "nfx_bn_apply_relu")
+            z2 = _generic.linear_forward(h1, l2)
+            h2 = torch.empty_like(z2)
+            _lib.check(L.nfx_bn_apply_relu(_lib.ptr(z2), _lib.ptr(bnp[2 * i + 1][2]), _lib.ptr(bnp[2 * i + 1][3]),
+                                           _lib.ptr(h2), B, H, _lib.stream_of(x)), "nfx_bn_apply_relu")
+            acts.append((z1, h1, z2, h2, _generic.linear_forward(h2, l3)))
+        return acts
+
+    def _generic_train_forward(self, x, direction):
+        """Train mode on the any-shape path: per conditioner BatchNorm the batch moments
+        (nfx_flowbn_moments, SyncBN-merged), mean/invstd/scale/shift and the running update
+        (nfx_bn_prepare), then the affine element map. Returns (y, ld, bnp, counts)."""
+        L = _lib.lib()
+        x = x.detach().contiguous()
+        B, d = x.shape
+        H = self._hidden()
+        dev = x.device
+        st = _lib.stream_of(x)
+        p = _lib.ptr
+        mask = self._mask_dev(dev)
+        ws = torch.empty(max(1, L.nfx_flowbn_workspace_bytes(B, H)), device=dev, dtype=torch.uint8)
+        bnp, counts, raw = [], [], []
+        for l1, bn1, l2, bn2, l3 in self._generic_nets():
+            h = x
+            for lin, bn, first in ((l1, bn1, True), (l2, bn2, False)):
+                z = _generic.linear_forward(h, lin, in_scale=mask if first else None)
+                stats = torch.empty(H, 3, device=dev, dtype=torch.float64)
+                _lib.check(L.nfx_flowbn_moments(p(z), B, H, p(stats), p(ws), st), "nfx_flowbn_moments")
+                _dist.merge_bn_stats(stats)
+                t = torch.empty(4, H, device=dev, dtype=torch.float32)
+                _lib.check(L.nfx_bn_prepare(p(stats), p(bn.weight.detach()), p(bn.bias.detach()), p(bn.running_mean),
+                                            p(bn.running_var), float(bn.eps), float(bn.momentum), 1, H, p(t[0]),
+                                            p(t[1]), p(t[2]), p(t[3]), st), "nfx_bn_prepare")
+                torch.autograd.graph.increment_version(bn.running_mean)
+                torch.autograd.graph.increment_version(bn.running_var)
+                h = torch.empty_like(z)
+                _lib.check(L.nfx_bn_apply_relu(p(z), p(t[2]), p(t[3]), p(h), B, H, st), "nfx_bn_apply_relu")
+                bnp.append(t)
+                counts.append(stats)  # stats[0, 0] = the global sample count
+            raw.append(_generic.linear_forward(h, l3))
+        bns = [self.s_net[1], self.s_net[4], self.b_net[1], self.b_net[4]]
+        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
+        y = torch.empty_like(x)
+        ld = torch.empty(B, device=dev, dtype=torch.float32)
+        _lib.check(L.nfx_affine_elem_forward(p(x), p(raw[0]), p(raw[1]), p(mask), p(y), p(ld), B, d, int(direction), 0,
+                                             st), "nfx_affine_elem_forward")
+        return y, ld, bnp, counts
+
+    def _generic_backward(self, x, gy, gld, direction, bnp, counts):
+        """dL/dx and the parameter gradients (parameters() order) on the any-shape path: the
+        conditioner recomputed with the call's BatchNorm normalisation, the affine element adjoint,
+        then per net the Linear / BatchNorm / ReLU backward (train: batch-statistics BatchNorm
+        backward with SyncBN-summed float64 sums; counts = None: eval, running statistics)."""
+        L = _lib.lib()
+        B, d = x.shape
+        H = self._hidden()
+        st = _lib.stream_of(x)
+        p = _lib.ptr
+        mask = self._mask_dev(x.device)
+        acts = self._generic_acts(x, mask, bnp)
+        gs, gb, gx = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+        _lib.check(L.nfx_affine_elem_backward(p(x), p(acts[0][4]), p(acts[1][4]), p(mask), p(gy), p(gld), p(gs), p(gb),
+                                              p(gx), B, d, int(direction), st), "nfx_affine_elem_backward")
+        ws = torch.empty(max(1, L.nfx_bn_workspace_bytes(B, H)), device=x.device, dtype=torch.uint8)
+        train = counts is not None
+        grads = []
+        for i, ((l1, bn1, l2, bn2, l3), g_out) in enumerate(zip(self._generic_nets(), (gs, gb))):
+            z1, h1, z2, h2, _ = acts[i]
+            w3 = _generic.linear_backward_weight(g_out, h2, l3)
+            g = _generic.linear_backward_data(g_out, l3, act=h2)
+            per = []
+            for z, hin, lin, bn, k in ((z2, h1, l2, bn2, 2 * i + 1), (z1, x, l1, bn1, 2 * i)):
+                t = bnp[k]
+                sums = torch.empty(2, H, device=x.device, dtype=torch.float64)
+                _lib.check(L.nfx_bn_backward_sums(p(g), p(z), p(t[0]), p(t[1]), p(sums), B, H, p(ws), st),
+                           "nfx_bn_backward_sums")
+                if train:
+                    _dist.allreduce_bn_sums(sums)
+                gz = torch.empty_like(g)
+                # train: the global sample count = n of the merged moments triple (device float64)
+                _lib.check(L.nfx_bn_backward_apply(p(g), p(z), p(t[0]), p(t[1]), p(bn.weight.detach()), p(sums),
+                                                   p(counts[k]) if train else None, int(train), p(gz), B, H, st),
+                           "nfx_bn_backward_apply")
+                first = lin is l1
+                wl = _generic.linear_backward_weight(gz, hin, lin, in_scale=mask if first else None)
+                if first:
+                    _generic.linear_backward_data(gz, lin, out_scale=mask, out=gx)
+                else:
+                    g = _generic.linear_backward_data(gz, lin, act=hin)
+                per.append((wl, sums[1].float(), sums[0].float()))
+            (w2, dg2, db2), (w1, dg1, db1) = per
+            grads += [w1[0], w1[1], dg1, db1, w2[0], w2[1], dg2, db2, w3[0], w3[1]]
+        return gx, grads
 
     def _dispatch(self, x, direction):
         if self._train_ok(x):
@@ -190,6 +344,8 @@ class CouplingLayer(HipFlow):
     def _train_forward(self, x, direction):
         """Batch statistics (2 passes, SyncBN merge between them), the fused layer with the
         statistics folded in, running-statistics update. Returns (y, ld, tpack, stats)."""
+        if not self._fused_train():
+            return self._generic_train_forward(x, direction)
         L = _lib.lib()
         x = x.detach().contiguous()
         B, d = x.shape
@@ -254,7 +410,7 @@ class CouplingLayer(HipFlow):
             return False
         if any(bn.training or not bn.affine or bn.running_mean is None for bn in bns):
             return False
-        return x.shape[1] == self.data_dim and self.data_dim <= MAX_D_TRAIN and self._hidden() <= MAX_H_TRAIN
+        return x.shape[1] == self.data_dim  # fused (d <= 8, H <= 128) or the any-shape path
 
     def _build_eval_backward_pack(self, device):
         L = _lib.lib()
@@ -275,6 +431,12 @@ class CouplingLayer(HipFlow):
         return tpack, stats
 
     def _hip_backward(self, x, gy, gld, direction):
+        if not self._fused_train():
+            x = x.contiguous()
+            gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
+            gld = torch.zeros(x.shape[0], device=x.device) if gld is None else gld.contiguous().float()
+            bnp = self._packed(x.device, self._generic_bn_eval, slot="_nfx_generic_pack_cache")
+            return self._generic_backward(x, gy, gld, direction, bnp, None)
         tpack, stats = self._packed(x.device, self._build_eval_backward_pack, slot="_nfx_evalbwd_pack_cache")
         return self._train_backward(x, gy, gld, direction, tpack, stats, sync=False)
 
@@ -289,6 +451,8 @@ class CouplingLayer(HipFlow):
         st = _lib.stream_of(x)
         gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
         gld = torch.zeros(B, device=dev) if gld is None else gld.contiguous().float()
+        if not self._fused_train():  # tpack, stats = the any-shape path's (bnp, counts)
+            return self._generic_backward(x, gy, gld, direction, tpack, stats)
         G = torch.empty(L.nfx_affine_train_grad_doubles(d, H), device=dev, dtype=torch.float64)
         gx = torch.empty_like(x)
         ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
@@ -321,12 +485,10 @@ class CouplingLayer(HipFlow):
         return gx, out
 
     def _hip_supported(self, x):
-        d, H = self.data_dim, self._hidden()
+        d = self.data_dim
         if x.dim() != 2 or x.shape[1] != d:
             return False, f"input shape {tuple(x.shape)} vs data_dim={d}"
-        if d > MAX_D or H > MAX_H:
-            return False, f"d={d} (<= {MAX_D}) H={H} (<= {MAX_H})"
-        return True, ""
+        return True, ""  # beyond the fused family: the any-shape path (_generic_launch)
 
     def _build_pack(self, device):
         d, H = self.data_dim, self._hidden()
@@ -344,6 +506,8 @@ class CouplingLayer(HipFlow):
         return packed
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
+        if not self._fused_family():
+            return self._generic_launch(x, out, log_det, direction, accumulate)
         packed = self._packed(x.device, self._build_pack)
         _lib.check(_lib.lib().nfx_affine_coupling(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), x.shape[0],
@@ -351,6 +515,8 @@ class CouplingLayer(HipFlow):
             _lib.stream_of(x)), "nfx_affine_coupling")
 
     def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
+        if not self._fused_family():
+            return False
         packed = self._packed(x.device, self._build_pack)
         _lib.check(_lib.lib().nfx_affine_coupling_logprob(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), _lib.ptr(logp),
