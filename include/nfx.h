@@ -453,6 +453,16 @@ int nfx_bn_backward_sums(const float* g, const float* z, const float* mean, cons
 int nfx_bn_backward_apply(const float* g, const float* z, const float* mean, const float* invstd,
                           const float* gamma, const double* sums, const double* count, int train, float* gz,
                           int64_t M, int N, void* stream);
+/* ARQS at any (d, H) and its backward (arqs.py:44-114, rational_quadratic_spline.py:4-104):
+ * one sequential step i on params = MADE(state) [B][d (3K-1)] (viewed [B, d, 3K-1] like the
+ * reference). mode 0: state[:, i] = spline(xr[:, i]) with params row i, log_det += its log-det;
+ * mode 1 (reverse): with lam [B][d] = dL/d(state after step i) and gld the log-det gradient,
+ * gparams row i = dL/d(params row i) (row i + 1 zeroed), gx[:, i] = dL/dxr[:, i], lam[:, i] = 0
+ * (the caller adds the MADE-input VJP of gparams into lam); mode 2: state[:, i] = 0.
+ * 2 <= K <= 11, data_min/data_max None. */
+int nfx_arqs_step(const float* xr, const float* params, float* state, float* log_det, const float* gld, float* lam,
+                  float* gparams, float* gx, int64_t B, int d, int K, int i, int direction, int mode,
+                  float min_bin_width, float min_bin_height, float min_derivative, void* stream);
 /* SplineCouplingLayer element math for any d (spline_coupling_layer.py:96-180 with the spline
  * of :182-309): params [B][d][3K-1] = param_net output; dims with mask == 0 go through the RQ
  * spline (forward: direction +1, inverse: -1), the rest pass through; layer guards and the

@@ -21,6 +21,7 @@
 #include <cstdlib>
 
 #include "nfx_common.h"
+#include "nfx_rqs_unit.h"           // rqs_unit_eval, rqs_unit_adjoint (ARQS)
 #include "nfx_spline_bwd_kernel.h"  // rq_spline_adjoint
 #include "nfx_spline_kernel.h"      // rq_spline_elem, SplineConsts
 
@@ -622,6 +623,77 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ g, const float* __
     }
 }
 
+// ---- ARQS (arqs.py:44-114), one sequential step at a time --------------------------------
+// params [B][d * R] = MADE(state) viewed [B, d, R] (R = 3K-1); row i = (widths | heights |
+// inner derivatives) of coordinate i. mode 0: forward step — state[:, i] = spline(xr[:, i]),
+// ld += log-det (the reference's x_new[:, i] / log_det_jacobian +=); mode 1: reverse step —
+// with lam = dL/d(state after step i): dL/d(row i) into gprm (row i + 1 of the previous reverse
+// step zeroed), dL/dx[:, i] into gx, lam[:, i] = 0 (the column was overwritten; the MADE-input
+// VJP is added by the caller); mode 2: state[:, i] = 0 (the state before step i).
+struct RqsConsts {
+    float min_w, cw, min_h, ch, min_d;
+};
+
+template <int K, bool INV>
+__global__ __launch_bounds__(256) void arqs_step_kernel(const float* __restrict__ xr, const float* __restrict__ prm,
+                                                        float* __restrict__ state, float* __restrict__ ld,
+                                                        const float* __restrict__ gld, float* __restrict__ lam,
+                                                        float* __restrict__ gprm, float* __restrict__ gx, int64_t B,
+                                                        int d, int i, int mode, const RqsConsts C) {
+    constexpr int R = 3 * K - 1;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    if (mode == 2) {
+        state[s * d + i] = 0.f;
+        return;
+    }
+    const float* p = prm + (s * d + i) * R;
+    float uw[K], uh[K], ud[K - 1];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uw[k] = p[k];
+        uh[k] = p[K + k];
+    }
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) ud[k] = p[2 * K + k];
+    const float xv = xr[s * d + i];
+    float o, l;
+    if (mode == 0) {
+        rqs_unit_eval<K, INV>(xv, uw, uh, ud, C.min_w, C.cw, C.min_h, C.ch, C.min_d, o, l);
+        state[s * d + i] = o;
+        ld[s] = ld[s] + l;
+        return;
+    }
+    float g, guw[K], guh[K], gud[K - 1];
+    rqs_unit_adjoint<K, INV>(xv, uw, uh, ud, C.min_w, C.cw, C.min_h, C.ch, C.min_d, lam[s * d + i],
+                             gld ? gld[s] : 0.f, o, l, g, guw, guh, gud);
+    float* gp = gprm + (s * d + i) * R;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        gp[k] = guw[k];
+        gp[K + k] = guh[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) gp[2 * K + k] = gud[k];
+    if (i + 1 < d) {
+#pragma unroll
+        for (int t = 0; t < R; ++t) gp[R + t] = 0.f;
+    }
+    gx[s * d + i] = g;
+    lam[s * d + i] = 0.f;
+}
+
+static const void* arqs_step_pick(int K, bool inv) {
+#define NFX_AS(k) \
+    case k:       \
+        return inv ? (const void*)arqs_step_kernel<k, true> : (const void*)arqs_step_kernel<k, false>;
+    switch (K) {
+        NFX_AS(2) NFX_AS(3) NFX_AS(4) NFX_AS(5) NFX_AS(6) NFX_AS(7) NFX_AS(8) NFX_AS(9) NFX_AS(10) NFX_AS(11)
+    }
+#undef NFX_AS
+    return nullptr;
+}
+
 }  // namespace nfx
 
 using namespace nfx;
@@ -922,4 +994,30 @@ extern "C" int nfx_bn_backward_apply(const float* g, const float* z, const float
     bn_bwd_apply_kernel<<<elem_grid(M * N), 256, 0, (hipStream_t)stream>>>(g, z, mean, invstd, gamma, sums, count, train,
                                                                           gz, M, N);
     return check_launch("bn_bwd_apply_kernel");
+}
+
+extern "C" int nfx_arqs_step(const float* xr, const float* params, float* state, float* log_det, const float* gld,
+                             float* lam, float* gparams, float* gx, int64_t B, int d, int K, int i, int direction,
+                             int mode, float min_bin_width, float min_bin_height, float min_derivative, void* stream) {
+    int rc = made_elem_check(B, d, "arqs_step");
+    if (rc) return rc;
+    if (K < 2 || K > 11) return set_error(NFX_EUNSUPPORTED, "arqs_step: K=%d outside 2..11", K);
+    if (i < 0 || i >= d) return set_error(NFX_EINVAL, "arqs_step: step %d outside 0..%d", i, d - 1);
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "arqs_step: direction");
+    if (mode < 0 || mode > 2) return set_error(NFX_EINVAL, "arqs_step: mode %d", mode);
+    if (B == 0) return NFX_OK;
+    if (!state || (mode != 2 && (!xr || !params)) || (mode == 0 && !log_det) || (mode == 1 && (!lam || !gparams || !gx)))
+        return set_error(NFX_EINVAL, "arqs_step: null pointer");
+    RqsConsts C;
+    C.min_w = min_bin_width;
+    C.cw = (float)(1.0 - (double)min_bin_width * K);
+    C.min_h = min_bin_height;
+    C.ch = (float)(1.0 - (double)min_bin_height * K);
+    C.min_d = min_derivative;
+    typedef void (*ak)(const float*, const float*, float*, float*, const float*, float*, float*, float*, int64_t, int, int,
+                       int, const RqsConsts);
+    ak k = (ak)arqs_step_pick(K, direction < 0);
+    k<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(xr, params, state, log_det, gld, lam, gparams, gx, B,
+                                                                     d, i, mode, C);
+    return check_launch("arqs_step_kernel");
 }

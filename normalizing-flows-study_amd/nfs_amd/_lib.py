@@ -55,7 +55,7 @@ EXPORTED_SYMBOLS = (
     "nfx_made_elem_forward", "nfx_made_elem_step", "nfx_made_elem_finish", "nfx_made_elem_backward",
     "nfx_made_elem_seq_backward",
     "nfx_affine_elem_forward", "nfx_affine_elem_backward", "nfx_bn_prepare", "nfx_bn_apply_relu",
-    "nfx_bn_workspace_bytes", "nfx_bn_backward_sums", "nfx_bn_backward_apply",
+    "nfx_bn_workspace_bytes", "nfx_bn_backward_sums", "nfx_bn_backward_apply", "nfx_arqs_step",
 )
 
 
@@ -111,6 +111,8 @@ _SIGNATURES = {
     "nfx_bn_prepare": (_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _int, _int, _vp, _vp, _vp,
                               _vp, _vp]),
     "nfx_bn_apply_relu": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _vp]),
+    "nfx_arqs_step": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _int, _f, _f, _f,
+                             _vp]),
     "nfx_bn_workspace_bytes": (_sz, [_i64, _int]),
     "nfx_bn_backward_sums": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _vp, _vp]),
     "nfx_bn_backward_apply": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _i64, _int, _vp]),

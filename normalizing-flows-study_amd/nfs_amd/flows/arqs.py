@@ -13,12 +13,16 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from . import generic as _generic
 from .autoregressive import MADE
 from .flow import HipFlow
 from .spline import _rqs_unit_torch
 
 MAX_K = 11   # 3K-1 <= 32: one MFMA row tile of spline parameters per step
 MAX_H = 128
+# Tests: route every call through the any-shape path (csrc/nfx_generic.hip) even where the fused
+# ARQS kernel exists, to pin it against the same fixtures.
+FORCE_GENERIC = False
 
 
 class ARQS(HipFlow):
@@ -85,11 +89,55 @@ class ARQS(HipFlow):
         d, H, K = self.dim, self.conditioner.hidden_dim, self.num_bins
         if x.dim() != 2 or x.shape[1] != d:
             return False, f"input shape {tuple(x.shape)} vs dim={d}"
-        if H > MAX_H or K > MAX_K or K < 2:
-            return False, f"H={H} (<= {MAX_H}) K={K} (2..{MAX_K})"
+        if K > MAX_K or K < 2:
+            return False, f"K={K} (2..{MAX_K})"
         if self._rescale_scalars() is None:
             return False, "per-dimension data_min/data_max tensors"
+        if not self._fused_family() and not self._generic_ok():
+            return False, f"H={H} > {MAX_H} needs data_min/data_max None (any-shape path)"
         return True, ""
+
+    def _fused_family(self):
+        """Shapes of the fused ARQS kernel (nfx_arqs*.hip: H <= 128)."""
+        return not FORCE_GENERIC and self.conditioner.hidden_dim <= MAX_H
+
+    def _generic_ok(self):
+        return 2 <= self.num_bins <= MAX_K and (self.data_min is None or self.data_max is None)
+
+    # -- any-shape path (csrc/nfx_generic.hip): the reference's d steps, MADE on MFMA GEMMs --------
+    def _generic_pack(self, device):
+        lins = self.conditioner.linears()
+        masks = [lin.mask.detach().to(device=device, dtype=torch.float32).contiguous() for lin in lins]
+        posts = [None, None, None]
+        for i, bn in enumerate(self.conditioner.batchnorms()):
+            sc = (bn.weight.detach() / torch.sqrt(bn.running_var.detach() + bn.eps)).float().contiguous()
+            posts[i] = (sc, (bn.bias.detach() - bn.running_mean.detach() * sc).float().contiguous())
+        return masks, posts
+
+    def _generic_made(self, state):
+        masks, posts = self._packed(state.device, self._generic_pack, slot="_nfx_generic_pack_cache")
+        return masks, _generic.made_forward(state, self.conditioner.linears(), masks, posts)
+
+    def _step(self, xr, prm, state, ld, gld, lam, gprm, gx, i, direction, mode):
+        B, d = state.shape
+        p = _lib.ptr
+        _lib.check(_lib.lib().nfx_arqs_step(p(xr), p(prm), p(state), p(ld), p(gld), p(lam), p(gprm), p(gx), B, d,
+                                            self.num_bins, i, int(direction), mode, float(self.min_bin_width),
+                                            float(self.min_bin_height), float(self.min_derivative),
+                                            _lib.stream_of(state)), "nfx_arqs_step")
+
+    def _generic_forward_state(self, xr, direction, state=None, ld=None):
+        """The reference's d steps (arqs.py:51-78 / :89-112) into `state` (zeroed first) with the
+        step log-dets added into `ld`: returns (state, ld)."""
+        state = torch.zeros_like(xr) if state is None else state.zero_()
+        ld = torch.zeros(xr.shape[0], device=xr.device, dtype=torch.float32) if ld is None else ld
+        for i in range(self.dim):
+            _, (_, _, _, prm) = self._generic_made(state)
+            self._step(xr, prm, state, ld, None, None, None, None, i, direction, 0)
+        return state, ld
+
+    def _generic_launch(self, x, out, log_det, direction, accumulate):
+        self._generic_forward_state(x, direction, out, log_det if accumulate else log_det.zero_())
 
     def _build_pack(self, device):
         d, H, K = self.dim, self.conditioner.hidden_dim, self.num_bins
@@ -102,7 +150,38 @@ class ARQS(HipFlow):
         packed._nfx_keep = keep
         return packed
 
+    # -- backward (training): reverse-mode through the reference's d steps ------------------------
+    def _hip_backward_ok(self, x, direction):
+        return (x.dtype == torch.float32 and not self.conditioner.batchnorms() and self._generic_ok())
+
+    def _hip_backward(self, x, gy, gld, direction):
+        """dL/dx and the parameter gradients (parameters() order) of one call, reverse-mode through
+        the reference's d steps: the state before step i is the final state with columns >= i
+        zeroed (each column is written once), so step i's MADE is recomputed there (GEMMs), its
+        spline row differentiated (nfx_arqs_step mode 1: rqs_unit_adjoint), the MADE's weight
+        gradients accumulated and its input VJP added into the running state adjoint."""
+        x = x.contiguous()
+        B, d = x.shape
+        gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
+        gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
+        state, _ = self._generic_forward_state(x, direction)
+        lam = gy.clone()
+        gx = torch.empty_like(x)
+        R = 3 * self.num_bins - 1
+        gprm = torch.zeros(B, d * R, device=x.device, dtype=torch.float32)
+        lins = self.conditioner.linears()
+        grads = None
+        for i in reversed(range(d)):
+            self._step(None, None, state, None, None, None, None, None, i, direction, 2)
+            masks, (h1, h2, h3, prm) = self._generic_made(state)
+            self._step(x, prm, state, None, gld, lam, gprm, gx, i, direction, 1)
+            gi = _generic.made_backward(state, lins, masks, h1, h2, h3, gprm, lam)
+            grads = gi if grads is None else [a.add_(b) for a, b in zip(grads, gi)]
+        return gx, grads
+
     def _hip_launch(self, x, out, log_det, direction, accumulate):
+        if not self._fused_family():
+            return self._generic_launch(x, out, log_det, direction, accumulate)
         packed = self._packed(x.device, self._build_pack)
         rescale, lo, hi = self._rescale_scalars()
         _lib.check(_lib.lib().nfx_arqs(

@@ -116,7 +116,7 @@ def test_arqs_nonfinite_inputs_match_reference_pattern(cuda_device):
 
 def test_arqs_in_flow_model_and_autograd(cuda_device):
     """ARQS inside NormalizingFlowModel (log_prob through the chain) and autograd through the
-    HIP forward (composite backward) against the CPU composite."""
+    HIP forward and the HIP reverse-sweep backward (nfx_arqs_step) against the CPU composite."""
     g = load_golden("g10_arqs.npz")
     a = _module(g, "a4bn", "cpu")
     b = copy.deepcopy(a)

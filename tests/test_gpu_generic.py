@@ -375,3 +375,90 @@ def test_generic_made_wide_backward_vs_float64(cuda_device, cls, dname):
     _grad_close(gx, gx32, gx64, "dL/dx")
     for k in gp64:
         _grad_close(gp[k], gp32[k], gp64[k], k)
+
+
+# ---- ARQS on the any-shape path: eval beyond H = 128 and the backward --------------------------
+from nfs_amd.flows import arqs as _aq  # noqa: E402
+
+
+def _arqs(d, H, K, seed, scale=0.05):
+    torch.manual_seed(seed)
+    f = nfs_amd.ARQS(d, hidden_dim=H, num_bins=K)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.add_(scale * torch.randn_like(p))
+    return f
+
+
+@pytest.mark.parametrize("d,H,K", [(3, 160, 8), (5, 256, 4), (2, 300, 11)])
+def test_generic_arqs_eval_vs_oracle(cuda_device, d, H, K):
+    """H > 128 (beyond nfx_arqs.hip): the reference's d steps, MADE on MFMA, vs the oracle."""
+    f = _arqs(d, H, K, d * 10 + H + K)
+    sd = {k: v.clone() for k, v in f.state_dict().items()}
+    x = torch.rand(500, d, generator=torch.Generator().manual_seed(d))
+    fg = f.to(cuda_device).eval()
+    assert not fg._fused_family()
+    for direction in (1, -1):
+        STATS["hip"] = STATS["torch"] = 0
+        with torch.no_grad():
+            yg, lg = (fg.forward if direction > 0 else fg.inverse)(x.to(cuda_device))
+        assert STATS["hip"] == 1 and STATS["torch"] == 0, STATS
+        yr, lr = oracle.arqs(sd, "", x, direction, K=K)
+        assert_y(yg.cpu(), yr, 1e-4)
+        assert_ld(lg.cpu(), lr, 1e-3)
+
+
+@pytest.mark.parametrize("d,H,K,direction", [(2, 32, 8, 1), (2, 32, 8, -1), (4, 64, 5, 1), (4, 64, 5, -1),
+                                             (3, 160, 10, -1), (6, 48, 3, 1)])
+def test_arqs_backward_vs_float64_autograd(cuda_device, d, H, K, direction):
+    """dL/dx and every parameter gradient of L = <wy, y> + <wl, ld> through ARQS (reverse mode
+    through the reference's d steps, nfx_arqs_step mode 1), against float64 autograd of the same
+    module, with the reference's own fp32 error as the yardstick (test_gpu_grad_fixtures
+    tolerance: max |g - g64| <= 2e-5 (1 + max|g64|) + 4 max|g32 - g64|)."""
+    f = _arqs(d, H, K, 7 * d + H + K)
+    g = torch.Generator().manual_seed(d + K)
+    x = 0.05 + 0.9 * torch.rand(700, d, generator=g)
+    wy, wl = torch.randn(700, d, generator=g), torch.randn(700, generator=g)
+
+    def run(m, xx, wyy, wll):
+        xx = xx.clone().requires_grad_(True)
+        for p in m.parameters():
+            p.grad = None
+        y, ld = m.forward(xx) if direction > 0 else m.inverse(xx)
+        ((y * wyy).sum() + (ld * wll).sum()).backward()
+        return y.detach(), ld.detach(), xx.grad, [p.grad for p in m.parameters()]
+
+    y64, l64, gx64, gp64 = run(copy.deepcopy(f).double(), x.double(), wy.double(), wl.double())
+    y32, l32, gx32, gp32 = run(copy.deepcopy(f), x, wy, wl)
+    fg = copy.deepcopy(f).to(cuda_device)
+    STATS["hip"] = STATS["torch"] = 0
+    yg, lg, gxg, gpg = run(fg, x.to(cuda_device), wy.to(cuda_device), wl.to(cuda_device))
+    assert STATS["hip"] == 2 and STATS["torch"] == 0, STATS
+    assert_y(yg.cpu(), y64, 1e-4)
+    assert_ld(lg.cpu(), l64, 1e-3)
+
+    def close(a, b32, b64, what):
+        a, b32, b64 = a.double().cpu(), b32.double(), b64.double()
+        bound = 2e-5 * (1 + b64.abs().max().item()) + 4 * (b32 - b64).abs().max().item()
+        err = (a - b64).abs().max().item()
+        assert err <= bound, f"{what}: max err {err:.3g} > {bound:.3g}"
+
+    close(gxg, gx32, gx64, "dL/dx")
+    for (n, _), a, b, c in zip(f.named_parameters(), gpg, gp32, gp64):
+        close(a, b, c, n)
+
+
+@pytest.mark.parametrize("name", ["a1", "a3", "a5", "a4bn", "a10"])
+def test_generic_arqs_vs_reference_g10(cuda_device, name):
+    """The any-shape ARQS steps (mode 0, also the backward's recompute) forced onto the
+    reference's ARQS fixtures (G10): outputs and log-dets under the fused kernel's parity test.
+    (Fixtures with data_min/data_max stay on the fused kernel: the any-shape path takes None.)"""
+    from test_gpu_arqs import _case, test_arqs_vs_reference
+    if _case(load_golden("g10_arqs.npz"), name)[4]:
+        pytest.skip("data_min/data_max rescale: fused kernel only")
+    old = _aq.FORCE_GENERIC
+    _aq.FORCE_GENERIC = True
+    try:
+        test_arqs_vs_reference(cuda_device, name)
+    finally:
+        _aq.FORCE_GENERIC = old
