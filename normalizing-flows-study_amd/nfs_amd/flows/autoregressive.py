@@ -23,8 +23,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
+from .. import distributed as _dist
 from . import generic as _generic
-from .flow import HipFlow
+from .flow import HipFlow, STATS
 
 MAX_H = 256       # eval kernels (H > 128: nfx_made_big.hip)
 MAX_H_BWD = 128   # fused backward kernels; wider layers differentiate through the composite
@@ -163,6 +164,102 @@ class _MadeAffineFlow(HipFlow):
         masks, posts = self._packed(x.device, self._generic_pack, slot="_nfx_generic_pack_cache")
         return masks, _generic.made_forward(x, self.conditioner.linears(), masks, posts)
 
+    def _generic_bn_eval(self, device):
+        """Per MADE BatchNorm [mean, invstd, scale, shift] from the running statistics."""
+        L = _lib.lib()
+        out = []
+        for bn in self.conditioner.batchnorms():
+            H = bn.num_features
+            t = torch.empty(4, H, device=device, dtype=torch.float32)
+            _lib.check(L.nfx_bn_prepare(None, _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()),
+                                        _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var), float(bn.eps), 0.0, 0,
+                                        H, _lib.ptr(t[0]), _lib.ptr(t[1]), _lib.ptr(t[2]), _lib.ptr(t[3]),
+                                        _lib.stream_of(t)), "nfx_bn_prepare")
+            out.append(t)
+        return out
+
+    def _generic_made_bn(self, x, bnp=None):
+        """MADE with BatchNorm (eval: running statistics unless bnp is given): (masks, acts, params)."""
+        masks, _ = self._packed(x.device, self._generic_pack, slot="_nfx_generic_pack_cache")
+        if bnp is None:
+            bnp = self._packed(x.device, self._generic_bn_eval, slot="_nfx_generic_bn_pack_cache")
+        acts, prm = _generic.made_bn_forward(x, self.conditioner.linears(), masks, bnp)
+        return masks, bnp, acts, prm
+
+    def _parallel(self, direction):
+        return self._variant(direction) in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD)
+
+    # -- train-mode BatchNorm in the MADE (use_batch_norm=True), parallel directions ----------------
+    def _bn_train_ok(self, x, direction):
+        bns = self.conditioner.batchnorms()
+        if not bns or not all(bn.training for bn in bns) or x.device.type != "cuda" or x.dtype != torch.float32:
+            return False
+        if any(not bn.affine or not bn.track_running_stats or bn.momentum is None or bn.running_mean is None
+               or bn.num_features > _generic_bn_max() for bn in bns):
+            return False
+        return x.dim() == 2 and x.shape[1] == self.dim and x.shape[0] >= 2 and self._parallel(direction)
+
+    def _dispatch(self, x, direction):
+        if self._bn_train_ok(x, direction):
+            STATS["hip"] += 1
+            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+                return _MadeTrainFunction.apply(self, direction, x, *list(self.parameters()))
+            y, ld, _, _ = self._generic_train_forward(x, direction)
+            return y, ld
+        return super()._dispatch(x, direction)
+
+    def _generic_train_forward(self, x, direction):
+        """Batch moments per MADE BatchNorm (nfx_flowbn_moments, SyncBN-merged), normalisation and
+        running update (nfx_bn_prepare), then the parallel element map. Returns (y, ld, bnp, counts)."""
+        L = _lib.lib()
+        x = x.detach().contiguous()
+        B, d = x.shape
+        dev = x.device
+        st = _lib.stream_of(x)
+        p = _lib.ptr
+        masks, _ = self._packed(dev, self._generic_pack, slot="_nfx_generic_pack_cache")
+        lins = self.conditioner.linears()
+        bns = self.conditioner.batchnorms()
+        bnp, counts, h = [], [], x
+        for i, bn in enumerate(bns):
+            z = _generic.linear_forward(h, lins[i], wmask=masks[i])
+            H = z.shape[1]
+            ws = torch.empty(max(1, L.nfx_flowbn_workspace_bytes(B, H)), device=dev, dtype=torch.uint8)
+            stats = torch.empty(H, 3, device=dev, dtype=torch.float64)
+            _lib.check(L.nfx_flowbn_moments(p(z), B, H, p(stats), p(ws), st), "nfx_flowbn_moments")
+            _dist.merge_bn_stats(stats)
+            t = torch.empty(4, H, device=dev, dtype=torch.float32)
+            _lib.check(L.nfx_bn_prepare(p(stats), p(bn.weight.detach()), p(bn.bias.detach()), p(bn.running_mean),
+                                        p(bn.running_var), float(bn.eps), float(bn.momentum), 1, H, p(t[0]), p(t[1]),
+                                        p(t[2]), p(t[3]), st), "nfx_bn_prepare")
+            torch.autograd.graph.increment_version(bn.running_mean)
+            torch.autograd.graph.increment_version(bn.running_var)
+            h = _generic.bn_apply_relu(z, t)
+            bnp.append(t)
+            counts.append(stats)  # stats[0, 0] = the global sample count
+        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
+        prm = _generic.linear_forward(h, lins[3], wmask=masks[3])
+        y = torch.empty_like(x)
+        ld = torch.empty(B, device=dev, dtype=torch.float32)
+        _lib.check(L.nfx_made_elem_forward(p(x), p(prm), p(y), p(ld), B, d, self._variant(direction), 0, st),
+                   "nfx_made_elem_forward")
+        return y, ld, bnp, counts
+
+    def _generic_bn_backward(self, x, gz, gld, direction, bnp=None, counts=None):
+        """Parallel direction with a BatchNorm MADE (eval: running statistics; train: the call's
+        batch statistics bnp / counts from _generic_train_forward)."""
+        B, d = x.shape
+        train = counts is not None
+        masks, bnp, acts, prm = self._generic_made_bn(x, bnp)
+        gprm = torch.empty_like(prm)
+        gx = torch.empty_like(x)
+        _lib.check(_lib.lib().nfx_made_elem_backward(_lib.ptr(x), _lib.ptr(prm), _lib.ptr(gz), _lib.ptr(gld),
+                                                     _lib.ptr(gprm), _lib.ptr(gx), B, d, self._variant(direction),
+                                                     _lib.stream_of(x)), "nfx_made_elem_backward")
+        grads = _generic.made_bn_backward(x, self.conditioner.linears(), masks, self.conditioner.batchnorms(), bnp,
+                                          acts, gprm, gx, train, counts, _dist.allreduce_bn_sums)
+        return gx, grads
+
     def _generic_launch(self, x, out, log_det, direction, accumulate):
         variant = self._variant(direction)
         L = _lib.lib()
@@ -202,8 +299,12 @@ class _MadeAffineFlow(HipFlow):
         st = _lib.stream_of(x)
         p = _lib.ptr
         work, _ = self._generic_seq_work(x, variant)
-        masks, (h1, h2, h3, prm) = self._generic_made(work)
         lins = self.conditioner.linears()
+        bns = self.conditioner.batchnorms()
+        if bns:  # eval-mode BatchNorm: a fixed per-feature affine inside the MADE
+            masks, bnp, acts, prm = self._generic_made_bn(work)
+        else:
+            masks, (h1, h2, h3, prm) = self._generic_made(work)
         gw = torch.empty_like(x)
         _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), None, p(gz), p(gld), p(gw), B, d, variant, 0,
                                                 st), "nfx_made_elem_seq_backward")
@@ -212,12 +313,17 @@ class _MadeAffineFlow(HipFlow):
         for _ in range(d - 1):
             _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), p(lam), p(gz), p(gld), p(dprm), B, d,
                                                     variant, 1, st), "nfx_made_elem_seq_backward")
-            lam = _generic.made_input_vjp(dprm, lins, masks, h1, h2, h3, gw.clone())
+            if bns:
+                lam = _generic.made_bn_input_vjp(dprm, lins, masks, bns, bnp, acts, gw.clone())
+            else:
+                lam = _generic.made_input_vjp(dprm, lins, masks, h1, h2, h3, gw.clone())
         _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), p(lam), p(gz), p(gld), p(dprm), B, d,
                                                 variant, 1, st), "nfx_made_elem_seq_backward")
         gx = torch.empty_like(x)
         _lib.check(L.nfx_made_elem_seq_backward(p(x), p(prm), p(work), p(lam), p(gz), p(gld), p(gx), B, d,
                                                 variant, 2, st), "nfx_made_elem_seq_backward")
+        if bns:
+            return gx, _generic.made_bn_backward(work, lins, masks, bns, bnp, acts, dprm, None)
         return gx, _generic.made_backward(work, lins, masks, h1, h2, h3, dprm, None)
 
     def _generic_backward(self, x, gz, gld, direction):
@@ -227,6 +333,8 @@ class _MadeAffineFlow(HipFlow):
         variant = self._variant(direction)
         if variant in (_lib.NFX_MAF_FORWARD, _lib.NFX_IAF_INVERSE):
             return self._generic_seq_backward(x, gz, gld, variant)
+        if self.conditioner.batchnorms():
+            return self._generic_bn_backward(x, gz, gld, direction)
         B, d = x.shape
         masks, (h1, h2, h3, prm) = self._generic_made(x)
         gprm = torch.empty_like(prm)
@@ -252,14 +360,19 @@ class _MadeAffineFlow(HipFlow):
 
     # -- training: fused backward of every direction (§8(f) item 1) --------------------------
     def _hip_backward_ok(self, x, direction):
-        if x.dtype != torch.float32 or self.conditioner.batchnorms():
+        if x.dtype != torch.float32:
+            return False
+        bns = self.conditioner.batchnorms()
+        if bns and (any(bn.training or not bn.affine or bn.running_mean is None for bn in bns)
+                    or bns[0].num_features > _generic_bn_max()):
             return False
         return True  # fused backward kernels, or the any-shape path (_generic_backward)
 
     def _fused_backward_ok(self):
         # parallel directions: made_bwd_kernel (d, H <= 64) / made_bwdw_kernel; sequential
         # directions: made_seq_bwd_kernel
-        return not FORCE_GENERIC and self.dim <= MAX_D and self.conditioner.hidden_dim <= MAX_H_BWD
+        return (not FORCE_GENERIC and not self.conditioner.batchnorms() and self.dim <= MAX_D
+                and self.conditioner.hidden_dim <= MAX_H_BWD)
 
     def _hip_backward(self, x, gz, gld, direction):
         """dL/dx and the parameter gradients (in self.parameters() order) of one call. Batches
@@ -353,6 +466,33 @@ class _MadeAffineFlow(HipFlow):
             return False  # no fused kernel for this (d, H): nothing was launched
         _lib.check(rc, "nfx_made_affine_logprob")
         return True
+
+
+def _generic_bn_max():
+    return 1024  # nfx_flowbn_moments: <= 1024 features
+
+
+class _MadeTrainFunction(torch.autograd.Function):
+    """MAF.inverse / IAF.forward with train-mode BatchNorm in the MADE: batch statistics and
+    running update in the forward, the batch-statistics BatchNorm backward (SyncBN sums) after."""
+
+    @staticmethod
+    def forward(ctx, layer, direction, x, *params):
+        y, ld, bnp, counts = layer._generic_train_forward(x, direction)
+        ctx.layer, ctx.direction, ctx.bnp, ctx.counts = layer, direction, bnp, counts
+        ctx.save_for_backward(x)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, gy, gld):
+        (x,) = ctx.saved_tensors
+        x = x.detach().contiguous()
+        gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
+        gld = torch.zeros(x.shape[0], device=x.device) if gld is None else gld.contiguous().float()
+        gx, grads = ctx.layer._generic_bn_backward(x, gy, gld, ctx.direction, ctx.bnp, ctx.counts)
+        STATS["hip"] += 1
+        params = list(ctx.layer.parameters())
+        return (None, None, gx, *[g if p.requires_grad else None for p, g in zip(params, grads)])
 
 
 class MaskedAutoregressiveFlow(_MadeAffineFlow):

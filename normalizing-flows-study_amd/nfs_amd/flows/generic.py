@@ -104,3 +104,75 @@ def made_backward(x, lins, masks, h1, h2, h3, gp, gx):
     if gx is not None:
         linear_backward_data(g, lins[0], wmask=masks[0], out=gx)
     return [*g1, *g2, *g3, *g4]
+
+
+# ---- MADE with BatchNorm1d (use_batch_norm=True): activations kept pre- and post-BatchNorm ------
+def bn_apply_relu(z, t):
+    """relu(z * scale + shift) with t = [mean, invstd, scale, shift] (nfx_bn_prepare)."""
+    h = torch.empty_like(z)
+    _lib.check(_lib.lib().nfx_bn_apply_relu(_lib.ptr(z), _lib.ptr(t[2]), _lib.ptr(t[3]), _lib.ptr(h), z.shape[0],
+                                            z.shape[1], _lib.stream_of(z)), "nfx_bn_apply_relu")
+    return h
+
+
+def bn_backward(g, z, t, gamma, train, count, sums_hook=None):
+    """dL/dz of BatchNorm + (dL/dgamma, dL/dbeta) as float64 sums; train: batch-statistics terms
+    with the global sample count (device float64 pointer `count`), sums passed to `sums_hook`
+    (SyncBN all-reduce) first."""
+    L = _lib.lib()
+    M, N = g.shape
+    st = _lib.stream_of(g)
+    sums = torch.empty(2, N, device=g.device, dtype=torch.float64)
+    ws = torch.empty(max(1, L.nfx_bn_workspace_bytes(M, N)), device=g.device, dtype=torch.uint8)
+    _lib.check(L.nfx_bn_backward_sums(_lib.ptr(g), _lib.ptr(z), _lib.ptr(t[0]), _lib.ptr(t[1]), _lib.ptr(sums), M, N,
+                                      _lib.ptr(ws), st), "nfx_bn_backward_sums")
+    if train and sums_hook is not None:
+        sums_hook(sums)
+    gz = torch.empty_like(g)
+    _lib.check(L.nfx_bn_backward_apply(_lib.ptr(g), _lib.ptr(z), _lib.ptr(t[0]), _lib.ptr(t[1]), _lib.ptr(gamma),
+                                       _lib.ptr(sums), _lib.ptr(count) if train else None, int(train), _lib.ptr(gz),
+                                       M, N, st), "nfx_bn_backward_apply")
+    return gz, sums
+
+
+def made_bn_forward(x, lins, masks, bnp):
+    """MADE with BatchNorm given each BatchNorm's [mean, invstd, scale, shift]: the pre-BatchNorm
+    z and post-ReLU h of the three hidden layers, and the params."""
+    acts, h = [], x
+    for i in range(3):
+        z = linear_forward(h, lins[i], wmask=masks[i])
+        h = bn_apply_relu(z, bnp[i])
+        acts.append((z, h))
+    return acts, linear_forward(h, lins[3], wmask=masks[3])
+
+
+def made_bn_backward(x, lins, masks, bns, bnp, acts, gp, gx, train=False, counts=None, sums_hook=None):
+    """Backward of made_bn_forward given dL/dparams = gp: parameter gradients in parameters()
+    order (Linear, BatchNorm per hidden layer, then the output Linear); dL/dx added into gx
+    (skipped when None)."""
+    w4 = linear_backward_weight(gp, acts[2][1], lins[3], wmask=masks[3])
+    g = linear_backward_data(gp, lins[3], act=acts[2][1], wmask=masks[3])
+    per = [None, None, None]
+    for i in (2, 1, 0):
+        z = acts[i][0]
+        gz, sums = bn_backward(g, z, bnp[i], bns[i].weight.detach(), train, counts[i] if train else None, sums_hook)
+        hin = x if i == 0 else acts[i - 1][1]
+        wl = linear_backward_weight(gz, hin, lins[i], wmask=masks[i])
+        if i > 0:
+            g = linear_backward_data(gz, lins[i], act=hin, wmask=masks[i])
+        elif gx is not None:
+            linear_backward_data(gz, lins[0], wmask=masks[0], out=gx)
+        per[i] = [wl[0], wl[1], sums[1].float(), sums[0].float()]
+    return [*per[0], *per[1], *per[2], *w4]
+
+
+def made_bn_input_vjp(gp, lins, masks, bns, bnp, acts, out):
+    """dL/d(MADE input) through eval-mode BatchNorm (a fixed per-feature scale), added into out."""
+    g = linear_backward_data(gp, lins[3], act=acts[2][1], wmask=masks[3])
+    for i in (2, 1, 0):
+        gz, _ = bn_backward(g, acts[i][0], bnp[i], bns[i].weight.detach(), False, None)
+        if i > 0:
+            g = linear_backward_data(gz, lins[i], act=acts[i - 1][1], wmask=masks[i])
+        else:
+            linear_backward_data(gz, lins[0], wmask=masks[0], out=out)
+    return out

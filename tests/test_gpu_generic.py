@@ -462,3 +462,65 @@ def test_generic_arqs_vs_reference_g10(cuda_device, name):
         test_arqs_vs_reference(cuda_device, name)
     finally:
         _aq.FORCE_GENERIC = old
+
+
+# ---- MADE with BatchNorm1d (use_batch_norm=True) under autograd --------------------------------
+def _made_bn(cls, d, H, seed):
+    torch.manual_seed(seed)
+    f = cls(d, H, use_batch_norm=True)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.add_(0.03 * torch.randn_like(p))
+        for m in f.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.normal_(0, 0.1)
+                m.running_var.uniform_(0.5, 1.5)
+                m.weight.normal_(1, 0.1)
+                m.bias.normal_(0, 0.1)
+    return f
+
+
+@pytest.mark.parametrize("cls", ["maf", "iaf"])
+@pytest.mark.parametrize("dname", ["inv", "fwd"])
+@pytest.mark.parametrize("d,H", [(12, 32), (5, 288)])
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_generic_made_batchnorm_backward_vs_float64(cuda_device, cls, dname, d, H, mode):
+    """MADE(use_batch_norm=True) under autograd. eval: running-statistics BatchNorm, both
+    directions (the sequential ones by the triangular adjoint through the BatchNorm'ed MADE);
+    train: batch-statistics BatchNorm with the running update, the parallel directions (MAF
+    inverse, IAF forward). Against float64 autograd of the same module (outputs, dL/dx, every
+    parameter gradient, running statistics after the step)."""
+    from test_gpu_grad_fixtures import _grad_close, _run
+    klass = nfs_amd.MaskedAutoregressiveFlow if cls == "maf" else nfs_amd.InverseAutoregressiveFlow
+    parallel = (cls == "maf") == (dname == "inv")
+    if mode == "train" and not parallel:
+        pytest.skip("train-mode BatchNorm in a sequential direction: torch composite (d batch-stat calls)")
+    f = _made_bn(klass, d, H, d * 7 + H)
+    f = f.train() if mode == "train" else f.eval()
+    g = torch.Generator().manual_seed(d + H)
+    x, wy, wl = torch.randn(1500, d, generator=g), torch.randn(1500, d, generator=g), torch.randn(1500, generator=g)
+    f64, f32 = copy.deepcopy(f).double(), copy.deepcopy(f)
+    _, _, gx64, gp64 = _run(f64, x.double(), wy.double(), wl.double(), dname)
+    y32, l32, gx32, gp32 = _run(f32, x, wy, wl, dname)
+    fg = copy.deepcopy(f).to(cuda_device)
+    STATS["hip"] = STATS["torch"] = 0
+    y, ld, gx, gp = _run(fg, x.to(cuda_device), wy.to(cuda_device), wl.to(cuda_device), dname)
+    assert STATS["torch"] == 0 and STATS["hip"] == 2, STATS
+    assert_y(y.cpu(), y32, 5e-5)
+    assert_ld(ld.cpu(), l32, 5e-4)
+    _grad_close(gx, gx32, gx64, "dL/dx")
+    gmax = max(float(v.abs().max()) for v in gp64.values())
+    for k in gp64:
+        if mode == "train" and k.endswith(("net.0.bias", "net.3.bias", "net.6.bias")):
+            # a Linear bias feeding a train-mode BatchNorm has an exactly-zero gradient (the
+            # batch mean removes it): both sides are summation noise, bounded as in
+            # test_gpu_affine_train._gclose by 2e-5 of the largest gradient or 4x the
+            # reference's own fp32 noise
+            err = float((gp[k].double().cpu() - gp64[k]).abs().max())
+            bound = max(2e-5 * gmax, 4 * float((gp32[k].double() - gp64[k]).abs().max()))
+            assert err <= bound, f"{k}: {err:.3g} not ~0 (bound {bound:.3g})"
+            continue
+        _grad_close(gp[k], gp32[k], gp64[k], k)
+    for (k, bg), (_, b64) in zip(fg.named_buffers(), f64.named_buffers()):
+        if k.endswith(("running_mean", "running_var")):
+            assert np.abs(bg.cpu().double().numpy() - b64.numpy()).max() <= 1e-6 * (1 + np.abs(b64.numpy()).max()), k
