@@ -446,6 +446,16 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         graphed_train = nfs_amd.GraphedTrainStep(flow, x, opt, warmup=a.warmup, clip_grad_norm=clip)
 
     eager_only = [False]  # the per-kernel event pass runs eager steps (a graph replay records no events)
+    # Eval steps all-reduce their float64 [sum log p, count] pair asynchronously: every step's
+    # 16 bytes still cross RCCL, but the next step's kernels do not queue behind the collective
+    # (the pair is copied out of the graph's reused output buffer first); all pending reductions
+    # are waited for before the closing synchronize + barrier, inside the timed region.
+    pending = []
+
+    def drain():
+        for w in pending:
+            w.wait()
+        pending.clear()
 
     def step():
         if graphed_train is not None and not eager_only[0]:
@@ -473,7 +483,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         else:
             logp, sums = flow.log_prob(x, return_sums=True)
         if world > 1:
-            dist.all_reduce(sums)  # RCCL over xGMI: 16 bytes
+            sums = sums.clone()
+            pending.append(dist.all_reduce(sums, async_op=True))  # RCCL over xGMI: 16 bytes
         return sums
 
     from nfs_amd.flows import autoregressive as _ar
@@ -482,6 +493,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     with torch.set_grad_enabled(training):
         for _ in range(a.warmup):
             step()
+        drain()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -489,6 +501,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         t0 = time.perf_counter()
         for _ in range(a.steps):
             out = step()
+        drain()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
