@@ -281,14 +281,19 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     if (in == out) return set_error(NFX_EINVAL, "made_affine: in and out must not alias");
     double* partials = reinterpret_cast<double*>(workspace);
     if (wide) {
-        made_par_kernel_t k = HT == 1 ? made_wide_pick_ht<1>(variant, fused) : made_wide_pick_ht<2>(variant, fused);
-        int rc = prepare_lds((const void*)k, wide_lds_bytes);
-        if (rc) return rc;
         const int64_t nchunks = (B + 63) / 64;
-        int grid = resident_grid((const void*)k, 512, wide_lds_bytes, (nchunks + kWideWaves - 1) / kWideWaves);
+        // 8 waves per workgroup share each staged weight slice; when that leaves CUs idle (fewer
+        // than one 8-chunk round per CU, e.g. a 64Ki per-GPU shard), 4-wave workgroups spread
+        // the chunks over twice as many CUs
+        const int nw = nchunks < (int64_t)kWideWaves * num_cus() ? 4 : kWideWaves;
+        const size_t lds_nw = (size_t)wide_lds(L, HT, nw).total * sizeof(float);
+        made_par_kernel_t k = HT == 1 ? made_wide_pick_ht<1>(variant, fused, nw) : made_wide_pick_ht<2>(variant, fused, nw);
+        int rc = prepare_lds((const void*)k, lds_nw);
+        if (rc) return rc;
+        int grid = resident_grid((const void*)k, 64 * nw, lds_nw, (nchunks + nw - 1) / nw);
         if (grid > kMaxPartials) grid = kMaxPartials;
-        k<<<grid, 512, wide_lds_bytes, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, logp, partials,
-                                            gauss_const(d));
+        k<<<grid, 64 * nw, lds_nw, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, logp, partials,
+                                        gauss_const(d));
         rc = check_launch("made_wide_kernel");
         if (rc || !fused) return rc;
         return gauss_finish(partials, grid, sums, B, s);

@@ -35,12 +35,16 @@ template made_par_kernel_t made_tile_pick_ht<2>(bool, int, bool);
 template made_par_kernel_t made_tile_pick_ht<3>(bool, int, bool);
 template made_par_kernel_t made_tile_pick_ht<4>(bool, int, bool);
 
-template <int HT>
-made_par_kernel_t made_wide_pick_ht(int variant, bool logp) {
-    if (variant != NFX_MAF_INVERSE) return made_wide_kernel<HT, NFX_IAF_FORWARD, false>;
-    return logp ? made_wide_kernel<HT, NFX_MAF_INVERSE, true> : made_wide_kernel<HT, NFX_MAF_INVERSE, false>;
+template <int HT, int NW>
+static made_par_kernel_t made_wide_pick_nw(int variant, bool logp) {
+    if (variant != NFX_MAF_INVERSE) return made_wide_kernel<HT, NFX_IAF_FORWARD, false, NW>;
+    return logp ? made_wide_kernel<HT, NFX_MAF_INVERSE, true, NW> : made_wide_kernel<HT, NFX_MAF_INVERSE, false, NW>;
 }
-template made_par_kernel_t made_wide_pick_ht<1>(int, bool);
-template made_par_kernel_t made_wide_pick_ht<2>(int, bool);
+template <int HT>
+made_par_kernel_t made_wide_pick_ht(int variant, bool logp, int nw) {
+    return nw == 4 ? made_wide_pick_nw<HT, 4>(variant, logp) : made_wide_pick_nw<HT, 8>(variant, logp);
+}
+template made_par_kernel_t made_wide_pick_ht<1>(int, bool, int);
+template made_par_kernel_t made_wide_pick_ht<2>(int, bool, int);
 
 }  // namespace nfx

@@ -36,7 +36,7 @@ struct WideLds {
     int r23, nr23, rb1, rb4, nrb4, wb, wbuf, xt, total;
 };
 
-__host__ __device__ inline WideLds wide_lds(const MadeLayout& L, int HT) {
+__host__ __device__ inline WideLds wide_lds(const MadeLayout& L, int HT, int nw = kWideWaves) {
     WideLds W{};
     int o = 0;
     W.r23 = o; W.nr23 = L.w4 - L.w2; o += W.nr23;    // w2 b2 w3 b3 (resident)
@@ -44,7 +44,7 @@ __host__ __device__ inline WideLds wide_lds(const MadeLayout& L, int HT) {
     W.rb4 = o; W.nrb4 = L.par_total - L.b4; o += W.nrb4;  // b4
     o = (o + 3) & ~3;
     W.wb = o; W.wbuf = 2 * HT * 1024; o += 2 * W.wbuf;    // two staging buffers (W1 slice / W4 block)
-    W.xt = o; o += kWideWaves * kStageFloats;             // wave-private x tiles [64][33]
+    W.xt = o; o += nw * kStageFloats;                     // wave-private x tiles [64][33]
     W.total = o;
     return W;
 }
@@ -133,46 +133,53 @@ __device__ __forceinline__ void out_pair2_n(int n, const float* __restrict__ wb,
     }
 }
 
-// Stage one weight slice (n4 float4s, contiguous in the packed image) into an LDS buffer: each
-// of the 512 threads moves at most two float4s; `reg` carries them across the compute step.
+// Stage one weight slice (n4 <= 1024 float4s, contiguous in the packed image) into an LDS
+// buffer: each of the NT threads moves at most 1024 / NT float4s; `reg` carries them across the
+// compute step.
+template <int NT>
 struct WideStage {
-    f32x4 v[2];
+    f32x4 v[1024 / NT];
 };
 
-__device__ __forceinline__ void wide_fetch(const float* __restrict__ src, int n4, WideStage& s) {
+template <int NT>
+__device__ __forceinline__ void wide_fetch(const float* __restrict__ src, int n4, WideStage<NT>& s) {
     const f32x4* p = reinterpret_cast<const f32x4*>(src);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int e = threadIdx.x + q * 512;
+    for (int q = 0; q < 1024 / NT; ++q) {
+        const int e = threadIdx.x + q * NT;
         s.v[q] = e < n4 ? p[e] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
-__device__ __forceinline__ void wide_store(float* __restrict__ dst, int n4, const WideStage& s) {
+template <int NT>
+__device__ __forceinline__ void wide_store(float* __restrict__ dst, int n4, const WideStage<NT>& s) {
     f32x4* p = reinterpret_cast<f32x4*>(dst);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int e = threadIdx.x + q * 512;
+    for (int q = 0; q < 1024 / NT; ++q) {
+        const int e = threadIdx.x + q * NT;
         if (e < n4) p[e] = s.v[q];
     }
 }
 
-template <int HT, int VAR, bool LOGP>
-__global__ __launch_bounds__(512) void made_wide_kernel(
+// NW waves per workgroup (8, or 4 when 8-wave workgroups would not cover every CU, e.g. the
+// 64Ki per-GPU shard of cfg5f): each wave owns one 64-sample chunk per round.
+template <int HT, int VAR, bool LOGP, int NW>
+__global__ __launch_bounds__(64 * NW) void made_wide_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t nchunks,
     float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
     const MadeLayout L = made_layout(d, HT);
-    const WideLds S = wide_lds(L, HT);
+    constexpr int NT = 64 * NW;
+    const WideLds S = wide_lds(L, HT, NW);
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
 
     // resident: w2 b2 w3 b3, b1, b4
-    for (int i = threadIdx.x; i < S.nr23; i += 512) lds[S.r23 + i] = packed[L.w2 + i];
-    for (int i = threadIdx.x; i < HT * 32; i += 512) lds[S.rb1 + i] = packed[L.b1 + i];
-    for (int i = threadIdx.x; i < S.nrb4; i += 512) lds[S.rb4 + i] = packed[L.b4 + i];
+    for (int i = threadIdx.x; i < S.nr23; i += NT) lds[S.r23 + i] = packed[L.w2 + i];
+    for (int i = threadIdx.x; i < HT * 32; i += NT) lds[S.rb1 + i] = packed[L.b1 + i];
+    for (int i = threadIdx.x; i < S.nrb4; i += NT) lds[S.rb4 + i] = packed[L.b4 + i];
     const float* W23 = lds + S.r23 - L.w2;  // indexable with the packed-image offsets
     const float* B1 = lds + S.rb1;
     const float* B4 = lds + S.rb4;
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
     const int n4w1 = HT * 256, n4w4 = 2 * HT * 256;
     double lpacc = 0.0;
 
-    for (int64_t cb = (int64_t)blockIdx.x * kWideWaves; cb < nchunks; cb += (int64_t)gridDim.x * kWideWaves) {
+    for (int64_t cb = (int64_t)blockIdx.x * NW; cb < nchunks; cb += (int64_t)gridDim.x * NW) {
         const int64_t c = cb + wave;
         const int64_t base = c * 64;
         const int rows = c < nchunks ? (int)(B - base < 64 ? B - base : 64) : 0;
@@ -236,7 +243,7 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
         {
             // stage slice 0: the HT tiles' 1024-float slices are strided by 4*NKC*256 floats
             f32x4* dst = reinterpret_cast<f32x4*>(lds + S.wb);
-            for (int e = threadIdx.x; e < n4w1; e += 512) {
+            for (int e = threadIdx.x; e < n4w1; e += NT) {
                 const int ht = e >> 8, q = e & 255;
                 dst[e] = reinterpret_cast<const f32x4*>(packed + L.w1 + (ht * 4 * NKC) * 256)[q];
             }
@@ -254,14 +261,20 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
             put_x(true);
             wave_lds_sync();
             // prefetch the next slice: x rows (registers) and the W1 slice (registers -> LDS)
-            f32x4 wn = f32x4{0.f, 0.f, 0.f, 0.f};
+            constexpr int NQ1 = (2 * 256 + NT - 1) / NT;  // float4s per thread of a W1 slice (HT <= 2)
+            f32x4 wn[NQ1];
+#pragma unroll
+            for (int qq = 0; qq < NQ1; ++qq) wn[qq] = f32x4{0.f, 0.f, 0.f, 0.f};
             const bool more = kc + 1 < NKC;
             if (more) {
                 load_x(kc + 1);
-                const int e = threadIdx.x;
-                if (e < n4w1) {
-                    const int ht = e >> 8, q = e & 255;
-                    wn = reinterpret_cast<const f32x4*>(packed + L.w1 + (ht * 4 * NKC + (kc + 1) * 4) * 256)[q];
+#pragma unroll
+                for (int qq = 0; qq < NQ1; ++qq) {
+                    const int e = threadIdx.x + qq * NT;
+                    if (e < n4w1) {
+                        const int ht = e >> 8, q = e & 255;
+                        wn[qq] = reinterpret_cast<const f32x4*>(packed + L.w1 + (ht * 4 * NKC + (kc + 1) * 4) * 256)[q];
+                    }
                 }
             }
 #pragma unroll
@@ -283,8 +296,13 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
                 }
             }
             wave_lds_sync();
-            if (more && threadIdx.x < n4w1)
-                reinterpret_cast<f32x4*>(lds + S.wb + ((kc + 1) & 1) * S.wbuf)[threadIdx.x] = wn;
+            if (more) {
+#pragma unroll
+                for (int qq = 0; qq < NQ1; ++qq) {
+                    const int e = threadIdx.x + qq * NT;
+                    if (e < n4w1) reinterpret_cast<f32x4*>(lds + S.wb + ((kc + 1) & 1) * S.wbuf)[e] = wn[qq];
+                }
+            }
             __syncthreads();
             ++kc;
         };
@@ -343,14 +361,14 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
         {
             f32x4* dst = reinterpret_cast<f32x4*>(lds + S.wb);
             const f32x4* src = reinterpret_cast<const f32x4*>(packed + L.w4);
-            for (int e = threadIdx.x; e < n4w4; e += 512) dst[e] = src[e];
+            for (int e = threadIdx.x; e < n4w4; e += NT) dst[e] = src[e];
         }
         __syncthreads();
         float acc0 = 0.f, acc1 = 0.f, zsq = 0.f;
         for (int j = 0; j < NJ; ++j) {
             const float* wbj = lds + S.wb + (j & 1) * S.wbuf;
             load_x(j);  // x slice j for the epilogue, in flight during the MFMAs
-            WideStage nx;
+            WideStage<NT> nx;
             const bool more = j + 1 < NJ;
             if (more) wide_fetch(packed + L.w4 + (j + 1) * 2 * HT * 1024, n4w4, nx);
             f32x16 mu0, mu1, al0, al1;
@@ -411,12 +429,12 @@ __global__ __launch_bounds__(512) void made_wide_kernel(
         }
     }
     if constexpr (LOGP) {
-        const double t = block_sum_f64<512>(lpacc);
+        const double t = block_sum_f64<NT>(lpacc);
         if (threadIdx.x == 0) partials[blockIdx.x] = t;
     }
 }
 
 template <int HT>
-made_par_kernel_t made_wide_pick_ht(int variant, bool logp);
+made_par_kernel_t made_wide_pick_ht(int variant, bool logp, int nw);
 
 }  // namespace nfx
