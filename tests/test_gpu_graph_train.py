@@ -1,7 +1,8 @@
 """GPU: a whole training step captured as one HIP graph (nfs_amd.GraphedTrainStep) computes the
 same training run as the eager step, bit for bit (every kernel is deterministic: fixed-order
 reductions), for the reference's full-batch RealNVP loop (README.md:107-117, train-mode
-BatchNorm) and a MAF stack (fused MAF backward)."""
+BatchNorm) and a MAF stack (fused MAF backward), and for wide models on the any-shape path
+(RealNVP H = 256 with train-mode BatchNorm, RealNVPSpline H = 128, MAF H = 320)."""
 import copy
 
 import pytest
@@ -19,11 +20,19 @@ def _data(n, seed):
     return x
 
 
-@pytest.mark.parametrize("kind", ["realnvp", "maf"])
+# realnvp / maf: the fused train kernels; the *_wide kinds run the any-shape path
+# (csrc/nfx_generic.hip: GEMM conditioner, BatchNorm moments / running update, element adjoints)
+@pytest.mark.parametrize("kind", ["realnvp", "maf", "realnvp_wide", "spline_wide", "maf_wide"])
 def test_graphed_train_step_equals_eager(cuda_device, kind):
     torch.manual_seed(3)
     if kind == "realnvp":
         m = nfs_amd.RealNVP(2, 8, 64)
+    elif kind == "realnvp_wide":
+        m = nfs_amd.RealNVP(2, 4, 256)
+    elif kind == "spline_wide":
+        m = nfs_amd.RealNVPSpline(2, 4, 128)
+    elif kind == "maf_wide":
+        m = nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(2, 320) for _ in range(3)])
     else:
         m = nfs_amd.NormalizingFlowModel([nfs_amd.MaskedAutoregressiveFlow(2, 64) for _ in range(4)])
     a = copy.deepcopy(m).to(cuda_device).train()
