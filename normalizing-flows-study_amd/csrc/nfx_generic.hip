@@ -284,35 +284,48 @@ static const void* spline_elem_pick(int K, bool inv) {
 // Parallel directions (one thread per sample, dims in order, log-det summed in dim order):
 //   MAF inverse  masked_autoregressive_flow.py:18-44   z = (x - mu) exp(clamp(-clamp(a,-3,3),-5,5))
 //   IAF forward  inverse_autoregressive_flow.py:30-63  y = x exp(clamp(clamp(a,-2,2),-3,3)) + clamp(mu,-10,10)
+// A wave per sample (grid-stride over samples), lanes over the dims: every row access is
+// coalesced; the log-det is a fixed-order wave reduction (xor butterfly) of the lanes' partial
+// sums — deterministic, summed in another order than the reference's left-to-right
+// torch.sum (within fp32 rounding).
+__device__ __forceinline__ float wave_sum_xor(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void made_elem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ prm,
                                                             float* __restrict__ y, float* __restrict__ log_det,
                                                             int64_t B, int d, int variant, int accumulate) {
 #pragma clang fp contract(off)
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B) return;
-    const float* mu = prm + s * 2 * d;
-    const float* al = mu + d;
-    float ld = 0.f;
-    if (variant == NFX_MAF_INVERSE) {
-        for (int j = 0; j < d; ++j) {
-            const float a = tclamp(al[j], -3.f, 3.f);
-            const float z = (x[s * d + j] - mu[j]) * exp_fast(tclamp(-a, -5.f, 5.f));
-            y[s * d + j] = nonfinite(z) ? 0.f : z;
-            ld = ld + a;
-        }
-        ld = -ld;
-        ld = nonfinite(ld) ? 0.f : tclamp(ld, -100.f, 100.f);
-    } else {
-        for (int j = 0; j < d; ++j) {
-            const float a = tclamp(al[j], -2.f, 2.f);
+    const int lane = lane_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const bool maf = variant == NFX_MAF_INVERSE;
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < B; s += nw) {
+        const float* mu = prm + s * 2 * d;
+        const float* al = mu + d;
+        float part = 0.f;
+        for (int j = lane; j < d; j += 64) {
             const float xv = x[s * d + j];
-            const float v = xv * exp_fast(tclamp(a, -3.f, 3.f)) + tclamp(mu[j], -10.f, 10.f);
-            y[s * d + j] = nonfinite(v) ? xv : v;
-            ld = ld + a;
+            if (maf) {
+                const float a = tclamp(al[j], -3.f, 3.f);
+                const float z = (xv - mu[j]) * exp_fast(tclamp(-a, -5.f, 5.f));
+                y[s * d + j] = nonfinite(z) ? 0.f : z;
+                part = part + a;
+            } else {
+                const float a = tclamp(al[j], -2.f, 2.f);
+                const float v = xv * exp_fast(tclamp(a, -3.f, 3.f)) + tclamp(mu[j], -10.f, 10.f);
+                y[s * d + j] = nonfinite(v) ? xv : v;
+                part = part + a;
+            }
         }
-        ld = nonfinite(ld) ? 0.f : tclamp(ld, -50.f, 50.f);
+        const float tot = wave_sum_xor(part);
+        if (lane == 0) {
+            float ld = maf ? -tot : tot;
+            ld = nonfinite(ld) ? 0.f : (maf ? tclamp(ld, -100.f, 100.f) : tclamp(ld, -50.f, 50.f));
+            log_det[s] = accumulate ? log_det[s] + ld : ld;
+        }
     }
-    log_det[s] = accumulate ? log_det[s] + ld : ld;
 }
 
 // One step i of a sequential direction on the running vector w [B][d] (the conditioner input of
@@ -355,47 +368,51 @@ __global__ __launch_bounds__(256) void made_elem_finish_kernel(const float* __re
 }
 
 // Adjoint of made_elem_fwd_kernel (autograd of the reference's ops, guards and clamps included):
-// gprm [B][2d] = (dL/dmu, dL/dalpha), gx [B][d] = the direct dL/dx term.
+// gprm [B][2d] = (dL/dmu, dL/dalpha), gx [B][d] = the direct dL/dx term. A wave per sample,
+// lanes over the dims, as the forward.
 __global__ __launch_bounds__(256) void made_elem_bwd_kernel(const float* __restrict__ x, const float* __restrict__ prm,
                                                             const float* __restrict__ gy, const float* __restrict__ gld,
                                                             float* __restrict__ gprm, float* __restrict__ gx, int64_t B,
                                                             int d, int variant) {
 #pragma clang fp contract(off)
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B) return;
-    const float* mu = prm + s * 2 * d;
-    const float* al = mu + d;
-    float* gmu = gprm + s * 2 * d;
-    float* gal = gmu + d;
+    const int lane = lane_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     const bool maf = variant == NFX_MAF_INVERSE;
     const float lo = maf ? -3.f : -2.f, hi = maf ? 3.f : 2.f, lim = maf ? 100.f : 50.f;
-    float asum = 0.f;
-    for (int j = 0; j < d; ++j) asum = asum + tclamp(al[j], lo, hi);
-    const float ldraw = maf ? -asum : asum;
-    const float ld1 = nonfinite(ldraw) ? 0.f : ldraw;
-    const float g0 = gld ? gld[s] : 0.f;
-    const float gl = (nonfinite(ldraw) || !(ld1 >= -lim && ld1 <= lim)) ? 0.f : g0;
-    for (int j = 0; j < d; ++j) {
-        const float xv = x[s * d + j], alpha = al[j], m = mu[j];
-        const float g = gy ? gy[s * d + j] : 0.f;
-        const float a = tclamp(alpha, lo, hi);
-        const bool ain = alpha >= lo && alpha <= hi;
-        if (maf) {
-            const float e = exp_fast(tclamp(-a, -5.f, 5.f));
-            const float xm = xv - m;
-            const float gz = nonfinite(xm * e) ? 0.f : g;
-            const float ge = gz * e;
-            gx[s * d + j] = ge;
-            gmu[j] = -ge;
-            gal[j] = ain ? -(gz * xm * e) - gl : 0.f;
-        } else {
-            const float e = exp_fast(tclamp(a, -3.f, 3.f));
-            const float yr = xv * e + tclamp(m, -10.f, 10.f);
-            const bool bad = nonfinite(yr);
-            const float gyr = bad ? 0.f : g;
-            gx[s * d + j] = bad ? g : gyr * e;
-            gmu[j] = (m >= -10.f && m <= 10.f) ? gyr : 0.f;
-            gal[j] = ain ? gyr * xv * e + gl : 0.f;
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < B; s += nw) {
+        const float* mu = prm + s * 2 * d;
+        const float* al = mu + d;
+        float* gmu = gprm + s * 2 * d;
+        float* gal = gmu + d;
+        float part = 0.f;
+        for (int j = lane; j < d; j += 64) part = part + tclamp(al[j], lo, hi);
+        const float asum = wave_sum_xor(part);
+        const float ldraw = maf ? -asum : asum;
+        const float ld1 = nonfinite(ldraw) ? 0.f : ldraw;
+        const float g0 = gld ? gld[s] : 0.f;
+        const float gl = (nonfinite(ldraw) || !(ld1 >= -lim && ld1 <= lim)) ? 0.f : g0;
+        for (int j = lane; j < d; j += 64) {
+            const float xv = x[s * d + j], alpha = al[j], m = mu[j];
+            const float g = gy ? gy[s * d + j] : 0.f;
+            const float a = tclamp(alpha, lo, hi);
+            const bool ain = alpha >= lo && alpha <= hi;
+            if (maf) {
+                const float e = exp_fast(tclamp(-a, -5.f, 5.f));
+                const float xm = xv - m;
+                const float gz = nonfinite(xm * e) ? 0.f : g;
+                const float ge = gz * e;
+                gx[s * d + j] = ge;
+                gmu[j] = -ge;
+                gal[j] = ain ? -(gz * xm * e) - gl : 0.f;
+            } else {
+                const float e = exp_fast(tclamp(a, -3.f, 3.f));
+                const float yr = xv * e + tclamp(m, -10.f, 10.f);
+                const bool bad = nonfinite(yr);
+                const float gyr = bad ? 0.f : g;
+                gx[s * d + j] = bad ? g : gyr * e;
+                gmu[j] = (m >= -10.f && m <= 10.f) ? gyr : 0.f;
+                gal[j] = ain ? gyr * xv * e + gl : 0.f;
+            }
         }
     }
 }
@@ -830,6 +847,12 @@ extern "C" int nfx_spline_elem_backward(const float* x, const float* params, con
     return check_launch("spline_elem_bwd_kernel");
 }
 
+// Blocks of 4 waves for the wave-per-sample element kernels (grid-stride beyond 16 Ki waves).
+static unsigned wave_grid(int64_t B) {
+    const int64_t b = (B + 3) / 4;
+    return (unsigned)(b < 4096 ? (b < 1 ? 1 : b) : 4096);
+}
+
 static int made_elem_check(int64_t B, int d, const char* what) {
     if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "%s: bad shape B=%lld d=%d", what, (long long)B, d);
     if ((B + 255) / 256 > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "%s: B too large", what);
@@ -844,7 +867,7 @@ extern "C" int nfx_made_elem_forward(const float* x, const float* params, float*
         return set_error(NFX_EINVAL, "made_elem_forward: parallel variants only (MAF inverse / IAF forward)");
     if (B == 0) return NFX_OK;
     if (!x || !params || !y || !log_det) return set_error(NFX_EINVAL, "made_elem_forward: null pointer");
-    made_elem_fwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, y, log_det, B, d,
+    made_elem_fwd_kernel<<<wave_grid(B), 256, 0, (hipStream_t)stream>>>(x, params, y, log_det, B, d,
                                                                                       variant, accumulate);
     return check_launch("made_elem_fwd_kernel");
 }
@@ -884,7 +907,7 @@ extern "C" int nfx_made_elem_backward(const float* x, const float* params, const
         return set_error(NFX_EINVAL, "made_elem_backward: parallel variants only");
     if (B == 0) return NFX_OK;
     if (!x || !params || !gparams || !gx) return set_error(NFX_EINVAL, "made_elem_backward: null pointer");
-    made_elem_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, params, gy, gld, gparams, gx,
+    made_elem_bwd_kernel<<<wave_grid(B), 256, 0, (hipStream_t)stream>>>(x, params, gy, gld, gparams, gx,
                                                                                       B, d, variant);
     return check_launch("made_elem_bwd_kernel");
 }
