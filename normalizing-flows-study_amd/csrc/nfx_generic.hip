@@ -471,30 +471,37 @@ __global__ __launch_bounds__(256) void made_elem_seq_bwd_kernel(const float* __r
 // ---- affine coupling element math (coupling_layer.py:40-96) ---------------------------------
 // s, b = clamp(raw, -10, 10); y = x m + (1 - m)(x exp(s) + b)  (forward) or
 // x m + (1 - m)((x - b) exp(-s)) (inverse); ld = sum_j (1 - m) (+-s); guards: y, ld non-finite -> 0.
+// A wave per sample, lanes over the dims (coalesced rows), log-det by a fixed-order wave
+// reduction (as the MADE element kernels).
 __global__ __launch_bounds__(256) void affine_elem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sr,
                                                               const float* __restrict__ br, const float* __restrict__ mask,
                                                               float* __restrict__ y, float* __restrict__ log_det,
                                                               int64_t B, int d, int dir, int accumulate) {
 #pragma clang fp contract(off)
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B) return;
-    float ld = 0.f;
-    for (int j = 0; j < d; ++j) {
-        const float m = mask[j], om = 1.f - m, xv = x[s * d + j];
-        const float sv = tclamp(sr[s * d + j], -10.f, 10.f), bv = tclamp(br[s * d + j], -10.f, 10.f);
-        float t;
-        if (dir > 0) {
-            t = xv * exp_fast(sv) + bv;
-            ld = ld + om * sv;
-        } else {
-            t = (xv - bv) * exp_fast(-sv);
-            ld = ld + om * (-sv);
+    const int lane = lane_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < B; s += nw) {
+        float part = 0.f;
+        for (int j = lane; j < d; j += 64) {
+            const float m = mask[j], om = 1.f - m, xv = x[s * d + j];
+            const float sv = tclamp(sr[s * d + j], -10.f, 10.f), bv = tclamp(br[s * d + j], -10.f, 10.f);
+            float t;
+            if (dir > 0) {
+                t = xv * exp_fast(sv) + bv;
+                part = part + om * sv;
+            } else {
+                t = (xv - bv) * exp_fast(-sv);
+                part = part + om * (-sv);
+            }
+            const float v = xv * m + om * t;
+            y[s * d + j] = nonfinite(v) ? 0.f : v;
         }
-        const float v = xv * m + om * t;
-        y[s * d + j] = nonfinite(v) ? 0.f : v;
+        float ld = wave_sum_xor(part);
+        if (lane == 0) {
+            if (nonfinite(ld)) ld = 0.f;
+            log_det[s] = accumulate ? log_det[s] + ld : ld;
+        }
     }
-    if (nonfinite(ld)) ld = 0.f;
-    log_det[s] = accumulate ? log_det[s] + ld : ld;
 }
 
 // Its adjoint: gs, gb = dL/d(raw net outputs), gx = the direct dL/dx term.
@@ -504,37 +511,40 @@ __global__ __launch_bounds__(256) void affine_elem_bwd_kernel(const float* __res
                                                               float* __restrict__ gs, float* __restrict__ gb,
                                                               float* __restrict__ gx, int64_t B, int d, int dir) {
 #pragma clang fp contract(off)
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= B) return;
-    float ld = 0.f;
-    for (int j = 0; j < d; ++j) {
-        const float om = 1.f - mask[j], sv = tclamp(sr[s * d + j], -10.f, 10.f);
-        ld = ld + om * (dir > 0 ? sv : -sv);
-    }
-    const float gl = (gld && !nonfinite(ld)) ? gld[s] : 0.f;
-    for (int j = 0; j < d; ++j) {
-        const float m = mask[j], om = 1.f - m, xv = x[s * d + j];
-        const float s0 = sr[s * d + j], b0 = br[s * d + j];
-        const float sv = tclamp(s0, -10.f, 10.f), bv = tclamp(b0, -10.f, 10.f);
-        const bool sin = s0 >= -10.f && s0 <= 10.f, bin = b0 >= -10.f && b0 <= 10.f;
-        const float g = gy ? gy[s * d + j] : 0.f;
-        float v, e, dts, dtb;
-        if (dir > 0) {
-            e = exp_fast(sv);
-            v = xv * m + om * (xv * e + bv);
-            dts = xv * e;
-            dtb = 1.f;
-        } else {
-            e = exp_fast(-sv);
-            v = xv * m + om * ((xv - bv) * e);
-            dts = -((xv - bv) * e);
-            dtb = -e;
+    const int lane = lane_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); s < B; s += nw) {
+        float part = 0.f;
+        for (int j = lane; j < d; j += 64) {
+            const float om = 1.f - mask[j], sv = tclamp(sr[s * d + j], -10.f, 10.f);
+            part = part + om * (dir > 0 ? sv : -sv);
         }
-        const float gv = nonfinite(v) ? 0.f : g;
-        const float gvo = gv * om;
-        gs[s * d + j] = sin ? gvo * dts + (dir > 0 ? gl * om : -(gl * om)) : 0.f;
-        gb[s * d + j] = bin ? gvo * dtb : 0.f;
-        gx[s * d + j] = gv * m + gvo * e;
+        const float ld = wave_sum_xor(part);
+        const float gl = (gld && !nonfinite(ld)) ? gld[s] : 0.f;
+        for (int j = lane; j < d; j += 64) {
+            const float m = mask[j], om = 1.f - m, xv = x[s * d + j];
+            const float s0 = sr[s * d + j], b0 = br[s * d + j];
+            const float sv = tclamp(s0, -10.f, 10.f), bv = tclamp(b0, -10.f, 10.f);
+            const bool sin = s0 >= -10.f && s0 <= 10.f, bin = b0 >= -10.f && b0 <= 10.f;
+            const float g = gy ? gy[s * d + j] : 0.f;
+            float v, e, dts, dtb;
+            if (dir > 0) {
+                e = exp_fast(sv);
+                v = xv * m + om * (xv * e + bv);
+                dts = xv * e;
+                dtb = 1.f;
+            } else {
+                e = exp_fast(-sv);
+                v = xv * m + om * ((xv - bv) * e);
+                dts = -((xv - bv) * e);
+                dtb = -e;
+            }
+            const float gv = nonfinite(v) ? 0.f : g;
+            const float gvo = gv * om;
+            gs[s * d + j] = sin ? gvo * dts + (dir > 0 ? gl * om : -(gl * om)) : 0.f;
+            gb[s * d + j] = bin ? gvo * dtb : 0.f;
+            gx[s * d + j] = gv * m + gvo * e;
+        }
     }
 }
 
@@ -940,7 +950,7 @@ extern "C" int nfx_affine_elem_forward(const float* x, const float* s_raw, const
     if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "affine_elem_forward: direction");
     if (B == 0) return NFX_OK;
     if (!x || !s_raw || !b_raw || !mask || !y || !log_det) return set_error(NFX_EINVAL, "affine_elem_forward: null pointer");
-    affine_elem_fwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, s_raw, b_raw, mask, y, log_det,
+    affine_elem_fwd_kernel<<<wave_grid(B), 256, 0, (hipStream_t)stream>>>(x, s_raw, b_raw, mask, y, log_det,
                                                                                         B, d, direction, accumulate);
     return check_launch("affine_elem_fwd_kernel");
 }
@@ -953,7 +963,7 @@ extern "C" int nfx_affine_elem_backward(const float* x, const float* s_raw, cons
     if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "affine_elem_backward: direction");
     if (B == 0) return NFX_OK;
     if (!x || !s_raw || !b_raw || !mask || !gs || !gb || !gx) return set_error(NFX_EINVAL, "affine_elem_backward: null pointer");
-    affine_elem_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, s_raw, b_raw, mask, gy, gld, gs,
+    affine_elem_bwd_kernel<<<wave_grid(B), 256, 0, (hipStream_t)stream>>>(x, s_raw, b_raw, mask, gy, gld, gs,
                                                                                         gb, gx, B, d, direction);
     return check_launch("affine_elem_bwd_kernel");
 }
