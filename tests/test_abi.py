@@ -80,3 +80,38 @@ def test_affine_kernel_policy_roundtrip():
     assert f(7) == _lib.NFX_EINVAL
     assert f(prev) == _lib.NFX_AFFINE_SMALL
     assert f(-1) == prev
+
+
+def test_any_shape_entry_points_validate_on_the_host():
+    """The any-shape path (csrc/nfx_generic.hip): shape / variant / mode checks and the B == 0
+    no-ops return before any device call; workspace sizes are host arithmetic."""
+    L = _lib.lib()
+    EINVAL, EUNSUP = _lib.NFX_EINVAL, _lib.NFX_EUNSUPPORTED
+    assert L.nfx_linear_forward(None, None, None, None, None, None, None, None, -1, 4, 4, 0, None) == EINVAL
+    assert L.nfx_linear_forward(None, None, None, None, None, None, None, None, 0, 4, 4, 0, None) == 0
+    assert L.nfx_linear_forward(None, None, None, None, None, None, None, None, 8, 4, 4, 0, None) == EINVAL
+    ps = ctypes.c_void_p(1)
+    assert L.nfx_linear_forward(ps, ps, None, None, None, ps, None, ps, 8, 4, 4, 0, None) == EINVAL
+    assert b"post_scale" in L.nfx_last_error()
+    assert L.nfx_linear_backward_data(None, None, None, None, None, None, 8, 0, 4, 0, None) == EINVAL
+    assert L.nfx_linear_backward_weight(None, None, None, None, None, None, 8, 4, 4, None, None) == EINVAL
+    assert L.nfx_linear_workspace_bytes(1 << 20, 128, 128) >= 128 * 128 * 4
+    assert L.nfx_linear_workspace_bytes(0, 128, 128) == 0
+    assert L.nfx_spline_elem_forward(None, None, None, None, None, 8, 2, 12, 5.0, 1e-3, 1e-3, 1e-3, 1, 0,
+                                     None) == EUNSUP
+    assert L.nfx_spline_elem_backward(None, None, None, None, None, None, None, 8, 2, 8, 5.0, 1e-3, 1e-3, 1e-3, 0,
+                                      None) == EINVAL
+    # the MADE element map: parallel variants only; a sequential step needs a sequential variant
+    assert L.nfx_made_elem_forward(None, None, None, None, 8, 4, _lib.NFX_MAF_FORWARD, 0, None) == EINVAL
+    assert L.nfx_made_elem_step(None, None, None, None, 8, 4, 0, _lib.NFX_MAF_INVERSE, None) == EINVAL
+    assert L.nfx_made_elem_step(None, None, None, None, 8, 4, 4, _lib.NFX_MAF_FORWARD, None) == EINVAL
+    assert L.nfx_made_elem_seq_backward(None, None, None, None, None, None, None, 8, 4, _lib.NFX_IAF_INVERSE, 3,
+                                        None) == EINVAL
+    assert L.nfx_made_elem_backward(None, None, None, None, None, None, 0, 4, _lib.NFX_IAF_FORWARD, None) == 0
+    assert L.nfx_affine_elem_forward(None, None, None, None, None, None, 8, 4, 0, 0, None) == EINVAL
+    assert L.nfx_arqs_step(None, None, None, None, None, None, None, None, 8, 4, 1, 0, 1, 0, 1e-3, 1e-3, 1e-3,
+                           None) == EUNSUP
+    assert L.nfx_arqs_step(None, None, None, None, None, None, None, None, 8, 4, 8, 0, 1, 5, 1e-3, 1e-3, 1e-3,
+                           None) == EINVAL
+    assert L.nfx_bn_prepare(None, None, None, None, None, 1e-5, 0.1, 0, 0, None, None, None, None, None) == EINVAL
+    assert L.nfx_bn_workspace_bytes(1 << 20, 64) >= 2 * 64 * 8
