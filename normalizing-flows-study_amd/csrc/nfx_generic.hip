@@ -46,7 +46,9 @@ struct GemmArgs {
     int64_t kchunk;          // split-K: workgroup z covers k in [z * kchunk, (z + 1) * kchunk)
 };
 
-template <int TA, int TB>
+// VA / VB: the operand's contiguous index is 16-byte aligned (ld % 4 == 0, aligned base): tiles
+// move as float4s (2 per thread per operand instead of 8 dword loads), edges component-wise.
+template <int TA, int TB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __shared__ float As[kGBM][kGBK + 1];
     __shared__ float Bs[kGBK][kGBN + 1];
@@ -56,38 +58,123 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     const int64_t kb = (int64_t)blockIdx.z * g.kchunk;
     const int64_t ke = kb + g.kchunk < g.K ? kb + g.kchunk : g.K;
     float ra[8], rb[8];
+    // element (r, c) of a row-major operand p[r * ld + c] with c the contiguous index, 4 at a time
+    auto vec4 = [](const float* p, const float* msk, int64_t r, int64_t c, int64_t ld, int64_t rmax, int64_t cmax,
+                   float (&o)[4]) {
+        if (r < rmax && c + 3 < cmax) {
+            f32x4 v = *reinterpret_cast<const f32x4*>(p + r * ld + c);
+            if (msk) v *= *reinterpret_cast<const f32x4*>(msk + r * ld + c);
+            o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = r < rmax && c + q < cmax;
+                o[q] = ok ? p[r * ld + c + q] * (msk ? msk[r * ld + c + q] : 1.f) : 0.f;
+            }
+        }
+    };
     // global -> registers for the K tile at k0 (coalesced along the contiguous index)
     auto load = [&](int64_t k0) {
+        if constexpr (VA) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int idx = e * 256 + t;
-            int mi, ki;
-            if (TA == 0) { mi = idx >> 5; ki = idx & 31; } else { ki = idx >> 6; mi = idx & 63; }
-            const int64_t m = m0 + mi, k = k0 + ki;
-            float v = 0.f;
-            if (m < g.M && k < ke) {
-                v = TA == 0 ? g.a[m * g.lda + k] : g.a[k * g.lda + m];
-                if (g.kscale) v *= g.kscale[k];
+            for (int e = 0; e < 2; ++e) {
+                const int q = e * 256 + t;
+                float o[4];
+                if (TA == 0) {  // k contiguous: row m, 4 k's
+                    const int64_t m = m0 + (q >> 3), k = k0 + (q & 7) * 4;
+                    vec4(g.a, nullptr, m, k, g.lda, g.M, ke, o);
+                    if (g.kscale)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) o[c] *= (k + c < ke) ? g.kscale[k + c] : 0.f;
+                } else {        // m contiguous: row k, 4 m's
+                    const int64_t k = k0 + (q >> 4), m = m0 + (q & 15) * 4;
+                    vec4(g.a, nullptr, k, m, g.lda, ke, g.M, o);
+                    if (g.kscale && k < ke)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) o[c] *= g.kscale[k];
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ra[4 * e + c] = o[c];
             }
-            ra[e] = v;
-            int ni, kj;
-            if (TB == 0) { kj = idx >> 6; ni = idx & 63; } else { ni = idx >> 5; kj = idx & 31; }
-            const int64_t n = n0 + ni, k2 = k0 + kj;
-            float w = 0.f;
-            if (n < g.N && k2 < ke) {
-                const int64_t o = TB == 0 ? k2 * g.ldb + n : n * g.ldb + k2;
-                w = g.b[o];
-                if (g.bmask) w *= g.bmask[o];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int idx = e * 256 + t;
+                int mi, ki;
+                if (TA == 0) { mi = idx >> 5; ki = idx & 31; } else { ki = idx >> 6; mi = idx & 63; }
+                const int64_t m = m0 + mi, k = k0 + ki;
+                float v = 0.f;
+                if (m < g.M && k < ke) {
+                    v = TA == 0 ? g.a[m * g.lda + k] : g.a[k * g.lda + m];
+                    if (g.kscale) v *= g.kscale[k];
+                }
+                ra[e] = v;
             }
-            rb[e] = w;
+        }
+        if constexpr (VB) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int q = e * 256 + t;
+                float o[4];
+                if (TB == 0) {  // n contiguous: row k, 4 n's
+                    vec4(g.b, g.bmask, k0 + (q >> 4), n0 + (q & 15) * 4, g.ldb, ke, g.N, o);
+                } else {        // k contiguous: row n, 4 k's
+                    vec4(g.b, g.bmask, n0 + (q >> 3), k0 + (q & 7) * 4, g.ldb, g.N, ke, o);
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) rb[4 * e + c] = o[c];
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int idx = e * 256 + t;
+                int ni, kj;
+                if (TB == 0) { kj = idx >> 6; ni = idx & 63; } else { ni = idx >> 5; kj = idx & 31; }
+                const int64_t n = n0 + ni, k2 = k0 + kj;
+                float w = 0.f;
+                if (n < g.N && k2 < ke) {
+                    const int64_t o = TB == 0 ? k2 * g.ldb + n : n * g.ldb + k2;
+                    w = g.b[o];
+                    if (g.bmask) w *= g.bmask[o];
+                }
+                rb[e] = w;
+            }
         }
     };
     auto park = [&]() {
+        if constexpr (VA) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int idx = e * 256 + t;
-            if (TA == 0) As[idx >> 5][idx & 31] = ra[e]; else As[idx & 63][idx >> 6] = ra[e];
-            if (TB == 0) Bs[idx >> 6][idx & 63] = rb[e]; else Bs[idx & 31][idx >> 5] = rb[e];
+            for (int e = 0; e < 2; ++e) {
+                const int q = e * 256 + t;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (TA == 0) As[q >> 3][(q & 7) * 4 + c] = ra[4 * e + c];
+                    else As[(q & 15) * 4 + c][q >> 4] = ra[4 * e + c];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int idx = e * 256 + t;
+                if (TA == 0) As[idx >> 5][idx & 31] = ra[e]; else As[idx & 63][idx >> 6] = ra[e];
+            }
+        }
+        if constexpr (VB) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int q = e * 256 + t;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (TB == 0) Bs[q >> 4][(q & 15) * 4 + c] = rb[4 * e + c];
+                    else Bs[(q & 7) * 4 + c][q >> 3] = rb[4 * e + c];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int idx = e * 256 + t;
+                if (TB == 0) Bs[idx >> 6][idx & 63] = rb[e]; else Bs[idx & 31][idx >> 5] = rb[e];
+            }
         }
     };
     f32x16 acc = {};
@@ -119,6 +206,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     }
 }
 
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int TA, int TB>
+static void gemm_go(const GemmArgs& g, dim3 grid, hipStream_t s) {
+    const bool va = g.lda % 4 == 0 && aligned16(g.a);
+    const bool vb = g.ldb % 4 == 0 && aligned16(g.b) && (!g.bmask || aligned16(g.bmask));
+    if (va && vb) gemm_kernel<TA, TB, true, true><<<grid, 256, 0, s>>>(g);
+    else if (va) gemm_kernel<TA, TB, true, false><<<grid, 256, 0, s>>>(g);
+    else if (vb) gemm_kernel<TA, TB, false, true><<<grid, 256, 0, s>>>(g);
+    else gemm_kernel<TA, TB, false, false><<<grid, 256, 0, s>>>(g);
+}
+
 static int gemm_launch(const GemmArgs& g, int ta, int tb, int64_t splits, hipStream_t s) {
     // M tiles on x (the batch: up to 2^31 - 1 tiles), N tiles and split-K slices on y / z (< 65536)
     const int64_t gm = (g.M + kGBM - 1) / kGBM, gn = (g.N + kGBN - 1) / kGBN;
@@ -126,9 +225,9 @@ static int gemm_launch(const GemmArgs& g, int ta, int tb, int64_t splits, hipStr
         return set_error(NFX_EUNSUPPORTED, "linear: grid %lld x %lld x %lld out of range", (long long)gm,
                          (long long)gn, (long long)splits);
     dim3 grid((unsigned)gm, (unsigned)gn, (unsigned)splits);
-    if (ta == 0 && tb == 1) gemm_kernel<0, 1><<<grid, 256, 0, s>>>(g);
-    else if (ta == 0 && tb == 0) gemm_kernel<0, 0><<<grid, 256, 0, s>>>(g);
-    else if (ta == 1 && tb == 0) gemm_kernel<1, 0><<<grid, 256, 0, s>>>(g);
+    if (ta == 0 && tb == 1) gemm_go<0, 1>(g, grid, s);
+    else if (ta == 0 && tb == 0) gemm_go<0, 0>(g, grid, s);
+    else if (ta == 1 && tb == 0) gemm_go<1, 0>(g, grid, s);
     else return set_error(NFX_EINVAL, "linear: unsupported layout");
     return check_launch("gemm_kernel");
 }
