@@ -237,6 +237,7 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, int64_t nz, 
                                     int accumulate, const float* __restrict__ mask) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         float v = 0.f;
+#pragma unroll 8
         for (int64_t z = 0; z < nz; ++z) v += part[z * n + i];
         if (mask) v *= mask[i];
         out[i] = accumulate ? out[i] + v : v;
@@ -271,6 +272,63 @@ static int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) {
     if (s < 1) s = 1;
     if (s > 1024) s = 1024;
     return s;
+}
+
+// Thin weight gradient (min(N, K) <= 8: a coupling net's first layer at small d, a MADE output
+// layer's few outputs): a 64x64 MFMA tile would waste up to 63/64 of its work, so this is a
+// streaming reduction instead. The wide operand (gy's N columns when THIN_X, else x's K columns)
+// goes one column per lane, coalesced rows; the thin one (KT <= 8 values per row) is a uniform
+// broadcast. 4 waves interleave the rows of a split; fixed-order LDS merge, one partial per split
+// (part_w[split][N][K] pre-scaled by in_scale[k] like the GEMM epilogue, part_b[split][N]).
+template <int KT, bool THIN_X>
+__global__ __launch_bounds__(256) void thin_wgrad_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                                                         const float* __restrict__ in_scale, int64_t M, int N, int K,
+                                                         int64_t rchunk, float* __restrict__ part_w,
+                                                         float* __restrict__ part_b) {
+    __shared__ float red[4][64][KT + 2];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const int C = THIN_X ? N : K;
+    const float* wide = THIN_X ? gy : x;
+    const float* thin = THIN_X ? x : gy;
+    const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t rb = (int64_t)blockIdx.y * rchunk;
+    const int64_t re = rb + rchunk < M ? rb + rchunk : M;
+    float acc[KT], bw = 0.f, bl = 0.f;
+#pragma unroll
+    for (int q = 0; q < KT; ++q) acc[q] = 0.f;
+#pragma unroll 4
+    for (int64_t m = rb + wave; m < re; m += 4) {
+        const float w = c < C ? wide[m * C + c] : 0.f;
+        bw += w;
+        // gy thin: lane q < KT keeps column q's sum (the bias gradient)
+        if (!THIN_X) bl += lane < KT ? thin[m * KT + lane] : 0.f;
+#pragma unroll
+        for (int q = 0; q < KT; ++q) acc[q] += w * thin[m * KT + q];
+    }
+#pragma unroll
+    for (int q = 0; q < KT; ++q) red[wave][lane][q] = acc[q];
+    red[wave][lane][KT] = bw;
+    red[wave][lane][KT + 1] = bl;
+    __syncthreads();
+    if (wave != 0) return;
+    const int64_t NK = (int64_t)N * K;
+    if (c < C) {
+#pragma unroll
+        for (int q = 0; q < KT; ++q) {
+            const float v = ((red[0][lane][q] + red[1][lane][q]) + red[2][lane][q]) + red[3][lane][q];
+            const int64_t k = THIN_X ? q : c, n = THIN_X ? c : q;
+            part_w[blockIdx.y * NK + n * K + k] = in_scale ? v * in_scale[k] : v;
+        }
+        if (THIN_X) {
+            const float v = ((red[0][lane][KT] + red[1][lane][KT]) + red[2][lane][KT]) + red[3][lane][KT];
+            part_b[(int64_t)blockIdx.y * N + c] = v;
+        }
+    }
+    // gy is the thin operand: its column sums (the bias gradient), per wave in lanes < KT
+    if (!THIN_X && blockIdx.x == 0 && lane < KT) {
+        const float v = ((red[0][lane][KT + 1] + red[1][lane][KT + 1]) + red[2][lane][KT + 1]) + red[3][lane][KT + 1];
+        part_b[(int64_t)blockIdx.y * N + lane] = v;
+    }
 }
 
 // ---- RQ spline coupling, element math ------------------------------------------------------
@@ -866,8 +924,32 @@ extern "C" int nfx_linear_backward_data(const float* gy, const float* w, const f
     return gemm_launch(g, 0, 0, 1, (hipStream_t)stream);
 }
 
+static constexpr int kThin = 8;
+
+// row splits of the thin weight gradient: about 8 blocks per CU, at least 256 rows each
+static int64_t thin_splits(int64_t M, int N, int K) {
+    const int64_t C = K <= kThin ? N : K;
+    const int64_t gx = (C + 63) / 64;
+    int64_t s = (8 * (int64_t)num_cus() + gx - 1) / gx;
+    const int64_t maxs = (M + 255) / 256;
+    if (s > maxs) s = maxs;
+    if (s > 4096) s = 4096;
+    return s < 1 ? 1 : s;
+}
+
+template <bool THIN_X>
+static void thin_wgrad_go(int kt, dim3 grid, hipStream_t s, const float* gy, const float* x, const float* sc, int64_t M,
+                          int N, int K, int64_t rchunk, float* pw, float* pb) {
+    switch (kt) {
+#define NFX_THIN(KT) case KT: thin_wgrad_kernel<KT, THIN_X><<<grid, 256, 0, s>>>(gy, x, sc, M, N, K, rchunk, pw, pb); break;
+        NFX_THIN(1) NFX_THIN(2) NFX_THIN(3) NFX_THIN(4) NFX_THIN(5) NFX_THIN(6) NFX_THIN(7) NFX_THIN(8)
+#undef NFX_THIN
+    }
+}
+
 extern "C" size_t nfx_linear_workspace_bytes(int64_t M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0) return 0;
+    if (K <= kThin || N <= kThin) return (size_t)(thin_splits(M, N, K) * (int64_t)N * (K + 1) * sizeof(float));
     const int64_t s = wgrad_splits(N, K, M);
     const int64_t cs = (M + 4095) / 4096 < 1024 ? (M + 4095) / 4096 : 1024;
     const int64_t a = s * (int64_t)N * K, b = (cs < 1 ? 1 : cs) * (int64_t)N;
@@ -887,6 +969,24 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
         if (gb) (void)hipMemsetAsync(gb, 0, (size_t)N * sizeof(float), s);
         return check_launch("linear_backward_weight(memset)");
     }
+    const int64_t NK = (int64_t)N * K;
+    if (K <= kThin || N <= kThin) {
+        const bool thin_x = K <= kThin;
+        const int64_t splits = thin_splits(M, N, K);
+        const int64_t rchunk = (M + splits - 1) / splits;
+        const int64_t nz = (M + rchunk - 1) / rchunk;
+        const dim3 grid((unsigned)(((thin_x ? N : K) + 63) / 64), (unsigned)nz);
+        float* pb = ws + nz * NK;
+        if (thin_x) thin_wgrad_go<true>(K, grid, s, gy, x, in_scale, M, N, K, rchunk, ws, pb);
+        else thin_wgrad_go<false>(N, grid, s, gy, x, in_scale, M, N, K, rchunk, ws, pb);
+        int rc = check_launch("thin_wgrad_kernel");
+        if (rc) return rc;
+        split_reduce_kernel<<<(unsigned)((NK + 255) / 256 < 4096 ? (NK + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, NK, gw, 0, wmask);
+        rc = check_launch("split_reduce_kernel");
+        if (rc || !gb) return rc;
+        split_reduce_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(pb, nz, N, gb, 0, nullptr);
+        return check_launch("split_reduce_kernel");
+    }
     // gw [N][K] = sum_m gy[m][n] x[m][k] s[k]: A(n, m) = gy[m * N + n] (TA = 1), B(m, k) = x[m * K + k]
     const int64_t splits = wgrad_splits(N, K, M);
     int64_t kchunk = (M + splits - 1) / splits;
@@ -902,8 +1002,7 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
     g.nscale = in_scale;
     int rc = gemm_launch(g, 1, 0, nz, s);
     if (rc) return rc;
-    const int64_t n = (int64_t)N * K;
-    split_reduce_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, n, gw, 0, wmask);
+    split_reduce_kernel<<<(unsigned)((NK + 255) / 256 < 4096 ? (NK + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, NK, gw, 0, wmask);
     rc = check_launch("split_reduce_kernel");
     if (rc || !gb) return rc;
     int64_t cs = (M + 4095) / 4096;

@@ -44,7 +44,9 @@ def _close(c, c64, conditioning, what):
 
 
 @pytest.mark.parametrize("M,K,N", [(1000, 2, 64), (4097, 64, 64), (300, 128, 232), (70001, 128, 128),
-                                   (5, 3, 1), (1, 96, 33), (2048, 784, 64)])
+                                   (5, 3, 1), (1, 96, 33), (2048, 784, 64),
+                                   # the thin weight gradient (min(N, K) <= 8): x thin, gy thin, both
+                                   (100003, 8, 256), (3000, 96, 5), (777, 200, 8), (65, 7, 3)])
 def test_linear_kernels_vs_float64(cuda_device, M, K, N):
     g = torch.Generator().manual_seed(M + K + N)
     lin = nn.Linear(K, N)
@@ -78,11 +80,12 @@ def test_linear_kernels_vs_float64(cuda_device, M, K, N):
     _close(gb, gy.double().sum(0), gy.double().abs().sum(0), "bias grad")
 
 
-def test_linear_weight_grad_deterministic(cuda_device):
-    """Split-K partials are summed in a fixed order: bitwise identical on repeat."""
-    lin = nn.Linear(128, 128).to(cuda_device)
-    x = torch.randn(300000, 128, device=cuda_device)
-    gy = torch.randn(300000, 128, device=cuda_device)
+@pytest.mark.parametrize("K,N", [(128, 128), (2, 256), (256, 3)])
+def test_linear_weight_grad_deterministic(cuda_device, K, N):
+    """Split-K partials (MFMA and thin paths) are summed in a fixed order: bitwise identical on repeat."""
+    lin = nn.Linear(K, N).to(cuda_device)
+    x = torch.randn(300000, K, device=cuda_device)
+    gy = torch.randn(300000, N, device=cuda_device)
     a = G.linear_backward_weight(gy, x, lin)
     b = G.linear_backward_weight(gy, x, lin)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
