@@ -498,6 +498,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         if world > 1:
             dist.barrier()
         nfs_amd.reset_stats()
+        w0 = time.monotonic_ns()  # the timed window on the clock rocprofv3 stamps kernels with
         t0 = time.perf_counter()
         for _ in range(a.steps):
             out = step()
@@ -506,6 +507,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         if world > 1:
             dist.barrier()
         t = time.perf_counter() - t0
+        w1 = time.monotonic_ns()
         torch_calls = nfs_amd.STATS["torch"]
         hip_calls = nfs_amd.STATS["hip"]
         # Kernel durations: the same K steps again with HIP events around every layer launch
@@ -513,10 +515,17 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         # ~5 us of GPU idle between kernels (measured, profiles/).
         eager_only[0] = True
         aux_events = []
+        # A spin kernel ahead of every recorded pass keeps the GPU busy while the host enqueues the
+        # pass (eager: ~20 us of Python + ctypes per layer), so an event pair brackets the kernel
+        # itself, not the host's launch latency (which dominated short kernels: a 22 us layer read
+        # 35 us without it).
+        def preroll():
+            torch.cuda._sleep(int(1.2e7 if training else 2e6))
         if coupling_train:
             from nfs_amd.flows import coupling as _cp
             _cp.TRAIN_EVENTS = []
             for _ in range(a.steps):
+                preroll()
                 step()
             torch.cuda.synchronize()
             events = [e for e in _cp.TRAIN_EVENTS if e[0].endswith("<BWD2>")]
@@ -524,6 +533,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         elif training:
             bwd_mod.BACKWARD_EVENTS = []
             for _ in range(a.steps):
+                preroll()
                 step()
             torch.cuda.synchronize()
             events = [e for e in bwd_mod.BACKWARD_EVENTS if e[0] != "made_wgrad_kernel"]
@@ -532,6 +542,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         else:
             flow.layer_events = []
             for _ in range(a.steps):
+                preroll()
                 if sampling:
                     flow.forward(x)
                 else:
@@ -550,8 +561,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     durs = [e0.elapsed_time(e1) for _, e0, e1 in events]
     kname = events[0][0] if events else "?"
     mean_ms = sum(durs) / max(1, len(durs))
-    # one-launch coupling chain (nfx_affine_chain): one event covers every layer
-    layers_per_launch = len(flow.flows) if kname == "affine_chain_kernel" else 1
+    # one-launch coupling chains (nfx_affine_chain / nfx_spline_chain): one event covers every layer
+    layers_per_launch = len(flow.flows) if kname in ("affine_chain_kernel", "spline_chain_kernel") else 1
     f_launch = f_layer * layers_per_launch
     achieved = f_launch * B / (mean_ms * 1e-3) / 1e12
 
@@ -585,27 +596,27 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         return None
     traffic = None
     rocprof = None
-    tp = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
+    # rocprofv3 evidence for this config (tools/profile_bench.sh + tools/reconcile_profile.py):
+    # the trace of bench.py itself, the kernels inside ITS timed window, the same process's
+    # ms_per_step, and the PMC HBM bytes per launch of the hot kernel. Quoted beside the live
+    # event-timed numbers, with both step checks (same-run, and against this run's step).
+    rp_name = config if B == DEFAULT_BATCH.get(config) else f"{config}_{B}"
+    tp = os.path.join(ROOT, "profiles", f"rocprof_{rp_name}.json")
     if os.path.exists(tp):
         with open(tp) as fh:
-            tj = json.load(fh)
-        spl = tj.get("samples_per_launch")
-        if spl:
-            traffic = tj["hbm_bytes_per_launch"] / spl * B
-        # the same kernel's mean duration under rocprofv3 --kernel-trace (the profile the traffic
-        # counters come from), dispatch-weighted over its template instances: frac quoted on it too
-        src = os.path.join(ROOT, "profiles", tj.get("source", ""))
-        if spl and os.path.isfile(src):
-            with open(src) as fh:
-                sj = json.load(fh)
-            sj = sj.get(config, sj)  # per-config file: {kernel: stats}
-            ks = [sj[k] for k in tj.get("kernel", []) if k in sj and sj[k].get("mean_us")]
-            n = sum(k["dispatches"] for k in ks)
-            if n:
-                mus = sum(k["mean_us"] * k["dispatches"] for k in ks) / n
-                ach = f_launch * spl / (mus * 1e-6) / 1e12
-                rocprof = {"mean_launch_us": mus, "samples_per_launch": spl, "achieved": ach,
-                           "frac": ach / PEAK_FP32_TFLOPS, "source": os.path.relpath(src, ROOT)}
+            rj = json.load(fh)
+        spl = rj["bench_roofline"]["samples_per_launch"]
+        if rj.get("hbm_bytes_per_launch") and spl:
+            traffic = rj["hbm_bytes_per_launch"] / spl * B
+        rocprof = {"kernels": rj["hot_kernels"], "mean_launch_us": rj["rocprof_mean_launch_us"],
+                   "launches_per_step": rj["launches_per_step"], "samples_per_launch": spl,
+                   "achieved": rj["rocprof_achieved_tflops"], "frac": rj["rocprof_frac"],
+                   "frac_executed": rj.get("rocprof_frac_executed"),
+                   "kernel_ms_per_step": rj["rocprof_ms_per_step"],
+                   "profiled_run_ms_per_step": rj["bench"]["ms_per_step"],
+                   "fits_profiled_step": rj["fits_bench_step"],
+                   "profiled_run_event_frac": rj["event_frac"],
+                   "source": os.path.relpath(tp, ROOT), "round": rj.get("round")}
     result = {
         "metric": METRIC,
         "value": B_global * a.steps / t_max,
@@ -628,6 +639,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                    "launch": "hip-graph replay" if graph else "eager"},
         "nll_f64": nll,
         "reference_check": ref_check,
+        "timed_window_monotonic_ns": [w0, w1],
         "roofline": {"bound": "mfma", "pipe": "valu" if config == "cfg5i" else "mfma",
                      "kernel": kname, "achieved": achieved,
                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
@@ -638,6 +650,11 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                      "rocprof": rocprof},
         "cpu_baseline": None,
     }
+    if rocprof is not None:
+        # rocprof kernel time per step vs THIS run's step (a different process; the profiled run's
+        # own check is fits_profiled_step) and the rocprof frac vs this run's event frac
+        rocprof["fits_this_step"] = rocprof["kernel_ms_per_step"] <= result["ms_per_step"]
+        rocprof["frac_rel_diff_vs_events"] = abs(rocprof["frac"] - result["roofline"]["frac"]) / result["roofline"]["frac"]
     if config == "cfg4":
         fe = made_executed_flop_per_sample(63, 64)
         ach_e = fe * B / (mean_ms * 1e-3) / 1e12

@@ -112,8 +112,15 @@ int nfx_affine_kernel_policy(int policy);
  * between layers. log_det: written (accumulate = 0) or added to, as a chain of per-layer calls
  * would. `packs` is a HOST array of device pointers. The _logprob variant (inverse only) also
  * writes logp and the float64 [sum, count] partials like nfx_affine_coupling_logprob
- * (workspace: nfx_gauss_workspace_bytes(B)). Returns NFX_EUNSUPPORTED for batches whose rows
- * do not fit a workgroup's LDS (B > 4096 * 170 * 32 at d = 2). */
+ * (workspace: nfx_gauss_workspace_bytes(B)).
+ * Two layouts: up to 64k rows (or under policy NFX_AFFINE_SMALL) the small-batch one above; beyond
+ * (or under NFX_AFFINE_STREAMING) the streaming one for H <= 64 (csrc/nfx_affine_schain.hip: one
+ * workgroup per CU carries its rows through every layer, the per-layer arithmetic of the
+ * streaming nfx_affine_coupling kernel, bit-identical to those per-layer calls; the next layer's
+ * weights are DMA'd into LDS while the current layer runs). NFX_EUNSUPPORTED when neither takes
+ * (B, d, H): nfx_affine_chain_supported tells beforehand (host-only, no GPU call; it depends on
+ * the current kernel policy). */
+int nfx_affine_chain_supported(int64_t B, int d, int H);
 int nfx_affine_chain(const float* const* packs, int n_layers, const float* in, float* out,
                      float* log_det, int64_t B, int d, int H, int direction, int accumulate,
                      void* stream);
@@ -142,6 +149,24 @@ int nfx_spline_coupling_logprob(const float* packed, const float* in, float* out
                                 int H, int K, float bound, float min_bin_width,
                                 float min_bin_height, float min_derivative, int rescale,
                                 float data_min, float data_max, int accumulate, void* stream);
+
+/* A whole chain of SplineCouplingLayers in ONE launch (eval mode; NormalizingFlowModel /
+ * RealNVPSpline, spline_coupling_layer.py:96-180 chained by normalizing_flow_model.py:40-65):
+ * packs[l] = layer l's nfx_spline_pack image (a HOST array of device pointers), every layer
+ * d = 2 with the same H <= 64, K, bound and minimums, no data_min/data_max rescale; n_layers <= 64.
+ * direction +1 runs layers 0 .. n-1, -1 runs n-1 .. 0. One workgroup per CU carries its rows and
+ * running log-det in LDS through every layer (csrc/nfx_spline_schain_kernel.h) with the per-layer
+ * kernel's arithmetic: bit-identical to the per-layer nfx_spline_coupling calls. The _logprob
+ * variant (inverse only) adds the Gaussian log-density and float64 [sum, count] as
+ * nfx_spline_coupling_logprob. nfx_spline_chain_supported: host-only check of (B, d, H, K). */
+int nfx_spline_chain_supported(int64_t B, int d, int H, int K);
+int nfx_spline_chain(const float* const* packs, int n_layers, const float* in, float* out, float* log_det,
+                     int64_t B, int d, int H, int K, float bound, float min_bin_width, float min_bin_height,
+                     float min_derivative, int direction, int accumulate, void* stream);
+int nfx_spline_chain_logprob(const float* const* packs, int n_layers, const float* in, float* out,
+                             float* log_det, float* logp, double* sums, void* workspace, int64_t B, int d,
+                             int H, int K, float bound, float min_bin_width, float min_bin_height,
+                             float min_derivative, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Unit-interval RQ spline — rational_quadratic_spline

@@ -114,6 +114,8 @@ static std::atomic<int>& affine_policy() {
     return v;
 }
 
+int affine_policy_get() { return affine_policy().load(std::memory_order_relaxed); }
+
 typedef void (*affine_wide_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t, float*,
                               double*, float);
 

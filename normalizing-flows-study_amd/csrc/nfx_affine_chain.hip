@@ -14,14 +14,9 @@
 // The log-det accumulates in the reference's order: ld = ((0 + ld_first) + ...) + ld_last (or
 // starts from the caller's log-det when accumulate = 1); the last layer of an inverse chain can
 // add the fused Gaussian log-density and float64 NLL partials (LOGP), as nfx_*_logprob do.
-#include "nfx_affine_kernel.h"
+#include "nfx_chain.h"
 
 namespace nfx {
-
-constexpr int kChainMax = 64;
-struct NfxChainPacks {
-    const float* p[kChainMax];
-};
 
 template <int HT, int D, int DIR, bool LOGP>
 __global__ __launch_bounds__(128 * HT) void affine_chain_kernel(NfxChainPacks packs, int nl, const float* __restrict__ in,
@@ -204,6 +199,22 @@ static int chain_pad_d(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : 8); }
 // Rows of state one workgroup may carry: tiles * 32 * (D + 1) floats of dynamic LDS <= 64 KiB.
 static int64_t chain_max_tpw(int D) { return 65536 / (32 * (D + 1) * 4); }
 
+// Largest batch the small-batch chain fits (min(4 x CUs, kMaxPartials) workgroups of
+// chain_max_tpw tiles).
+static int64_t small_chain_max_b(int D) {
+    const int64_t cap = 4 * (int64_t)num_cus() < (int64_t)kMaxPartials ? 4 * (int64_t)num_cus() : (int64_t)kMaxPartials;
+    return cap * chain_max_tpw(D) * 32;
+}
+
+bool chain_supported(int64_t B, int d, int H) {
+    if (d != 2 && d != 4 && d != 8) return false;
+    if (H <= 0 || H > 128 || B < 0) return false;
+    const int pol = affine_policy_get();
+    const bool want_stream = pol == NFX_AFFINE_STREAMING || (pol == NFX_AFFINE_AUTO && B > kSmallChainMaxB);
+    if (want_stream && schain_supported(B, d, H)) return true;
+    return B <= small_chain_max_b(d);
+}
+
 static int chain_launch(const float* const* packs, int nl, const float* in, float* out, float* log_det, int64_t B,
                         int d, int H, int direction, int accumulate, float* logp, double* sums, void* workspace,
                         hipStream_t s) {
@@ -226,6 +237,13 @@ static int chain_launch(const float* const* packs, int nl, const float* in, floa
     }
     const int HT = (H + 31) / 32, D = chain_pad_d(d);
     if (d != D) return set_error(NFX_EUNSUPPORTED, "affine_chain: d=%d must be 2, 4 or 8 (row layout)", d);
+    // Layout: the streaming chain (nfx_affine_schain.hip, the per-layer streaming kernel's
+    // arithmetic) for large batches, the small-batch chain below otherwise; the affine kernel
+    // policy forces either (tests compare each with its per-layer kernel bit for bit).
+    const int pol = affine_policy_get();
+    const bool want_stream = pol == NFX_AFFINE_STREAMING || (pol == NFX_AFFINE_AUTO && B > kSmallChainMaxB);
+    if (want_stream && schain_supported(B, d, H))
+        return schain_launch(P, nl, in, out, log_det, B, d, H, direction, accumulate, logp, sums, workspace, s);
     affine_chain_t k = HT == 1 ? chain_pick_ht<1>(d, direction, fused)
                        : HT == 2 ? chain_pick_ht<2>(d, direction, fused)
                        : HT == 3 ? chain_pick_ht<3>(d, direction, fused) : chain_pick_ht<4>(d, direction, fused);
@@ -258,6 +276,8 @@ extern "C" int nfx_affine_chain(const float* const* packs, int n_layers, const f
     return chain_launch(packs, n_layers, in, out, log_det, B, d, H, direction, accumulate, nullptr, nullptr, nullptr,
                         (hipStream_t)stream);
 }
+
+extern "C" int nfx_affine_chain_supported(int64_t B, int d, int H) { return chain_supported(B, d, H) ? 1 : 0; }
 
 extern "C" int nfx_affine_chain_logprob(const float* const* packs, int n_layers, const float* in, float* out,
                                         float* log_det, float* logp, double* sums, void* workspace, int64_t B,

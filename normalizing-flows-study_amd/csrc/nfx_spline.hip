@@ -136,19 +136,8 @@ static int spline_launch(const float* packed, const float* in, float* out, float
     const int HT = (H + 31) / 32;
     spline_kernel_t k = pick_spline(HT, K, direction, fused, d);
     if (!k) return set_error(NFX_EUNSUPPORTED, "spline_coupling: no kernel for H=%d K=%d", H, K);
-    // Scalars exactly as the reference's Python-float expressions round them into fp32 ops.
-    SplineConsts C;
-    C.bound = bound;
-    C.two_bound = (float)(2.0 * (double)bound);
-    C.min_w = min_bin_width;
-    C.cw = (float)(1.0 - (double)min_bin_width * K);
-    C.min_h = min_bin_height;
-    C.ch = (float)(1.0 - (double)min_bin_height * K);
-    C.min_d = min_derivative;
-    C.rescale = rescale ? 1 : 0;
-    C.rs_lo = data_min;
-    C.rs_to_scale = rescale ? (float)((2.0 * bound) / ((double)data_max - (double)data_min)) : 1.f;
-    C.rs_from_scale = rescale ? (float)(((double)data_max - (double)data_min) / (2.0 * bound)) : 1.f;
+    const SplineConsts C =
+        spline_consts(K, bound, min_bin_width, min_bin_height, min_derivative, rescale, data_min, data_max);
     if (d > 8) {  // wide kernel: 32-sample tiles, weights from L2
         const size_t ldsw = (size_t)kSplineWideWaves * 32 * (d | 1) * sizeof(float);
         const int64_t ntiles = (B + 31) / 32;

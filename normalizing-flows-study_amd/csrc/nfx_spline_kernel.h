@@ -69,6 +69,24 @@ struct SplineConsts {
     float rs_from_scale;        // (hi-lo)/(2B)
 };
 
+// Scalars exactly as the reference's Python-float expressions round them into fp32 ops.
+inline SplineConsts spline_consts(int K, float bound, float min_bin_width, float min_bin_height, float min_derivative,
+                                  int rescale, float data_min, float data_max) {
+    SplineConsts C;
+    C.bound = bound;
+    C.two_bound = (float)(2.0 * (double)bound);
+    C.min_w = min_bin_width;
+    C.cw = (float)(1.0 - (double)min_bin_width * K);
+    C.min_h = min_bin_height;
+    C.ch = (float)(1.0 - (double)min_bin_height * K);
+    C.min_d = min_derivative;
+    C.rescale = rescale ? 1 : 0;
+    C.rs_lo = data_min;
+    C.rs_to_scale = rescale ? (float)((2.0 * bound) / ((double)data_max - (double)data_min)) : 1.f;
+    C.rs_from_scale = rescale ? (float)(((double)data_max - (double)data_min) / (2.0 * bound)) : 1.f;
+    return C;
+}
+
 // torch softplus (beta=1, threshold=20): x > 20 ? x : log1p(exp(x)).
 // log1p(u) = log(w) * u / (w - 1) with w = fl(1 + u) (exact u when w == 1): the rounding error
 // of 1 + u cancels in the ratio, giving log1p to a few ulp for every u > 0 at ~1/6 the cost of
@@ -244,6 +262,112 @@ __device__ __forceinline__ void rq_spline_elem(float v, const float (&p)[32], co
     }
     if (nonfinite(out)) out = v;      // :306
     if (nonfinite(lad)) lad = 0.f;    // :307
+}
+
+// The layer's conditioner MLP and splines for one unit (TILES = 2: a 64-sample chunk, 1: a
+// 32-sample half chunk) on the lane's own sample: xb = the layer-1 B operands (rescaled and
+// masked), xr = the lane's raw row. Returns the layer output row before the layer-level guard
+// (transformed dims replaced by the spline outputs, spline-guarded) and the spline log-det sum.
+// The streaming chain's copy (nfx_spline_schain.hip) of spline_coupling_kernel's unit body, the
+// same operations in the same order (bit-identical results); the per-layer kernel keeps its own
+// inline body (factoring it out perturbed its register allocation: K = 8 spilled 15 VGPRs).
+template <int HT, int K, int DIR, int DMAX, int TILES>
+__device__ __forceinline__ void spline_unit_apply(const float* P, const SplineLayout& L,
+                                                  const SplineConsts& C, int KS1, int NT, const float (&xb)[2][4],
+                                                  const float (&xr)[DMAX], float (&y)[DMAX], float& ld) {
+#pragma clang fp contract(off)
+    const int lane = lane_id(), h = lane >> 5;
+    // Layer 1 + ReLU
+    f32x16 h1[HT][2];
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) {
+        f32x16 a0, a1;
+        load_bias16_x2(P + L.b1 + ht * 32, h, a0, a1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            if (ks < KS1) {
+                const float w = P[L.w1 + (ht * 4 + ks) * 64 + lane];
+                a0 = mfma32(w, xb[0][ks], a0);
+                if constexpr (TILES == 2) a1 = mfma32(w, xb[1][ks], a1);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            a1[r] = trelu(a1[r]);
+        }
+        h1[ht][0] = a0;
+        h1[ht][1] = a1;
+    }
+    // Layer 2 + ReLU
+    f32x16 h2[HT][2];
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a0, a1;
+        load_bias16_x2(P + L.b2 + hto * 32, h, a0, a1);
+#pragma unroll
+        for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(
+                    P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
+                    if constexpr (TILES == 2) a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            a1[r] = trelu(a1[r]);
+        }
+        h2[hto][0] = a0;
+        h2[hto][1] = a1;
+    }
+
+    #pragma unroll
+    for (int j = 0; j < DMAX; ++j) y[j] = xr[j];
+    ld = 0.f;
+    for (int t = 0; t < NT; ++t) {
+        // Layer 3, tile t: the 3K-1 parameters of transformed dim tdim[t].
+        f32x16 a0, a1;
+        load_bias16_x2(P + L.b3 + t * 32, h, a0, a1);
+#pragma unroll
+        for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(
+                    P + L.w3 + (((t * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    a0 = mfma32(w[rr], h2[kt][0][4 * rq + rr], a0);
+                    if constexpr (TILES == 2) a1 = mfma32(w[rr], h2[kt][1][4 * rq + rr], a1);
+                }
+            }
+        }
+        // Half-wave exchange: afterwards every lane holds rows 0..31 of its own sample.
+        float prm[32];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0[r]), __float_as_uint(a1[r]),
+                                                       false, false);
+            prm[crow(r, 0)] = __uint_as_float(sw[0]);
+            prm[crow(r, 1)] = __uint_as_float(sw[1]);
+        }
+        const int dt = (int)P[L.tdim + t];
+        float v = 0.f;
+#pragma unroll
+        for (int j = 0; j < DMAX; ++j) v = (j == dt) ? xr[j] : v;
+        if (C.rescale) v = C.rs_to_scale * (v - C.rs_lo) - C.bound;
+        float o, l;
+        rq_spline_elem<K, (DIR < 0)>(v, prm, C, o, l);
+        if (C.rescale) o = (o + C.bound) * C.rs_from_scale + C.rs_lo;
+#pragma unroll
+        for (int j = 0; j < DMAX; ++j) y[j] = (j == dt) ? o : y[j];
+        ld = (t == 0) ? l : ld + l;
+    }
 }
 
 // DS = the data dimension when it is fixed at compile time (2: the two-moons-shaped BASELINE

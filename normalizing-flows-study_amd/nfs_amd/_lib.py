@@ -33,8 +33,9 @@ NFX_MADE_SEQ_WAVE = 2
 EXPORTED_SYMBOLS = (
     "nfx_abi_version", "nfx_last_error", "nfx_debug_fill_lds",
     "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
-    "nfx_affine_kernel_policy", "nfx_affine_chain", "nfx_affine_chain_logprob",
+    "nfx_affine_kernel_policy", "nfx_affine_chain", "nfx_affine_chain_logprob", "nfx_affine_chain_supported",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
+    "nfx_spline_chain_supported", "nfx_spline_chain", "nfx_spline_chain_logprob",
     "nfx_rqs_unit",
     "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob", "nfx_made_seq_policy",
@@ -119,6 +120,7 @@ _SIGNATURES = {
     "nfx_spline_elem_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int, _int, _vp]),
     "nfx_spline_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f, _f, _int,
                                         _vp]),
+    "nfx_affine_chain_supported": (_int, [_i64, _int, _int]),
     "nfx_affine_chain": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,
                                         _int, _vp]),
@@ -132,6 +134,11 @@ _SIGNATURES = {
                                    _int, _f, _f, _int, _int, _vp]),
     "nfx_spline_coupling_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f,
                                            _f, _f, _int, _f, _f, _int, _vp]),
+    "nfx_spline_chain_supported": (_int, [_i64, _int, _int, _int]),
+    "nfx_spline_chain": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _f,
+                                _int, _int, _vp]),
+    "nfx_spline_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,
+                                        _int, _f, _f, _f, _f, _int, _vp]),
     "nfx_rqs_unit": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int, _vp]),
     "nfx_made_packed_floats": (_sz, [_int, _int]),
     "nfx_made_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),

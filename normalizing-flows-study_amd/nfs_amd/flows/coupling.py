@@ -39,9 +39,11 @@ ctypes_vp = ctypes.c_void_p
 # here (bench.py roofline timing); None = no events.
 TRAIN_EVENTS = None
 
-# One-launch layer chains (nfx_affine_chain, csrc/nfx_affine_chain.hip) are used for batches up to
-# this many samples; above it the per-layer streaming kernels (higher MFMA efficiency) run.
-CHAIN_MAX_B = int(os.environ.get("NFX_CHAIN_MAX_B", str(1 << 16)))
+# One-launch layer chains (nfx_affine_chain: the small-batch layout of csrc/nfx_affine_chain.hip
+# up to 64k samples, the streaming layout of csrc/nfx_affine_schain.hip above) run every batch the
+# library accepts (nfx_affine_chain_supported) up to this many samples; 0 disables them (tests
+# compare them with the per-layer kernels).
+CHAIN_MAX_B = int(os.environ.get("NFX_CHAIN_MAX_B", str(1 << 62)))
 # Tests: route every call through the any-shape path (csrc/nfx_generic.hip) even where a fused
 # kernel exists, to pin it against the same fixtures.
 FORCE_GENERIC = False
@@ -50,7 +52,8 @@ GENERIC_MAX_H = 1024  # conditioner BatchNorm moments (nfx_flowbn_moments): <= 1
 
 def chain_ok(flows, x):
     """A run of eval-mode CouplingLayers with one (d, H), d in {2, 4, 8}, H <= 128, on fp32 ROCm
-    rows, small enough for the one-launch chain kernel."""
+    rows, that a one-launch chain kernel takes (the streaming chain: H <= 64; the small-batch
+    chain: up to ~1M rows at d = 2)."""
     if FORCE_GENERIC or not flows or len(flows) > 64 or x.shape[0] > CHAIN_MAX_B or x.shape[0] == 0:
         return False
     f0 = flows[0]
@@ -58,6 +61,8 @@ def chain_ok(flows, x):
         return False
     d, H = f0.data_dim, f0._hidden()
     if d not in (2, 4, 8) or H > MAX_H or x.shape[1] != d:
+        return False
+    if not _lib.lib().nfx_affine_chain_supported(x.shape[0], d, H):
         return False
     for f in flows:
         if type(f) is not CouplingLayer or f.data_dim != d or f._hidden() != H or f._torch_only():

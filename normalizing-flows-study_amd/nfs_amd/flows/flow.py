@@ -274,10 +274,12 @@ class SequentialFlow(Flow):
         x = x.contiguous()
         ld = torch.zeros(x.shape[0], device=x.device, dtype=torch.float32)
         from . import coupling as _coupling
-        if _coupling.chain_ok(list(self.flows), x):  # one launch (csrc/nfx_affine_chain.hip)
-            out = torch.empty_like(x)
-            _coupling.chain_launch(list(self.flows), x, out, ld, direction, True)
-            return out, ld
+        from . import spline as _spline
+        for mod in (_coupling, _spline):  # one launch (csrc/nfx_affine_*chain*, nfx_spline_schain*)
+            if mod.chain_ok(list(self.flows), x):
+                out = torch.empty_like(x)
+                mod.chain_launch(list(self.flows), x, out, ld, direction, True)
+                return out, ld
         bufs = [torch.empty_like(x), torch.empty_like(x)]
         cur, k = x, 0
         for f in (self.flows if direction > 0 else reversed(self.flows)):

@@ -9,6 +9,9 @@ bin search, the RQ spline (forward or citardauq inverse), guards and log-det.
 `rational_quadratic_spline` is the stand-alone unit-interval spline of
 src/flows/spline/rational_quadratic_spline.py:4-104 (elementwise kernel nfx_rqs_unit on GPU).
 """
+import ctypes
+import os
+
 import torch
 import torch.nn as nn
 from torch.nn import functional as F
@@ -354,6 +357,56 @@ class SplineCouplingLayer(HipFlow):
             float(self.min_bin_height), float(self.min_derivative), rescale, lo, hi,
             int(bool(accumulate)), _lib.stream_of(x)), "nfx_spline_coupling_logprob")
         return True
+
+
+# One-launch chains of SplineCouplingLayers (nfx_spline_chain, csrc/nfx_spline_schain_kernel.h) run
+# every batch of at least this many samples (0 = every batch); NFX_SPLINE_CHAIN_MIN_B overrides,
+# tests set CHAIN_ENABLED = False to compare with the per-layer kernels.
+CHAIN_ENABLED = True
+CHAIN_MIN_B = int(os.environ.get("NFX_SPLINE_CHAIN_MIN_B", "0"))
+
+
+def chain_ok(flows, x):
+    """A run of eval-mode SplineCouplingLayers, d = 2, one (H, K, bound, minimums), no rescale, on
+    fp32 ROCm rows that nfx_spline_chain takes."""
+    if not CHAIN_ENABLED or FORCE_GENERIC or not flows or len(flows) > 64 or x.shape[0] < max(1, CHAIN_MIN_B):
+        return False
+    f0 = flows[0]
+    if type(f0) is not SplineCouplingLayer:
+        return False
+    key = (f0.data_dim, f0._hidden(), f0.num_bins, float(f0.bound), float(f0.min_bin_width),
+           float(f0.min_bin_height), float(f0.min_derivative))
+    if x.dim() != 2 or x.shape[1] != f0.data_dim:
+        return False
+    for f in flows:
+        if type(f) is not SplineCouplingLayer or f._torch_only() or not f._fused_family():
+            return False
+        if f._rescale_scalars() != (0, 0.0, 0.0):
+            return False
+        if (f.data_dim, f._hidden(), f.num_bins, float(f.bound), float(f.min_bin_width), float(f.min_bin_height),
+                float(f.min_derivative)) != key:
+            return False
+    return bool(_lib.lib().nfx_spline_chain_supported(x.shape[0], key[0], key[1], key[2]))
+
+
+def chain_launch(flows, x, out, ld, direction, accumulate, logprob=None):
+    """All `flows` (module order) in one nfx_spline_chain launch; logprob=(logp, sums, workspace)
+    adds the fused Gaussian log-density to an inverse chain."""
+    packs = (ctypes.c_void_p * len(flows))(*[_lib.ptr(f._packed(x.device, f._build_pack)) for f in flows])
+    f0 = flows[0]
+    L = _lib.lib()
+    p = _lib.ptr
+    consts = (float(f0.bound), float(f0.min_bin_width), float(f0.min_bin_height), float(f0.min_derivative))
+    if logprob is not None:
+        logp, sums, ws = logprob
+        _lib.check(L.nfx_spline_chain_logprob(packs, len(flows), p(x), p(out), p(ld), p(logp), p(sums), p(ws),
+                                              x.shape[0], f0.data_dim, f0._hidden(), f0.num_bins, *consts,
+                                              int(bool(accumulate)), _lib.stream_of(x)), "nfx_spline_chain_logprob")
+    else:
+        _lib.check(L.nfx_spline_chain(packs, len(flows), p(x), p(out), p(ld), x.shape[0], f0.data_dim, f0._hidden(),
+                                      f0.num_bins, *consts, int(direction), int(bool(accumulate)), _lib.stream_of(x)),
+                   "nfx_spline_chain")
+    STATS["hip"] += 1
 
 
 def _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,

@@ -19,6 +19,7 @@ import torch.nn as nn
 from .. import _lib
 from ..distributed import merge_bn_stats, sync_bn_world
 from ..flows import coupling as _coupling
+from ..flows import spline as _spline
 from ..flows.flow import HipFlow, STATS
 
 
@@ -129,17 +130,21 @@ class NormalizingFlowModel(nn.Module):
         B = x.shape[0]
         ld = torch.empty(B, device=x.device, dtype=torch.float32)
         n = len(self.flows)
-        if not self.batch_norm_between_layers and _coupling.chain_ok(list(self.flows), x):
-            # the whole chain in one launch (csrc/nfx_affine_chain.hip), same roundings
+        chain = None
+        if not self.batch_norm_between_layers:
+            chain = next((m for m in (_coupling, _spline) if m.chain_ok(list(self.flows), x)), None)
+        if chain is not None:
+            # the whole chain in one launch (csrc/nfx_affine_chain.hip / nfx_affine_schain.hip /
+            # nfx_spline_schain_kernel.h), the per-layer kernels' roundings
             out = torch.empty_like(x)
             ev = self.layer_events
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            _coupling.chain_launch(list(self.flows), x, out, ld, direction, False, logprob)
+            chain.chain_launch(list(self.flows), x, out, ld, direction, False, logprob)
             if ev is not None:
                 e1.record()
-                ev.append(("affine_chain_kernel", e0, e1))
+                ev.append(("affine_chain_kernel" if chain is _coupling else "spline_chain_kernel", e0, e1))
             return (out, ld, True) if logprob is not None else (out, ld)
         bufs = [torch.empty_like(x), torch.empty_like(x)]
         order = range(n) if direction > 0 else reversed(range(n))

@@ -116,3 +116,65 @@ def test_chain_sequential_flow_and_graph(cuda_device):
         yg = gf()
     yg = yg[0] if isinstance(yg, tuple) else yg
     assert torch.equal(yg, ye)
+
+
+def _policy(pol, fn, chain=True):
+    """Run fn under nfx_affine_kernel_policy(pol), with the one-launch chains on or off."""
+    L = _lib.lib()
+    old_max = _cp.CHAIN_MAX_B
+    if not chain:
+        _cp.CHAIN_MAX_B = 0
+    old_pol = L.nfx_affine_kernel_policy(pol)
+    try:
+        return fn()
+    finally:
+        _cp.CHAIN_MAX_B = old_max
+        L.nfx_affine_kernel_policy(old_pol)
+
+
+@pytest.mark.parametrize("d,H,nl,B", [(2, 64, 8, 125000), (2, 64, 8, 1), (2, 64, 2, 65), (2, 32, 3, 70001),
+                                      (4, 64, 5, 200003), (8, 64, 4, 600001), (8, 16, 6, 9999),
+                                      (2, 64, 8, 2_000_001)])
+def test_streaming_chain_equals_per_layer_bitwise(cuda_device, d, H, nl, B):
+    """The streaming chain (csrc/nfx_affine_schain.hip: rows in LDS through every layer, the next
+    layer's weights DMA'd during the current one) runs the per-layer streaming kernel's arithmetic:
+    y, log-det and logp equal the per-layer streaming launches bit for bit; the float64 NLL sums
+    (summed in another order) to 1e-12. B = 2,000,001 at d = 2 and 600,001 at d = 8 take more than
+    one LDS slice per workgroup; B = 1 and 65 leave most workgroups without rows."""
+    S = _lib.NFX_AFFINE_STREAMING
+    m = _model(d, H, nl, d * 1000 + H + nl).to(cuda_device).eval()
+    x = torch.randn(B, d, device=cuda_device, generator=torch.Generator(device=cuda_device).manual_seed(B))
+    if B > 4:
+        x[0, 0] = float("nan")
+        x[1, -1] = float("inf")
+        x[2] = 1e10
+    assert _policy(S, lambda: _cp.chain_ok(list(m.flows), x))
+    with torch.no_grad():
+        nfs_amd.reset_stats()
+        zc, ldc = _policy(S, lambda: m.inverse(x))
+        xc, lfc = _policy(S, lambda: m.forward(x))
+        lpc, sc = _policy(S, lambda: m.log_prob(x, return_sums=True))
+        assert nfs_amd.STATS["hip"] == 3 and nfs_amd.STATS["torch"] == 0, nfs_amd.STATS  # one launch each
+        zp, ldp = _policy(S, lambda: m.inverse(x), chain=False)
+        xp, lfp = _policy(S, lambda: m.forward(x), chain=False)
+        lpp, sp = _policy(S, lambda: m.log_prob(x, return_sums=True), chain=False)
+    for a, b, what in ((zc, zp, "z"), (ldc, ldp, "ld"), (xc, xp, "x"), (lfc, lfp, "fwd ld"), (lpc, lpp, "logp")):
+        assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(b, nan=7.0)), what
+        assert torch.equal(torch.isnan(a), torch.isnan(b)), what
+    assert float(sc[1]) == float(sp[1]) == B
+    assert abs(float(sc[0]) - float(sp[0])) <= 1e-12 * max(1.0, abs(float(sp[0]))), (sc, sp)
+
+
+def test_streaming_chain_realnvp_vs_reference(cuda_device):
+    """G2 through the streaming chain (policy forced) and the G8 full-scale cfg2 NLL at 1M rows
+    through the default (AUTO) route, which is the streaming chain at that batch."""
+    g = load_golden("g2_realnvp.npz")
+    m = nfs_amd.RealNVP(2, 8, 64)
+    m.load_state_dict(state_dict_from(g, "", m))
+    m = m.to(cuda_device).eval()
+    x = torch.from_numpy(g["x"]).to(cuda_device)
+    with torch.no_grad():
+        zi, ldi = _policy(_lib.NFX_AFFINE_STREAMING, lambda: m.inverse(x))
+    a, ref = zi.cpu().numpy().astype(np.float64), g["inv_z"].astype(np.float64)
+    assert (np.abs(a - ref) <= 1e-5 * (1 + np.abs(ref))).all()
+    assert np.abs(ldi.cpu().numpy() - g["inv_ld"]).max() <= 1e-4

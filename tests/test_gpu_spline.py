@@ -62,7 +62,7 @@ def test_spline_model_vs_reference(cuda_device, tag):
         zi, ldi = m.inverse(x)
         xf, ldf = m.forward(z)
         lp = m.log_prob(x)
-    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] >= 16
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] >= 3  # one chain launch per call
     K = 8 if tag == "k8." else 10
     spec = [("spline", f"{'flow.' if K == 10 else ''}flows.{i}.", {"K": K}) for i in range(8)]
     sd = sd64(oracle_sd(g, tag))

@@ -1,0 +1,177 @@
+"""Reconcile a rocprofv3 trace of bench.py with the bench line the same process printed.
+
+    python tools/reconcile_profile.py gpurun_out/prof_<tag> <round tag, e.g. r04>
+
+For every config directory written by tools/profile_bench.sh (bench.json = the bench line,
+trace/ = rocprofv3 --kernel-trace --stats of that same process, optional fetch/ and write/ =
+the FETCH_SIZE / WRITE_SIZE passes) this writes profiles/<round>_<cfg>.json with
+  * the per-kernel dispatch counts and mean durations (kernel_stats.csv),
+  * the hot kernel's launches per step (the bench's event pass: launches / steps),
+  * rocprof_ms_per_step = the summed duration of every kernel dispatched inside the bench's timed
+    window (bench.py prints it as timed_window_monotonic_ns, on the clock rocprofv3 stamps kernels
+    with) / steps, and the hot kernel's mean over those dispatches only (no warm-up ramps),
+  * the check rocprof_ms_per_step <= the bench's own ms_per_step (same process, same clock),
+  * the rocprof frac (algorithmic flop per launch / rocprof mean / peak) next to the event frac,
+  * with the PMC passes: HBM bytes per launch (FETCH_SIZE doubled per MI355X_MICROARCH.md, gfx950
+    reports half of a wide streaming read; WRITE_SIZE as reported), dispatch-weighted.
+and copies the kernel_stats.csv next to it (profiles/<round>_<cfg>_kernel_stats.csv).
+bench.py quotes profiles/rocprof_<cfg>.json (the latest reconciled file per config).
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PEAK = 157.3
+
+# hot-kernel name fragments per config family (template instances are summed)
+HOT = {
+    "cfg2": ("affine_coupling_kernel", "affine_schain_kernel", "affine_chain_kernel"),
+    "cfg3": ("spline_coupling_kernel", "spline_schain_kernel"),
+    "cfg4": ("made_tile_kernel",),
+    "cfg5i": ("made_seqs_kernel", "made_seqw_kernel"),
+    "cfg5f": ("made_wide_kernel",),
+    "sample4k": ("affine_chain_kernel", "affine_small_kernel", "affine_coupling_kernel"),
+    "sample4k_spline": ("spline_coupling_kernel", "spline_schain_kernel"),
+    "sample4k_maf": ("made_seqs_kernel", "made_seqw_kernel", "made_seq_kernel"),
+    "sample4k_iaf": ("made_tile_kernel",),
+}
+PER_PASS = ("gauss_finish_kernel",)  # once per log_prob pass besides the layer kernels
+
+
+def _kernel_stats(path):
+    out = {}
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            name = r["Name"].split("(")[0].replace("void ", "")
+            out[name] = {"dispatches": int(r["Calls"]), "mean_us": float(r["AverageNs"]) / 1e3,
+                         "total_us": float(r["TotalDurationNs"]) / 1e3}
+    return out
+
+
+def _counter(path, counter):
+    """Per-dispatch counter values of counter_collection.csv: {kernel: [value, ...]}"""
+    out = {}
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            out.setdefault(name, []).append(float(r["Counter_Value"]))
+    return out
+
+
+def reconcile(cdir, rtag):
+    name = os.path.basename(cdir.rstrip("/"))
+    cfg = name.split("_")[0] if not name.startswith("sample4k") else "_".join(
+        p for p in name.split("_") if not p.isdigit())
+    with open(os.path.join(cdir, "bench.json")) as fh:
+        bench = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
+    ks_path = glob.glob(os.path.join(cdir, "trace", "*", "*_kernel_stats.csv"))[0]
+    ks = _kernel_stats(ks_path)
+    frags = HOT.get(cfg, ())
+    rf = bench["roofline"]
+    win = bench.get("timed_window_monotonic_ns")
+    tr = glob.glob(os.path.join(cdir, "trace", "*", "*_kernel_trace.csv"))
+    if win and tr:
+        # exactly the kernels of the timed steps: dispatches inside the bench's timed window
+        # (bench.py stamps it with time.monotonic_ns, the clock rocprofv3 stamps kernels with)
+        with open(tr[0]) as fh:
+            rows = [r for r in csv.DictReader(fh)
+                    if int(r["Start_Timestamp"]) >= win[0] and int(r["End_Timestamp"]) <= win[1]]
+        win_k = {}
+        for r in rows:
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            e = win_k.setdefault(k, {"dispatches": 0, "total_us": 0.0})
+            e["dispatches"] += 1
+            e["total_us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        for e in win_k.values():
+            e["mean_us"] = e["total_us"] / e["dispatches"]
+        hot = {k: v for k, v in win_k.items() if any(f in k for f in frags)}
+        n_hot = sum(v["dispatches"] for v in hot.values())
+        lps = n_hot / bench["steps"]
+        passes = bench["steps"]
+        hot_ms = sum(v["total_us"] for v in hot.values()) / passes / 1e3
+        extra_ms = (sum(v["total_us"] for v in win_k.values()) / passes / 1e3) - hot_ms  # every other kernel
+        window = {"kernels_in_window": win_k, "span_ms": (win[1] - win[0]) / 1e6}
+    else:
+        # no window: every dispatch of the process (warm-up ramps included), per pass
+        hot = {k: v for k, v in ks.items() if any(f in k for f in frags)}
+        lps = rf["launches"] / bench["steps"]  # launches of the hot kernel per pass (event pass)
+        n_hot = sum(v["dispatches"] for v in hot.values())
+        passes = n_hot / lps
+        hot_ms = sum(v["total_us"] for v in hot.values()) / passes / 1e3
+        extra = {k: v for k, v in ks.items() if any(f in k for f in PER_PASS)}
+        extra_ms = sum(v["total_us"] for v in extra.values()) / passes / 1e3
+        window = None
+    mean_us = sum(v["total_us"] for v in hot.values()) / n_hot
+    f_launch = rf["flop_per_sample_per_launch"]
+    spl = rf["samples_per_launch"]
+    ach = f_launch * spl / (mean_us * 1e-6) / 1e12
+    res = {
+        "config": name, "round": rtag,
+        "bench": {k: bench.get(k) for k in ("value", "ms_per_step", "steps", "warmup", "n_gpus")},
+        "bench_roofline": {k: rf.get(k) for k in ("kernel", "mean_launch_ms", "launches", "frac",
+                                                    "frac_executed", "flop_per_sample_per_launch",
+                                                    "samples_per_launch")},
+        "kernels_process": ks, "timed_window": window, "hot_kernels": sorted(hot), "launches_per_step": lps,
+        "passes_counted": passes,
+        "rocprof_mean_launch_us": mean_us,
+        "rocprof_hot_ms_per_step": hot_ms,
+        "rocprof_ms_per_step": hot_ms + extra_ms,
+        "fits_bench_step": hot_ms + extra_ms <= bench["ms_per_step"],
+        "rocprof_achieved_tflops": ach, "rocprof_frac": ach / PEAK,
+        "event_frac": rf["frac"], "frac_rel_diff": abs(ach / PEAK - rf["frac"]) / rf["frac"],
+        "source": {"kernel_stats": os.path.relpath(ks_path, ROOT),
+                   "bench": os.path.relpath(os.path.join(cdir, "bench.json"), ROOT)},
+    }
+    if rf.get("frac_executed"):
+        fe = rf["flop_per_sample_executed"]
+        res["rocprof_frac_executed"] = fe * spl / (mean_us * 1e-6) / 1e12 / PEAK
+    fetch = glob.glob(os.path.join(cdir, "fetch", "*", "*counter_collection.csv"))
+    write = glob.glob(os.path.join(cdir, "write", "*", "*counter_collection.csv"))
+    if fetch and write:
+        fv, wv = _counter(fetch[0], "FETCH_SIZE"), _counter(write[0], "WRITE_SIZE")
+        fs = [v for k, vs in fv.items() if k in hot for v in vs]
+        ws = [v for k, vs in wv.items() if k in hot for v in vs]
+        if fs and ws:
+            fb = 2 * 1024 * sum(fs) / len(fs)  # KB, doubled (gfx950 FETCH_SIZE correction)
+            wb = 1024 * sum(ws) / len(ws)
+            res["hbm_bytes_per_launch"] = fb + wb
+            res["fetch_bytes_corrected"] = fb
+            res["write_bytes"] = wb
+            res["pmc_dispatches"] = len(fs)
+            res["pmc_note"] = ("FETCH_SIZE (KB) doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide "
+                               "streaming read), WRITE_SIZE as reported; mean over the hot kernel's dispatches")
+    out = os.path.join(ROOT, "profiles", f"{rtag}_{name}.json")
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    shutil.copy(ks_path, os.path.join(ROOT, "profiles", f"{rtag}_{name}_kernel_stats.csv"))
+    # the file bench.py quotes for this config (full-batch runs only)
+    if name in HOT or name == cfg and name in HOT:
+        with open(os.path.join(ROOT, "profiles", f"rocprof_{name}.json"), "w") as fh:
+            json.dump(res, fh, indent=1)
+    return res
+
+
+def main():
+    pdir, rtag = sys.argv[1], sys.argv[2]
+    for cdir in sorted(glob.glob(os.path.join(pdir, "*"))):
+        if not os.path.isfile(os.path.join(cdir, "bench.json")):
+            continue
+        try:
+            r = reconcile(cdir, rtag)
+        except Exception as e:  # noqa: BLE001 - report and continue with the other configs
+            print(f"{cdir}: {e}")
+            continue
+        print(f"{r['config']:>18}: step {r['bench']['ms_per_step']:.4f} ms, rocprof kernels/step "
+              f"{r['rocprof_ms_per_step']:.4f} ms (fits: {r['fits_bench_step']}), mean {r['rocprof_mean_launch_us']:.1f} us"
+              f" x {r['launches_per_step']:.0f}, frac rocprof {r['rocprof_frac']:.3f} / events {r['event_frac']:.3f}"
+              + (f", HBM {r['hbm_bytes_per_launch']/1e6:.1f} MB/launch" if "hbm_bytes_per_launch" in r else ""))
+
+
+if __name__ == "__main__":
+    main()
