@@ -250,6 +250,10 @@ static std::atomic<int>& made_seq_policy() {
     return v;
 }
 
+namespace nfx {
+int made_seq_policy_get() { return made_seq_policy().load(std::memory_order_relaxed); }
+}  // namespace nfx
+
 static int made_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
                        int d, int H, int variant, int accumulate, float* logp, double* sums,
                        void* workspace, hipStream_t s) {

@@ -301,6 +301,28 @@ static made_seq_bwd_t seq_bwd_pick(int HT) {
     }
 }
 
+bool made_seqw_bwd_supported(int d, int H);
+int made_seqw_bwd_launch(const float* packed, const float* in, const float* gout, const float* gld, float* gin,
+                         float* fac, int64_t B, int d, int H, int variant, hipStream_t s);
+int made_seq_policy_get();
+
+// Which sequential backward runs (nfx_made_seq_policy): SEGMENT = this file's lane-per-sample
+// kernel, WAVE = made_seqw_bwd_kernel (a wave per sample, H <= 64, d <= 1024), AUTO = by a cost
+// model of instruction issue per SIMD: the lane kernel runs ceil(B / 64 / SIMDs) rounds of a lane's
+// serial sweeps (~ d*6Hp + 8Hp^2 VALU), the wave kernel ceil(B / SIMDs) samples per SIMD of
+// ~ 80d + 30Hp instructions (reductions, rank-1 updates, the completions' broadcast FMAs).
+static bool seq_bwd_use_wave(int64_t B, int d, int H) {
+    if (!made_seqw_bwd_supported(d, H)) return false;
+    const int pol = made_seq_policy_get();
+    if (pol == NFX_MADE_SEQ_WAVE) return true;
+    if (pol == NFX_MADE_SEQ_SEGMENT) return false;
+    const int64_t simds = 4 * (int64_t)num_cus();
+    const int64_t Hp = 32 * ((H + 31) / 32);
+    const double lane = (double)((B + 64 * simds - 1) / (64 * simds)) * (double)(d * 6 * Hp + 8 * Hp * Hp);
+    const double wave = (double)((B + simds - 1) / simds) * (double)(80 * d + 30 * Hp);
+    return wave < lane;
+}
+
 }  // namespace nfx
 
 using namespace nfx;
@@ -323,6 +345,9 @@ extern "C" int nfx_made_seq_backward(const float* packed, const float* in, const
     if (B == 0) return NFX_OK;
     if (!packed || !in || !grad_out || !grad_log_det || !grad_in || !factors)
         return set_error(NFX_EINVAL, "made_seq_backward: null pointer");
+    if (seq_bwd_use_wave(B, d, H))
+        return made_seqw_bwd_launch(packed, in, grad_out, grad_log_det, grad_in, factors, B, d, H, variant,
+                                    (hipStream_t)stream);
     const int HT = (H + 31) / 32;
     made_seq_bwd_t k = variant == NFX_IAF_INVERSE ? seq_bwd_pick<NFX_IAF_INVERSE>(HT) : seq_bwd_pick<NFX_MAF_FORWARD>(HT);
     const size_t lds = (size_t)3 * 64 * (32 * HT + 4) * sizeof(float);

@@ -160,6 +160,25 @@ def test_all_directions_backward_vs_float64_autograd(cuda_device, kind, directio
         _close_or_ref(g, r, r32, 2e-5, k)
 
 
+@pytest.mark.parametrize("policy", ["wave", "segment"])
+@pytest.mark.parametrize("kind,direction,d,H,B", [
+    ("iaf", -1, 2, 64, 2000), ("iaf", -1, 5, 16, 1), ("iaf", -1, 20, 32, 300), ("iaf", -1, 100, 48, 64),
+    ("iaf", -1, 784, 64, 6), ("maf", 1, 2, 64, 2000), ("maf", 1, 5, 16, 77), ("maf", 1, 63, 64, 300),
+])
+def test_sequential_backward_both_kernels(cuda_device, kind, direction, d, H, B, policy):
+    """The sequential directions' backward on both kernels (nfx_made_seq_policy): the
+    lane-per-sample reverse sweep (made_seq_bwd_kernel) and the wave-per-sample one
+    (made_seqw_bwd_kernel, H <= 64), against float64 autograd side by side with the fp32
+    composite; d = 2, H = 64, B = 2,000 is the reference's IAF / MAF figure-model layer."""
+    from nfs_amd import _lib
+    L = _lib.lib()
+    old = L.nfx_made_seq_policy(_lib.NFX_MADE_SEQ_WAVE if policy == "wave" else _lib.NFX_MADE_SEQ_SEGMENT)
+    try:
+        test_all_directions_backward_vs_float64_autograd(cuda_device, kind, direction, d, H, B)
+    finally:
+        L.nfx_made_seq_policy(old)
+
+
 def test_iaf_density_training_step(cuda_device):
     """NormalizingFlowModel of IAF layers trained on the density direction (the reference's
     IAF.inverse under -log_prob): loss and every gradient match float64 autograd."""
