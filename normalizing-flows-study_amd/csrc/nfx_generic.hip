@@ -206,12 +206,195 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     }
 }
 
+// ---- large-tile GEMM (M >= 128, N >= 64) -------------------------------------------------------
+// 128 x BN output tile per 256-thread workgroup, 2 x 2 waves of 64 x BN/2, i.e. 2 x BN/64
+// independent 32 x 32 accumulators per wave. The K tile (16 = 8 MFMA k-steps) sits in LDS split by
+// k parity, A as [h][m][s] and B as [h][n][s] (k = 2s + h, rows padded to 12 floats), so a lane's
+// four k-steps of one 32-row operand are ONE ds_read_b128 (12-float rows: the 16 rows of a
+// ds_read_b128 lane group land on 16 different 16-B bank slots) and a k-step feeds 2 x BN/64
+// MFMAs from 2 + BN/64 fragments already in registers. Double-buffered: the next K tile's global
+// loads are in flight during the current tile's MFMAs and are parked into the other buffer after
+// them, one barrier per K tile. The k-steps run in increasing k like gemm_kernel's, so both produce
+// the same sums.
+constexpr int kG2M = 128, kG2K = 16, kG2RS = 12;
+
+template <int TA, int TB, bool VA, bool VB, int BN>
+__global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
+    constexpr int NJ = BN / 64;                 // 32-column tiles per wave
+    constexpr int ASZ = 2 * kG2M * kG2RS;       // floats of one A stage
+    constexpr int BSZ = 2 * BN * kG2RS;
+    __shared__ __attribute__((aligned(16))) float sm[2 * (ASZ + BSZ)];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, h = lane >> 5, col = lane & 31;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int64_t m0 = (int64_t)blockIdx.x * kG2M, n0 = (int64_t)blockIdx.y * BN;
+    const int64_t kb = (int64_t)blockIdx.z * g.kchunk;
+    const int64_t ke = kb + g.kchunk < g.K ? kb + g.kchunk : g.K;
+    // A tile: 128 x 16 = 512 float4 -> 2 per thread; B tile: BN x 16 -> BN / 64 per thread
+    constexpr int NA = 2, NB = BN / 64;
+    float ra[NA][4], rb[NB][4];
+    auto ld4 = [](const float* p, const float* msk, int64_t r, int64_t c, int64_t ld, int64_t rmax, int64_t cmax,
+                  bool vec, float (&o)[4]) {
+        if (vec && r < rmax && c + 3 < cmax) {
+            f32x4 v = *reinterpret_cast<const f32x4*>(p + r * ld + c);
+            if (msk) v *= *reinterpret_cast<const f32x4*>(msk + r * ld + c);
+            o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = r < rmax && c + q < cmax;
+                o[q] = ok ? p[r * ld + c + q] * (msk ? msk[r * ld + c + q] : 1.f) : 0.f;
+            }
+        }
+    };
+    // A: TA = 0 -> thread q owns row m = q >> 2, k = 4 (q & 3) .. +3; TA = 1 -> row k = q >> 5, m = 4 (q & 31) .. +3
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int e = 0; e < NA; ++e) {
+            const int q = e * 256 + t;
+            if (TA == 0) {
+                const int64_t m = m0 + (q >> 2), k = k0 + (q & 3) * 4;
+                ld4(g.a, nullptr, m, k, g.lda, g.M, ke, VA, ra[e]);
+                if (g.kscale)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) ra[e][c] *= (k + c < ke) ? g.kscale[k + c] : 0.f;
+            } else {
+                const int64_t k = k0 + (q >> 5), m = m0 + (q & 31) * 4;
+                ld4(g.a, nullptr, k, m, g.lda, ke, g.M, VA, ra[e]);
+                if (g.kscale && k < ke)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) ra[e][c] *= g.kscale[k];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < NB; ++e) {
+            const int q = e * 256 + t;
+            if (TB == 1) {  // k contiguous: row n, 4 k's
+                ld4(g.b, g.bmask, n0 + (q >> 2), k0 + (q & 3) * 4, g.ldb, g.N, ke, VB, rb[e]);
+            } else {        // n contiguous: row k, 4 n's
+                ld4(g.b, g.bmask, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, g.ldb, ke, g.N, VB, rb[e]);
+            }
+        }
+    };
+    auto park = [&](int buf) {
+        float* As = sm + buf * (ASZ + BSZ);
+        float* Bs = As + ASZ;
+#pragma unroll
+        for (int e = 0; e < NA; ++e) {
+            const int q = e * 256 + t;
+            if (TA == 0) {  // k = 4 (q & 3) + c -> (h = c & 1, s = 2 (q & 3) + (c >> 1))
+                const int m = q >> 2, s0 = 2 * (q & 3);
+                *reinterpret_cast<f32x2*>(As + (0 * kG2M + m) * kG2RS + s0) = f32x2{ra[e][0], ra[e][2]};
+                *reinterpret_cast<f32x2*>(As + (1 * kG2M + m) * kG2RS + s0) = f32x2{ra[e][1], ra[e][3]};
+            } else {
+                const int k = q >> 5, m = (q & 31) * 4;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) As[((k & 1) * kG2M + m + c) * kG2RS + (k >> 1)] = ra[e][c];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < NB; ++e) {
+            const int q = e * 256 + t;
+            if (TB == 1) {
+                const int n = q >> 2, s0 = 2 * (q & 3);
+                *reinterpret_cast<f32x2*>(Bs + (0 * BN + n) * kG2RS + s0) = f32x2{rb[e][0], rb[e][2]};
+                *reinterpret_cast<f32x2*>(Bs + (1 * BN + n) * kG2RS + s0) = f32x2{rb[e][1], rb[e][3]};
+            } else {
+                const int k = q / (BN / 4), n = (q % (BN / 4)) * 4;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) Bs[((k & 1) * BN + n + c) * kG2RS + (k >> 1)] = rb[e][c];
+            }
+        }
+    };
+    f32x16 acc[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
+    int buf = 0;
+    if (kb < ke) {
+        load(kb);
+        park(0);
+    }
+    __syncthreads();
+    for (int64_t k0 = kb; k0 < ke; k0 += kG2K) {
+        const bool more = k0 + kG2K < ke;
+        if (more) load(k0 + kG2K);  // in flight during this tile's MFMAs
+        const float* As = sm + buf * (ASZ + BSZ);
+        const float* Bs = As + ASZ;
+#pragma unroll
+        for (int sh = 0; sh < 2; ++sh) {  // k-steps 4 sh .. 4 sh + 3
+            f32x4 fa[2], fb[NJ];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                fa[i] = *reinterpret_cast<const f32x4*>(As + (h * kG2M + wm * 64 + i * 32 + col) * kG2RS + 4 * sh);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                fb[j] = *reinterpret_cast<const f32x4*>(Bs + (h * BN + wn * (BN / 2) + j * 32 + col) * kG2RS + 4 * sh);
+#pragma unroll
+            for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(fa[i][ss], fb[j][ss], acc[i][j]);
+        }
+        if (more) park(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* c = g.c + (int64_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t m = m0 + wm * 64 + i * 32 + crow(r, h), n = n0 + wn * (BN / 2) + j * 32 + col;
+                if (m < g.M && n < g.N) {
+                    float v = acc[i][j][r];
+                    if (g.bias) v += g.bias[n];
+                    if (g.pscale) v = v * g.pscale[n] + g.pshift[n];
+                    if (g.relu) v = trelu(v);
+                    if (g.act) v = g.act[m * g.ldact + n] > 0.f ? v : 0.f;
+                    if (g.nscale) v *= g.nscale[n];
+                    float* p = c + m * g.ldc + n;
+                    if (g.accumulate) v += *p;
+                    *p = v;
+                }
+            }
+}
+
+// Which GEMM: the large-tile kernel where the output has at least one full 128-row tile and 64
+// columns (the conditioner GEMMs over the batch, the weight gradients of H >= 64 layers);
+// $NFX_GEMM_TILE=64 forces the 64 x 64 kernel (tests compare both).
+static int gemm_tile_bn(int64_t M, int64_t N) {
+    static const int force = [] {
+        const char* e = getenv("NFX_GEMM_TILE");
+        return e ? atoi(e) : 0;
+    }();
+    if (force == 64 || M < kG2M || N < 64) return 0;
+    return N >= 128 ? 128 : 64;
+}
+
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <int TA, int TB>
-static void gemm_go(const GemmArgs& g, dim3 grid, hipStream_t s) {
+static void gemm_go(const GemmArgs& g, dim3 grid, int bn, hipStream_t s) {
     const bool va = g.lda % 4 == 0 && aligned16(g.a);
     const bool vb = g.ldb % 4 == 0 && aligned16(g.b) && (!g.bmask || aligned16(g.bmask));
+    if (bn == 128) {
+        if (va && vb) gemm2_kernel<TA, TB, true, true, 128><<<grid, 256, 0, s>>>(g);
+        else if (va) gemm2_kernel<TA, TB, true, false, 128><<<grid, 256, 0, s>>>(g);
+        else if (vb) gemm2_kernel<TA, TB, false, true, 128><<<grid, 256, 0, s>>>(g);
+        else gemm2_kernel<TA, TB, false, false, 128><<<grid, 256, 0, s>>>(g);
+        return;
+    }
+    if (bn == 64) {
+        if (va && vb) gemm2_kernel<TA, TB, true, true, 64><<<grid, 256, 0, s>>>(g);
+        else if (va) gemm2_kernel<TA, TB, true, false, 64><<<grid, 256, 0, s>>>(g);
+        else if (vb) gemm2_kernel<TA, TB, false, true, 64><<<grid, 256, 0, s>>>(g);
+        else gemm2_kernel<TA, TB, false, false, 64><<<grid, 256, 0, s>>>(g);
+        return;
+    }
     if (va && vb) gemm_kernel<TA, TB, true, true><<<grid, 256, 0, s>>>(g);
     else if (va) gemm_kernel<TA, TB, true, false><<<grid, 256, 0, s>>>(g);
     else if (vb) gemm_kernel<TA, TB, false, true><<<grid, 256, 0, s>>>(g);
@@ -220,14 +403,16 @@ static void gemm_go(const GemmArgs& g, dim3 grid, hipStream_t s) {
 
 static int gemm_launch(const GemmArgs& g, int ta, int tb, int64_t splits, hipStream_t s) {
     // M tiles on x (the batch: up to 2^31 - 1 tiles), N tiles and split-K slices on y / z (< 65536)
-    const int64_t gm = (g.M + kGBM - 1) / kGBM, gn = (g.N + kGBN - 1) / kGBN;
+    const int bn = gemm_tile_bn(g.M, g.N);
+    const int64_t tm = bn ? kG2M : kGBM, tn = bn ? bn : kGBN;
+    const int64_t gm = (g.M + tm - 1) / tm, gn = (g.N + tn - 1) / tn;
     if (gm > 0x7fffffff || gn > 65535 || splits > 65535)
         return set_error(NFX_EUNSUPPORTED, "linear: grid %lld x %lld x %lld out of range", (long long)gm,
                          (long long)gn, (long long)splits);
     dim3 grid((unsigned)gm, (unsigned)gn, (unsigned)splits);
-    if (ta == 0 && tb == 1) gemm_go<0, 1>(g, grid, s);
-    else if (ta == 0 && tb == 0) gemm_go<0, 0>(g, grid, s);
-    else if (ta == 1 && tb == 0) gemm_go<1, 0>(g, grid, s);
+    if (ta == 0 && tb == 1) gemm_go<0, 1>(g, grid, bn, s);
+    else if (ta == 0 && tb == 0) gemm_go<0, 0>(g, grid, bn, s);
+    else if (ta == 1 && tb == 0) gemm_go<1, 0>(g, grid, bn, s);
     else return set_error(NFX_EINVAL, "linear: unsupported layout");
     return check_launch("gemm_kernel");
 }
@@ -265,7 +450,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ d
 }
 
 static int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) {
-    const int64_t tiles = ((M + kGBM - 1) / kGBM) * ((N + kGBN - 1) / kGBN);
+    const int bn = gemm_tile_bn(M, N);
+    const int64_t tm = bn ? kG2M : kGBM, tn = bn ? bn : kGBN;
+    const int64_t tiles = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
     const int64_t want = (4 * (int64_t)num_cus() + tiles - 1) / tiles;
     const int64_t maxs = (K + 1023) / 1024;  // at least 1024 rows per split
     int64_t s = want < maxs ? want : maxs;
