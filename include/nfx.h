@@ -450,6 +450,18 @@ int nfx_made_elem_backward(const float* x, const float* params, const float* gy,
 int nfx_made_elem_seq_backward(const float* x, const float* params, const float* work, const float* lam,
                                const float* gy, const float* gld, float* out, int64_t B, int d, int variant, int mode,
                                void* stream);
+/* Train-mode BatchNorm in the MADE of a sequential direction: each of the reference's d calls
+ * normalises with the batch statistics of its own partial vector, so the backward runs call by
+ * call. nfx_made_elem_seq_step_backward: step i's adjoint from lam [B][d] (column i final):
+ * grad_params [B][2d] = call i's (dL/dmu_i, dL/dalpha_i) in row i and zeros elsewhere, grad_in
+ * column i = dL/dx_i; params = call i's MADE output, work / work_ld = the forward's raw vector and
+ * running log-det (the clamp decision). nfx_made_elem_prefix: out = work with columns >= i zeroed
+ * (call i's conditioner input). */
+int nfx_made_elem_seq_step_backward(const float* x, const float* params, const float* work, const float* work_ld,
+                                    const float* lam, const float* grad_out, const float* grad_log_det,
+                                    float* grad_params, float* grad_in, int64_t B, int d, int i, int variant,
+                                    void* stream);
+int nfx_made_elem_prefix(const float* work, float* out, int64_t B, int d, int i, void* stream);
 /* CouplingLayer element math for any (d, H) (coupling_layer.py:40-96): s_raw, b_raw [B][d] are
  * the raw s_net / b_net outputs; forward (+1) or inverse (-1) affine map with the clamps, guards
  * and log-det; the backward gives dL/ds_raw, dL/db_raw and the direct dL/dx term. */

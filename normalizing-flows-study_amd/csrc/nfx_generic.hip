@@ -812,6 +812,50 @@ __global__ __launch_bounds__(256) void made_elem_seq_bwd_kernel(const float* __r
     }
 }
 
+// Train-mode BatchNorm in a sequential direction (use_batch_norm=True, the MADE in train mode):
+// every one of the reference's d calls normalises with the batch statistics of ITS partial vector,
+// so step i's params are row i of call i's MADE output (no single-evaluation shortcut). The
+// reverse sweep then differentiates call by call; one step's adjoint from lam (the total dL/dw,
+// column i final once every later call has passed its input VJP back):
+//   dL/dparams of call i = (dmu_i, dalpha_i) in row i, zeros elsewhere; dL/dx_i = lam_i e_i (+ the
+//   IAF output guard's share). The log-det clamp decision uses the forward's running sum ldw.
+__global__ __launch_bounds__(256) void made_elem_seq_step_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ prm, const float* __restrict__ w,
+    const float* __restrict__ ldw, const float* __restrict__ lam, const float* __restrict__ gy,
+    const float* __restrict__ gld, float* __restrict__ dprm, float* __restrict__ gx, int64_t B, int d, int i,
+    int variant) {
+#pragma clang fp contract(off)
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    const bool maf = variant == NFX_MAF_FORWARD;
+    const float lo = maf ? -3.f : -2.f, hi = maf ? 3.f : 2.f, lim = maf ? 100.f : 50.f;
+    const float ldr = ldw[s];
+    const float gl = (nonfinite(ldr) || !(ldr >= -lim && ldr <= lim)) ? 0.f : (gld ? gld[s] : 0.f);
+    const float m = prm[s * 2 * d + i], alpha = prm[s * 2 * d + d + i], xv = x[s * d + i], l = lam[s * d + i];
+    const float a = tclamp(alpha, lo, hi);
+    const bool ain = alpha >= lo && alpha <= hi;
+    const float e = maf ? exp_fast(tclamp(a, -5.f, 5.f)) : exp_fast(tclamp(-a, -3.f, 3.f));
+    for (int j = 0; j < 2 * d; ++j) dprm[s * 2 * d + j] = 0.f;
+    if (maf) {
+        dprm[s * 2 * d + i] = l;
+        dprm[s * 2 * d + d + i] = ain ? l * xv * e + gl : 0.f;
+    } else {
+        const float xm = xv - tclamp(m, -10.f, 10.f);
+        dprm[s * 2 * d + i] = (m >= -10.f && m <= 10.f) ? -(l * e) : 0.f;
+        dprm[s * 2 * d + d + i] = ain ? -(l * xm * e) - gl : 0.f;
+    }
+    const float gd = (!maf && gy && nonfinite(w[s * d + i])) ? gy[s * d + i] : 0.f;  // IAF guard: y = x
+    gx[s * d + i] = l * e + gd;
+}
+
+// out[:, j] = j < i ? w[:, j] : 0 — call i's conditioner input rebuilt from the finished vector
+// (every column is written once, by its own step).
+__global__ __launch_bounds__(256) void made_elem_prefix_kernel(const float* __restrict__ w, float* __restrict__ out,
+                                                               int64_t B, int d, int i) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < B * d; e += (int64_t)gridDim.x * blockDim.x)
+        out[e] = (int)(e % d) < i ? w[e] : 0.f;
+}
+
 // ---- affine coupling element math (coupling_layer.py:40-96) ---------------------------------
 // s, b = clamp(raw, -10, 10); y = x m + (1 - m)(x exp(s) + b)  (forward) or
 // x m + (1 - m)((x - b) exp(-s)) (inverse); ld = sum_j (1 - m) (+-s); guards: y, ld non-finite -> 0.
@@ -1265,6 +1309,35 @@ extern "C" int nfx_made_elem_forward(const float* x, const float* params, float*
     made_elem_fwd_kernel<<<wave_grid(B), 256, 0, (hipStream_t)stream>>>(x, params, y, log_det, B, d,
                                                                                       variant, accumulate);
     return check_launch("made_elem_fwd_kernel");
+}
+
+extern "C" int nfx_made_elem_seq_step_backward(const float* x, const float* params, const float* work,
+                                               const float* work_ld, const float* lam, const float* grad_out,
+                                               const float* grad_log_det, float* grad_params, float* grad_in,
+                                               int64_t B, int d, int i, int variant, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_seq_step_backward");
+    if (rc) return rc;
+    if (variant != NFX_MAF_FORWARD && variant != NFX_IAF_INVERSE)
+        return set_error(NFX_EINVAL, "made_elem_seq_step_backward: sequential variants only (MAF forward / IAF inverse)");
+    if (i < 0 || i >= d) return set_error(NFX_EINVAL, "made_elem_seq_step_backward: step %d outside 0..%d", i, d - 1);
+    if (B == 0) return NFX_OK;
+    if (!x || !params || !work || !work_ld || !lam || !grad_params || !grad_in)
+        return set_error(NFX_EINVAL, "made_elem_seq_step_backward: null pointer");
+    made_elem_seq_step_bwd_kernel<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        x, params, work, work_ld, lam, grad_out, grad_log_det, grad_params, grad_in, B, d, i, variant);
+    return check_launch("made_elem_seq_step_bwd_kernel");
+}
+
+extern "C" int nfx_made_elem_prefix(const float* work, float* out, int64_t B, int d, int i, void* stream) {
+    int rc = made_elem_check(B, d, "made_elem_prefix");
+    if (rc) return rc;
+    if (i < 0 || i > d) return set_error(NFX_EINVAL, "made_elem_prefix: column count %d outside 0..%d", i, d);
+    if (B == 0) return NFX_OK;
+    if (!work || !out) return set_error(NFX_EINVAL, "made_elem_prefix: null pointer");
+    const int64_t n = B * d;
+    made_elem_prefix_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0,
+                              (hipStream_t)stream>>>(work, out, B, d, i);
+    return check_launch("made_elem_prefix_kernel");
 }
 
 extern "C" int nfx_made_elem_step(const float* x, const float* params, float* work, float* work_ld, int64_t B, int d,

@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = (
     "nfx_linear_forward", "nfx_linear_backward_data", "nfx_linear_workspace_bytes", "nfx_linear_backward_weight",
     "nfx_spline_elem_forward", "nfx_spline_elem_backward",
     "nfx_made_elem_forward", "nfx_made_elem_step", "nfx_made_elem_finish", "nfx_made_elem_backward",
-    "nfx_made_elem_seq_backward",
+    "nfx_made_elem_seq_backward", "nfx_made_elem_seq_step_backward", "nfx_made_elem_prefix",
     "nfx_affine_elem_forward", "nfx_affine_elem_backward", "nfx_bn_prepare", "nfx_bn_apply_relu",
     "nfx_bn_workspace_bytes", "nfx_bn_backward_sums", "nfx_bn_backward_apply", "nfx_arqs_step",
 )
@@ -107,6 +107,9 @@ _SIGNATURES = {
     "nfx_made_elem_finish": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_made_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp]),
     "nfx_made_elem_seq_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
+    "nfx_made_elem_seq_step_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int,
+                                               _vp]),
+    "nfx_made_elem_prefix": (_int, [_vp, _vp, _i64, _int, _int, _vp]),
     "nfx_affine_elem_forward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_affine_elem_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _vp]),
     "nfx_bn_prepare": (_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _int, _int, _vp, _vp, _vp,

@@ -189,24 +189,127 @@ class _MadeAffineFlow(HipFlow):
     def _parallel(self, direction):
         return self._variant(direction) in (_lib.NFX_MAF_INVERSE, _lib.NFX_IAF_FORWARD)
 
-    # -- train-mode BatchNorm in the MADE (use_batch_norm=True), parallel directions ----------------
-    def _bn_train_ok(self, x, direction):
+    # -- train-mode BatchNorm in the MADE (use_batch_norm=True) ---------------------------------------
+    def _bn_train_any(self, x):
         bns = self.conditioner.batchnorms()
         if not bns or not all(bn.training for bn in bns) or x.device.type != "cuda" or x.dtype != torch.float32:
             return False
         if any(not bn.affine or not bn.track_running_stats or bn.momentum is None or bn.running_mean is None
                or bn.num_features > _generic_bn_max() for bn in bns):
             return False
-        return x.dim() == 2 and x.shape[1] == self.dim and x.shape[0] >= 2 and self._parallel(direction)
+        return x.dim() == 2 and x.shape[1] == self.dim and x.shape[0] >= 2
+
+    def _bn_train_ok(self, x, direction):
+        """Parallel direction: one MADE call with batch statistics."""
+        return self._bn_train_any(x) and self._parallel(direction)
+
+    def _bn_train_seq_ok(self, x, direction):
+        """Sequential direction: the reference's d MADE calls, each with its own batch statistics."""
+        return self._bn_train_any(x) and not self._parallel(direction)
 
     def _dispatch(self, x, direction):
+        grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
         if self._bn_train_ok(x, direction):
             STATS["hip"] += 1
-            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            if grad:
                 return _MadeTrainFunction.apply(self, direction, x, *list(self.parameters()))
             y, ld, _, _ = self._generic_train_forward(x, direction)
             return y, ld
+        if self._bn_train_seq_ok(x, direction):
+            STATS["hip"] += 1
+            if grad:
+                return _MadeSeqTrainFunction.apply(self, direction, x, *list(self.parameters()))
+            return self._generic_seq_train_forward(x, direction)[:2]
         return super()._dispatch(x, direction)
+
+    def _generic_made_bn_train(self, h):
+        """One train-mode MADE call on h: batch moments per BatchNorm (nfx_flowbn_moments,
+        SyncBN-merged), running update + normalisation (nfx_bn_prepare), ReLU; returns (params,
+        bnp, counts)."""
+        L = _lib.lib()
+        B = h.shape[0]
+        dev = h.device
+        st = _lib.stream_of(h)
+        p = _lib.ptr
+        masks, _ = self._packed(dev, self._generic_pack, slot="_nfx_generic_pack_cache")
+        lins = self.conditioner.linears()
+        bns = self.conditioner.batchnorms()
+        bnp, counts = [], []
+        for i, bn in enumerate(bns):
+            z = _generic.linear_forward(h, lins[i], wmask=masks[i])
+            H = z.shape[1]
+            ws = torch.empty(max(1, L.nfx_flowbn_workspace_bytes(B, H)), device=dev, dtype=torch.uint8)
+            stats = torch.empty(H, 3, device=dev, dtype=torch.float64)
+            _lib.check(L.nfx_flowbn_moments(p(z), B, H, p(stats), p(ws), st), "nfx_flowbn_moments")
+            _dist.merge_bn_stats(stats)
+            t = torch.empty(4, H, device=dev, dtype=torch.float32)
+            _lib.check(L.nfx_bn_prepare(p(stats), p(bn.weight.detach()), p(bn.bias.detach()), p(bn.running_mean),
+                                        p(bn.running_var), float(bn.eps), float(bn.momentum), 1, H, p(t[0]), p(t[1]),
+                                        p(t[2]), p(t[3]), st), "nfx_bn_prepare")
+            torch.autograd.graph.increment_version(bn.running_mean)
+            torch.autograd.graph.increment_version(bn.running_var)
+            h = _generic.bn_apply_relu(z, t)
+            bnp.append(t)
+            counts.append(stats)  # stats[0, 0] = the global sample count
+        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
+        return _generic.linear_forward(h, lins[3], wmask=masks[3]), bnp, counts
+
+    def _generic_seq_train_forward(self, x, direction):
+        """A sequential direction with train-mode BatchNorm, as the reference runs it: d MADE calls
+        on the partial vector, each normalising with its own batch statistics and updating the
+        running statistics (so d updates per forward), one element step each; then the guards.
+        Returns (y, ld, work, wld, bnps, counts)."""
+        L = _lib.lib()
+        x = x.detach().contiguous()
+        B, d = x.shape
+        variant = self._variant(direction)
+        st = _lib.stream_of(x)
+        p = _lib.ptr
+        work = torch.zeros_like(x)
+        wld = torch.zeros(B, device=x.device, dtype=torch.float32)
+        bnps, counts = [], []
+        for i in range(d):
+            prm, bnp, cnt = self._generic_made_bn_train(work)
+            _lib.check(L.nfx_made_elem_step(p(x), p(prm), p(work), p(wld), B, d, i, variant, st), "nfx_made_elem_step")
+            bnps.append(bnp)
+            counts.append(cnt)
+        y = torch.empty_like(x)
+        ld = torch.empty(B, device=x.device, dtype=torch.float32)
+        _lib.check(L.nfx_made_elem_finish(p(x), p(work), p(wld), p(y), p(ld), B, d, variant, 0, st),
+                   "nfx_made_elem_finish")
+        return y, ld, work, wld, bnps, counts
+
+    def _generic_seq_train_backward(self, x, gy, gld, direction, work, wld, bnps, counts):
+        """Autograd through the d train-mode calls, in reverse: lam = the total dL/dwork (the output
+        guard's share of gy, then every later call's input VJP); for call i the conditioner input
+        is work with columns >= i zeroed, its MADE is recomputed with its own batch statistics, the
+        step adjoint gives (dmu_i, dalpha_i) and dL/dx_i, and the batch-statistics MADE backward
+        adds the call's parameter gradients and its input VJP into lam (columns >= i get exact
+        zeros through the masks)."""
+        L = _lib.lib()
+        B, d = x.shape
+        variant = self._variant(direction)
+        st = _lib.stream_of(x)
+        p = _lib.ptr
+        lam = torch.empty_like(x)
+        _lib.check(L.nfx_made_elem_seq_backward(p(x), None, p(work), None, p(gy), p(gld), p(lam), B, d, variant, 0, st),
+                   "nfx_made_elem_seq_backward")
+        gx = torch.empty_like(x)
+        wi = torch.empty_like(x)
+        lins = self.conditioner.linears()
+        bns = self.conditioner.batchnorms()
+        acc = None
+        for i in range(d - 1, -1, -1):
+            _lib.check(L.nfx_made_elem_prefix(p(work), p(wi), B, d, i, st), "nfx_made_elem_prefix")
+            masks, bnp, acts, prm = self._generic_made_bn(wi, bnps[i])
+            dprm = torch.empty_like(prm)
+            _lib.check(L.nfx_made_elem_seq_step_backward(p(x), p(prm), p(work), p(wld), p(lam), p(gy), p(gld),
+                                                         p(dprm), p(gx), B, d, i, variant, st),
+                       "nfx_made_elem_seq_step_backward")
+            grads = _generic.made_bn_backward(wi, lins, masks, bns, bnp, acts, dprm, lam if i > 0 else None, True,
+                                              counts[i], _dist.allreduce_bn_sums)
+            acc = grads if acc is None else [a + g if g is not None else a for a, g in zip(acc, grads)]
+        return gx, acc
 
     def _generic_train_forward(self, x, direction):
         """Batch moments per MADE BatchNorm (nfx_flowbn_moments, SyncBN-merged), normalisation and
@@ -490,6 +593,30 @@ class _MadeTrainFunction(torch.autograd.Function):
         gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
         gld = torch.zeros(x.shape[0], device=x.device) if gld is None else gld.contiguous().float()
         gx, grads = ctx.layer._generic_bn_backward(x, gy, gld, ctx.direction, ctx.bnp, ctx.counts)
+        STATS["hip"] += 1
+        params = list(ctx.layer.parameters())
+        return (None, None, gx, *[g if p.requires_grad else None for p, g in zip(params, grads)])
+
+
+class _MadeSeqTrainFunction(torch.autograd.Function):
+    """MAF.forward / IAF.inverse with train-mode BatchNorm in the MADE: the reference's d calls,
+    each with its own batch statistics and running update; backward call by call
+    (_generic_seq_train_backward)."""
+
+    @staticmethod
+    def forward(ctx, layer, direction, x, *params):
+        y, ld, work, wld, bnps, counts = layer._generic_seq_train_forward(x, direction)
+        ctx.layer, ctx.direction, ctx.bnps, ctx.counts = layer, direction, bnps, counts
+        ctx.save_for_backward(x, work, wld)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, gy, gld):
+        x, work, wld = ctx.saved_tensors
+        x = x.detach().contiguous()
+        gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
+        gld = torch.zeros(x.shape[0], device=x.device) if gld is None else gld.contiguous().float()
+        gx, grads = ctx.layer._generic_seq_train_backward(x, gy, gld, ctx.direction, work, wld, ctx.bnps, ctx.counts)
         STATS["hip"] += 1
         params = list(ctx.layer.parameters())
         return (None, None, gx, *[g if p.requires_grad else None for p, g in zip(params, grads)])

@@ -225,8 +225,16 @@ def made(sd, p, x):
     return h
 
 
-def maf(sd, p, x, direction):
+def _net(batch_norm, training):
+    """The MADE conditioner: made (use_batch_norm=False) or made_bn (eval / train mode)."""
+    if not batch_norm:
+        return made
+    return lambda sd, p, x: made_bn(sd, p, x, training)
+
+
+def maf(sd, p, x, direction, batch_norm=False, training=False):
     d = x.shape[1]
+    made = _net(batch_norm, training)  # noqa: F823 - the conditioner of this layer
     if direction < 0:                                                              # :18-44
         mu, alpha = made(sd, p + "conditioner.", x).chunk(2, dim=1)
         alpha = torch.clamp(alpha, min=-3, max=3)
@@ -248,8 +256,9 @@ def maf(sd, p, x, direction):
     return z, torch.clamp(ld, min=-100, max=100)
 
 
-def iaf(sd, p, x, direction):
+def iaf(sd, p, x, direction, batch_norm=False, training=False):
     d = x.shape[1]
+    made = _net(batch_norm, training)  # noqa: F823 - the conditioner of this layer
     if direction > 0:                                                              # :30-63
         mu, alpha = made(sd, p + "conditioner.", x).chunk(2, dim=1)
         alpha = torch.clamp(alpha, min=-2, max=2)
@@ -275,8 +284,10 @@ def iaf(sd, p, x, direction):
 # ---------------------------------------------------------------------------------------------
 # ARQS — src/flows/spline/arqs.py:7-114 (MADE(d, H, 3K-1) conditioner + unit RQS, sequential)
 # ---------------------------------------------------------------------------------------------
-def made_bn(sd, p, x):
-    """MADE with use_batch_norm=True in eval: MaskedLinear -> BatchNorm1d -> ReLU (made.py:87-114)."""
+def made_bn(sd, p, x, training=False):
+    """MADE with use_batch_norm=True: MaskedLinear -> BatchNorm1d -> ReLU (made.py:87-114). Eval:
+    running statistics; training=True: batch statistics, and the running statistics in `sd`
+    updated in place (momentum 0.1, unbiased variance), once per call as nn.BatchNorm1d does."""
     h = x
     idx = 0
     for i in range(4):
@@ -286,16 +297,16 @@ def made_bn(sd, p, x):
         if i < 3:
             b = f"{p}net.{idx}."
             h = F.batch_norm(h, sd[b + "running_mean"], sd[b + "running_var"], sd[b + "weight"],
-                             sd[b + "bias"], False, 0.0, 1e-5)
+                             sd[b + "bias"], training, 0.1, 1e-5)
             h = F.relu(h)
             idx += 2
     return h
 
 
-def arqs(sd, p, x, direction, K=8, data_min=None, data_max=None, batch_norm=False):
+def arqs(sd, p, x, direction, K=8, data_min=None, data_max=None, batch_norm=False, training=False):
     B, d = x.shape
     R = 3 * K - 1
-    net = made_bn if batch_norm else made
+    net = _net(batch_norm, training)
     rescale = data_min is not None and data_max is not None
     xr = (x - data_min) / (data_max - data_min) if rescale else x                   # :28-34
     state = torch.zeros_like(xr)                                                    # :49 / :87

@@ -36,6 +36,9 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
   g16_fig_models.npz  the other benchmark-figure models (plots/_common.py:157-169): RealNVPSpline(2,8,64),
                       6x MAF(2,64), 6x IAF(2,64): first train step (z, ld, loss, gradients) and 3 Adam +
                       clip steps (losses, final state) on 2,000 two-moons points
+  g17_options.npz     the remaining constructor options under autograd: train-mode use_batch_norm=True
+                      in IAF density (2-layer model step) and MAF sampling, ARQS with BatchNorm in train
+                      mode (both directions), SplineCouplingLayer with per-dimension data_min/data_max
   g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes (+ cfg5: IAF(784,64)
                       inverse NLL at B=8192 and forward checksums at B=524288)
 
@@ -629,6 +632,79 @@ def g16(flows, models):
     np.savez_compressed(os.path.join(HERE, "g16_fig_models.npz"), **out)
 
 
+def g17(flows, models):
+    """The reference's remaining constructor options under autograd:
+      iafbn   NormalizingFlowModel of 2x InverseAutoregressiveFlow(5, 32, use_batch_norm=True) in
+              TRAIN mode, density direction (the sequential IAF.inverse: d MADE calls, each with its
+              own batch statistics, inverse_autoregressive_flow.py:65-103, made.py:93-106):
+              z, ld, loss = -mean log_prob, every gradient, running statistics after the step
+      mafbn   MaskedAutoregressiveFlow(5, 32, use_batch_norm=True), TRAIN mode, forward (sampling,
+              sequential, masked_autoregressive_flow.py:46-78) under L = sum(y wy) + sum(ld wl)
+      arqsbn  ARQS(4, 32, num_bins=5, use_batch_norm=True) (arqs.py:7-114), TRAIN mode, both
+              directions under L (each direction on a fresh copy of the initial state)
+      spldm   SplineCouplingLayer(3, 32, mask = 0, num_bins=6, data_min/data_max = per-dimension
+              tensors) (spline_coupling_layer.py:78-91), eval, both directions under L
+    Per case: y, ld, dL/dx, every parameter gradient and (train mode) the running statistics after."""
+    from torch.distributions import MultivariateNormal
+    out = {}
+    g = torch.Generator().manual_seed(170)
+
+    # iafbn: density training step through NormalizingFlowModel
+    torch.manual_seed(1700)
+    m = models.NormalizingFlowModel([flows.InverseAutoregressiveFlow(5, 32, use_batch_norm=True) for _ in range(2)])
+    perturb(m, 0.1, 1701)
+    m.train()
+    out.update(sd_arrays(m, "iafbn.init."))
+    x = torch.randn(256, 5, generator=g)
+    out["iafbn.x"] = x.numpy()
+    z, ld = m.inverse(x)
+    base = MultivariateNormal(torch.zeros(5), torch.eye(5))
+    loss = -(base.log_prob(z) + ld).mean()
+    loss.backward()
+    out.update({"iafbn.z": z.detach().numpy(), "iafbn.ld": ld.detach().numpy(), "iafbn.loss": np.float64(loss.item())})
+    for k, p in m.named_parameters():
+        out["iafbn.grad." + k] = p.grad.numpy()
+    out.update({k: v for k, v in sd_arrays(m, "iafbn.after.").items() if k.endswith(("running_mean", "running_var"))})
+
+    def layer_case(name, build, dirs, B, scale):
+        torch.manual_seed(1710 + len(out) % 97)
+        f = build()
+        perturb(f, 0.1, 1720 + len(name))
+        init = {k: v.detach().clone() for k, v in f.state_dict().items()}
+        out.update(sd_arrays(f, name + ".init."))
+        d = f.dim if hasattr(f, "dim") else f.data_dim
+        xx = torch.randn(B, d, generator=g) * scale
+        wy = torch.randn(B, d, generator=g)
+        wl = torch.randn(B, generator=g)
+        out.update({f"{name}.x": xx.numpy(), f"{name}.wy": wy.numpy(), f"{name}.wl": wl.numpy()})
+        for dname in dirs:
+            f.load_state_dict(init)
+            f.zero_grad()
+            xr = xx.clone().requires_grad_(True)
+            y, ldd = (f.forward if dname == "fwd" else f.inverse)(xr)
+            ((y * wy).sum() + (ldd * wl).sum()).backward()
+            out[f"{name}.{dname}.y"] = y.detach().numpy()
+            out[f"{name}.{dname}.ld"] = ldd.detach().numpy()
+            out[f"{name}.{dname}.gx"] = xr.grad.numpy()
+            for k, p in f.named_parameters():
+                out[f"{name}.{dname}.grad.{k}"] = p.grad.numpy()
+            out.update({k: v for k, v in sd_arrays(f, f"{name}.{dname}.after.").items()
+                        if k.endswith(("running_mean", "running_var"))})
+
+    layer_case("mafbn", lambda: flows.MaskedAutoregressiveFlow(5, 32, use_batch_norm=True).train(), ("fwd",), 200, 1.0)
+    layer_case("arqsbn", lambda: flows.ARQS(4, 32, num_bins=5, use_batch_norm=True).train(), ("fwd", "inv"), 200, 0.3)
+    dmin, dmax = torch.tensor([-3.0, -2.0, -4.0]), torch.tensor([3.0, 2.5, 1.0])
+    out["spldm.data_min"], out["spldm.data_max"] = dmin.numpy(), dmax.numpy()
+    # (per-dimension bounds only run in the reference when every dim is transformed: with a
+    # conditioning dim, _rescale_from_spline broadcasts the [d] bounds against the [B, n_t] slice and
+    # raises — spline_coupling_layer.py:94,122)
+    layer_case("spldm", lambda: flows.SplineCouplingLayer(3, 32, torch.tensor([0.0, 0.0, 0.0]), num_bins=6,
+                                                          data_min=dmin, data_max=dmax).eval(),
+               ("fwd", "inv"), 300, 1.2)
+    np.savez_compressed(os.path.join(HERE, "g17_options.npz"), **out)
+    print("g17 written", flush=True)
+
+
 def g8_cfg5(f6):
     """cfg5 IAF(784,64) (G6 weights): inverse NLL at B=8192 (seed 1237) and forward checksums at
     B=524288 (seed 1238); merged into g8_full_nll.json."""
@@ -726,6 +802,9 @@ def main():
     if a.only == "g16":
         g16(flows, models)
         return
+    if a.only == "g17":
+        g17(flows, models)
+        return
     if a.only == "g8_cfg5":
         g8_cfg5(g6(flows))
         return
@@ -744,6 +823,7 @@ def main():
     g14(flows)
     g15(models)
     g16(flows, models)
+    g17(flows, models)
     if not a.skip_full:
         g8(m2, m3, m5)
         g8_cfg5(f6)

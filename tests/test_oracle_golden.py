@@ -317,3 +317,64 @@ def test_figure_models_g16(name):
         assert np.abs(p.grad.numpy() - ref).max() <= 1e-4 * (1 + np.abs(ref).max()), k
         n += 1
     assert n == 48
+
+
+def _g17_layer_spec(name):
+    if name == "mafbn":
+        return "maf", {"batch_norm": True, "training": True}
+    if name == "arqsbn":
+        return "arqs", {"K": 5, "batch_norm": True, "training": True}
+    return "spline", {"K": 6}
+
+
+@pytest.mark.parametrize("case", ["iafbn", "mafbn.fwd", "arqsbn.fwd", "arqsbn.inv", "spldm.fwd", "spldm.inv"])
+def test_options_g17(case):
+    """G17 (the reference's remaining constructor options under autograd): the oracle reproduces
+    the reference's outputs, gradients and running statistics — train-mode use_batch_norm=True in
+    the sequential MADE directions (d calls, each with its own batch statistics), ARQS with a
+    train-mode BatchNorm MADE, and per-dimension data_min/data_max spline bounds."""
+    g = load_golden("g17_options.npz")
+    if case == "iafbn":
+        sd = oracle_sd(g, "iafbn.init.")
+        params = {k: v.clone().requires_grad_(True) for k, v in sd.items()
+                  if not k.endswith(("mask", "running_mean", "running_var"))}
+        sd.update(params)
+        spec = [("iaf", f"flows.{i}.", {"batch_norm": True, "training": True}) for i in range(2)]
+        x = torch.from_numpy(g["iafbn.x"])
+        z, ld = oracle.flow_model(sd, spec, x, -1)
+        loss = -oracle.gauss_log_prob(z, ld).mean()
+        loss.backward()
+        close(z.detach(), g["iafbn.z"], rtol=2e-5, atol=2e-5)
+        close(ld.detach(), g["iafbn.ld"], rtol=2e-5, atol=2e-5)
+        assert abs(loss.item() - float(g["iafbn.loss"])) <= 1e-5
+        grads = {k: p.grad for k, p in params.items()}
+        gpre, after = "iafbn.grad.", "iafbn.after."
+    else:
+        name, dname = case.split(".")
+        kind, kw = _g17_layer_spec(name)
+        sd = oracle_sd(g, name + ".init.")
+        params = {k: v.clone().requires_grad_(True) for k, v in sd.items()
+                  if not k.endswith(("mask", "running_mean", "running_var"))}
+        sd.update(params)
+        if name == "spldm":
+            kw = dict(kw, data_min=torch.from_numpy(g["spldm.data_min"]), data_max=torch.from_numpy(g["spldm.data_max"]))
+        x = torch.from_numpy(g[name + ".x"]).clone().requires_grad_(True)
+        y, ld = getattr(oracle, {"maf": "maf", "arqs": "arqs", "spline": "spline_coupling"}[kind])(
+            sd, "", x, 1 if dname == "fwd" else -1, **kw)
+        ((y * torch.from_numpy(g[name + ".wy"])).sum() + (ld * torch.from_numpy(g[name + ".wl"])).sum()).backward()
+        close(y.detach(), g[f"{case}.y"], rtol=2e-5, atol=2e-5)
+        close(ld.detach(), g[f"{case}.ld"], rtol=2e-5, atol=2e-5)
+        ref = g[f"{case}.gx"]
+        assert np.abs(x.grad.numpy() - ref).max() <= 1e-4 * (1 + np.abs(ref).max())
+        grads = {k: p.grad for k, p in params.items()}
+        gpre, after = f"{case}.grad.", f"{case}.after."
+    n = 0
+    for k, gr in grads.items():
+        ref = g[gpre + k]
+        assert gr is not None, k
+        assert np.abs(gr.numpy() - ref).max() <= 1e-4 * (1 + np.abs(ref).max()), k
+        n += 1
+    assert n > 0
+    for k in g:  # running statistics after the step(s): updated once per MADE call
+        if k.startswith(after):
+            close(sd[k[len(after):]], g[k], rtol=1e-5, atol=1e-6)
