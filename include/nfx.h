@@ -515,6 +515,21 @@ int nfx_spline_elem_backward(const float* x, const float* params, const float* m
                              const float* gld, float* gparams, float* gx, int64_t B, int d, int K, float bound,
                              float min_bin_width, float min_bin_height, float min_derivative, int direction,
                              void* stream);
+/* The same with data_min / data_max bounds (spline_coupling_layer.py:78-94, scalar or
+ * per-dimension): bounds = device [3][d] = data_min | 2B/(data_max - data_min) |
+ * (data_max - data_min)/(2B) per dimension, rounded as the reference's expressions round them;
+ * x is the raw input (the spline runs on to (x - lo) - B, its outputs map back, and the
+ * backward's dL/dx includes both scales). nfx_spline_rescale writes xr = to (x - lo) - B, the
+ * conditioner's input (times the mask in nfx_linear_forward). */
+int nfx_spline_elem_forward_bounded(const float* x, const float* params, const float* mask, const float* bounds,
+                                    float* y, float* log_det, int64_t B, int d, int K, float bound,
+                                    float min_bin_width, float min_bin_height, float min_derivative, int direction,
+                                    int accumulate, void* stream);
+int nfx_spline_elem_backward_bounded(const float* x, const float* params, const float* mask, const float* bounds,
+                                     const float* gy, const float* gld, float* gparams, float* gx, int64_t B, int d,
+                                     int K, float bound, float min_bin_width, float min_bin_height,
+                                     float min_derivative, int direction, void* stream);
+int nfx_spline_rescale(const float* x, const float* bounds, float* xr, int64_t B, int d, float bound, void* stream);
 
 #ifdef __cplusplus
 }

@@ -540,7 +540,9 @@ __global__ __launch_bounds__(256) void spline_elem_fwd_kernel(const float* __res
                                                               const float* __restrict__ prm,
                                                               const float* __restrict__ mask, float* __restrict__ y,
                                                               float* __restrict__ log_det, int64_t B, int d,
-                                                              int accumulate, const SplineConsts C) {
+                                                              int accumulate, const SplineConsts C,
+                                                              const float* __restrict__ rs) {
+#pragma clang fp contract(off)  // the reference's separate roundings of the rescale
     constexpr int P = 3 * K - 1;
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= B) return;
@@ -555,7 +557,10 @@ __global__ __launch_bounds__(256) void spline_elem_fwd_kernel(const float* __res
 #pragma unroll
             for (int i = 0; i < 32; ++i) p[i] = i < P ? pr[i] : 0.f;
             float lad;
-            rq_spline_elem<K, INV>(v, p, C, o, lad);
+            // rs = [lo | to | from][d]: data_min/data_max bounds (spline_coupling_layer.py:78-94)
+            const float vr = rs ? rs[d + j] * (v - rs[j]) - C.bound : v;
+            rq_spline_elem<K, INV>(vr, p, C, o, lad);
+            if (rs) o = (o + C.bound) * rs[2 * d + j] + rs[j];
             ld = first ? lad : ld + lad;
             first = false;
         }
@@ -576,7 +581,9 @@ __global__ __launch_bounds__(256) void spline_elem_bwd_kernel(const float* __res
                                                               const float* __restrict__ gy,
                                                               const float* __restrict__ gld,
                                                               float* __restrict__ gprm, float* __restrict__ gx,
-                                                              int64_t B, int d, const SplineConsts C) {
+                                                              int64_t B, int d, const SplineConsts C,
+                                                              const float* __restrict__ rs) {
+#pragma clang fp contract(off)
     constexpr int P = 3 * K - 1;
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
     const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + col;
@@ -593,8 +600,16 @@ __global__ __launch_bounds__(256) void spline_elem_bwd_kernel(const float* __res
 #pragma unroll
             for (int i = 0; i < 32; ++i) p[i] = i < P ? pr[i] : 0.f;
             float o, gs[K], gd[K / 2], gv;
-            // the layer guard zeroes a non-finite output, which only a non-finite input gives
-            rq_spline_adjoint<K, INV>(v, p, C, nonfinite(v) ? 0.f : g, gl, o, gs, gd, gv);
+            // the layer guard zeroes a non-finite output, which only a non-finite input gives;
+            // with bounds y = (S(vr) + B) from + lo, vr = to (v - lo) - B: dL/dS = g from, dv = dvr to
+            const float gg = nonfinite(v) ? 0.f : g;
+            if (rs) {
+                const float vr = rs[d + j] * (v - rs[j]) - C.bound;
+                rq_spline_adjoint<K, INV>(vr, p, C, gg * rs[2 * d + j], gl, o, gs, gd, gv);
+                gv = gv * rs[d + j];
+            } else {
+                rq_spline_adjoint<K, INV>(v, p, C, gg, gl, o, gs, gd, gv);
+            }
             if (ok) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) gp[h * K + k] = gs[k];
@@ -1248,42 +1263,102 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
     return check_launch("split_reduce_kernel");
 }
 
-extern "C" int nfx_spline_elem_forward(const float* x, const float* params, const float* mask, float* y,
-                                       float* log_det, int64_t B, int d, int K, float bound, float min_bin_width,
-                                       float min_bin_height, float min_derivative, int direction, int accumulate,
-                                       void* stream) {
+// bounds (optional): device [3][d] = data_min | 2B/(data_max - data_min) | (data_max - data_min)/(2B)
+// per dimension, rounded as the reference's expressions round them (the caller computes them).
+static int spline_elem_fwd_launch(const float* x, const float* params, const float* mask, const float* bounds, float* y,
+                                  float* log_det, int64_t B, int d, int K, float bound, float min_bin_width,
+                                  float min_bin_height, float min_derivative, int direction, int accumulate,
+                                  hipStream_t stream) {
     if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "spline_elem_forward: bad shape B=%lld d=%d", (long long)B, d);
     if (K < 2 || K > 11) return set_error(NFX_EUNSUPPORTED, "spline_elem_forward: K=%d outside 2..11", K);
     if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "spline_elem_forward: direction");
     if (B == 0) return NFX_OK;
     if (!x || !params || !mask || !y || !log_det) return set_error(NFX_EINVAL, "spline_elem_forward: null pointer");
     if (x == y) return set_error(NFX_EINVAL, "spline_elem_forward: x and y must not alias");
-    typedef void (*fk)(const float*, const float*, const float*, float*, float*, int64_t, int, int, const SplineConsts);
+    typedef void (*fk)(const float*, const float*, const float*, float*, float*, int64_t, int, int, const SplineConsts,
+                       const float*);
     fk k = (fk)spline_elem_pick<false>(K, direction < 0);
     const SplineConsts C = spline_consts(K, bound, min_bin_width, min_bin_height, min_derivative);
     const int64_t blocks = (B + 255) / 256;
     if (blocks > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "spline_elem_forward: B too large");
-    k<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, params, mask, y, log_det, B, d, accumulate, C);
+    k<<<(unsigned)blocks, 256, 0, stream>>>(x, params, mask, y, log_det, B, d, accumulate, C, bounds);
     return check_launch("spline_elem_fwd_kernel");
 }
 
-extern "C" int nfx_spline_elem_backward(const float* x, const float* params, const float* mask, const float* gy,
-                                        const float* gld, float* gparams, float* gx, int64_t B, int d, int K,
-                                        float bound, float min_bin_width, float min_bin_height, float min_derivative,
-                                        int direction, void* stream) {
+static int spline_elem_bwd_launch(const float* x, const float* params, const float* mask, const float* bounds,
+                                  const float* gy, const float* gld, float* gparams, float* gx, int64_t B, int d, int K,
+                                  float bound, float min_bin_width, float min_bin_height, float min_derivative,
+                                  int direction, hipStream_t stream) {
     if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "spline_elem_backward: bad shape B=%lld d=%d", (long long)B, d);
     if (K < 2 || K > 11) return set_error(NFX_EUNSUPPORTED, "spline_elem_backward: K=%d outside 2..11", K);
     if (direction != NFX_FORWARD && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "spline_elem_backward: direction");
     if (B == 0) return NFX_OK;
     if (!x || !params || !mask || !gparams || !gx) return set_error(NFX_EINVAL, "spline_elem_backward: null pointer");
     typedef void (*bk)(const float*, const float*, const float*, const float*, const float*, float*, float*, int64_t,
-                       int, const SplineConsts);
+                       int, const SplineConsts, const float*);
     bk k = (bk)spline_elem_pick<true>(K, direction < 0);
     const SplineConsts C = spline_consts(K, bound, min_bin_width, min_bin_height, min_derivative);
     const int64_t blocks = (B + 127) / 128;
     if (blocks > 0x7fffffff) return set_error(NFX_EUNSUPPORTED, "spline_elem_backward: B too large");
-    k<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, params, mask, gy, gld, gparams, gx, B, d, C);
+    k<<<(unsigned)blocks, 256, 0, stream>>>(x, params, mask, gy, gld, gparams, gx, B, d, C, bounds);
     return check_launch("spline_elem_bwd_kernel");
+}
+
+extern "C" int nfx_spline_elem_forward(const float* x, const float* params, const float* mask, float* y,
+                                       float* log_det, int64_t B, int d, int K, float bound, float min_bin_width,
+                                       float min_bin_height, float min_derivative, int direction, int accumulate,
+                                       void* stream) {
+    return spline_elem_fwd_launch(x, params, mask, nullptr, y, log_det, B, d, K, bound, min_bin_width, min_bin_height,
+                                  min_derivative, direction, accumulate, (hipStream_t)stream);
+}
+
+extern "C" int nfx_spline_elem_forward_bounded(const float* x, const float* params, const float* mask,
+                                               const float* bounds, float* y, float* log_det, int64_t B, int d, int K,
+                                               float bound, float min_bin_width, float min_bin_height,
+                                               float min_derivative, int direction, int accumulate, void* stream) {
+    if (!bounds) return set_error(NFX_EINVAL, "spline_elem_forward_bounded: null bounds");
+    return spline_elem_fwd_launch(x, params, mask, bounds, y, log_det, B, d, K, bound, min_bin_width, min_bin_height,
+                                  min_derivative, direction, accumulate, (hipStream_t)stream);
+}
+
+extern "C" int nfx_spline_elem_backward(const float* x, const float* params, const float* mask, const float* gy,
+                                        const float* gld, float* gparams, float* gx, int64_t B, int d, int K,
+                                        float bound, float min_bin_width, float min_bin_height, float min_derivative,
+                                        int direction, void* stream) {
+    return spline_elem_bwd_launch(x, params, mask, nullptr, gy, gld, gparams, gx, B, d, K, bound, min_bin_width,
+                                  min_bin_height, min_derivative, direction, (hipStream_t)stream);
+}
+
+extern "C" int nfx_spline_elem_backward_bounded(const float* x, const float* params, const float* mask,
+                                                const float* bounds, const float* gy, const float* gld, float* gparams,
+                                                float* gx, int64_t B, int d, int K, float bound, float min_bin_width,
+                                                float min_bin_height, float min_derivative, int direction,
+                                                void* stream) {
+    if (!bounds) return set_error(NFX_EINVAL, "spline_elem_backward_bounded: null bounds");
+    return spline_elem_bwd_launch(x, params, mask, bounds, gy, gld, gparams, gx, B, d, K, bound, min_bin_width,
+                                  min_bin_height, min_derivative, direction, (hipStream_t)stream);
+}
+
+// xr = to (x - lo) - bound per element (spline_coupling_layer.py:78-85, fp32 ops in order):
+// the conditioner input of a layer with data_min / data_max bounds (times the mask in the GEMM).
+__global__ __launch_bounds__(256) void spline_rescale_kernel(const float* __restrict__ x, const float* __restrict__ rs,
+                                                             float* __restrict__ xr, int64_t B, int d, float bound) {
+#pragma clang fp contract(off)
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < B * d; e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e % d);
+        xr[e] = rs[d + j] * (x[e] - rs[j]) - bound;
+    }
+}
+
+extern "C" int nfx_spline_rescale(const float* x, const float* bounds, float* xr, int64_t B, int d, float bound,
+                                  void* stream) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "spline_rescale: bad shape B=%lld d=%d", (long long)B, d);
+    if (B == 0) return NFX_OK;
+    if (!x || !bounds || !xr) return set_error(NFX_EINVAL, "spline_rescale: null pointer");
+    const int64_t n = B * d;
+    spline_rescale_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0, (hipStream_t)stream>>>(
+        x, bounds, xr, B, d, bound);
+    return check_launch("spline_rescale_kernel");
 }
 
 // Blocks of 4 waves for the wave-per-sample element kernels (grid-stride beyond 16 Ki waves).

@@ -61,16 +61,16 @@ def mlp3_forward(x, l1, l2, l3, in_scale):
     return h1, h2, linear_forward(h2, l3)
 
 
-def mlp3_backward(x, l1, l2, l3, in_scale, h1, h2, g3, gx):
+def mlp3_backward(x, l1, l2, l3, in_scale, h1, h2, g3, gx, out_scale=None):
     """Backward of mlp3_forward given dL/dout = g3: parameter gradients in parameters() order
-    (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias); dL/dx (times in_scale) is
-    added into gx."""
+    (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias); dL/dx (times out_scale, default
+    in_scale) is added into gx."""
     gw3, gb3 = linear_backward_weight(g3, h2, l3)
     g2 = linear_backward_data(g3, l3, act=h2)
     gw2, gb2 = linear_backward_weight(g2, h1, l2)
     g1 = linear_backward_data(g2, l2, act=h1)
     gw1, gb1 = linear_backward_weight(g1, x, l1, in_scale)
-    linear_backward_data(g1, l1, out_scale=in_scale, out=gx)
+    linear_backward_data(g1, l1, out_scale=in_scale if out_scale is None else out_scale, out=gx)
     return [gw1, gb1, gw2, gb2, gw3, gb3]
 
 

@@ -196,59 +196,113 @@ class SplineCouplingLayer(HipFlow):
         d, H, K = self.data_dim, self._hidden(), self.num_bins
         if x.dim() != 2 or x.shape[1] != d:
             return False, f"input shape {tuple(x.shape)} vs data_dim={d}"
-        if self._fused_family():
-            if self._rescale_scalars() is None:
-                return False, "per-dimension data_min/data_max tensors"
-            return True, ""
-        if self._generic_ok():
+        if self._fused_family() or self._generic_ok():
             return True, ""
         return False, (f"d={d} H={H} K={K}: fused kernels need d <= {MAX_D}, H <= {MAX_H}, K <= {MAX_K}; "
-                       f"the any-shape path needs 2 <= K <= {MAX_K} and data_min/data_max None")
+                       f"the any-shape path needs 2 <= K <= {MAX_K} and scalar or [d] data_min/data_max")
 
     def _fused_family(self):
-        """Shapes of the fused eval kernels (spline_coupling_kernel / spline_wide_kernel)."""
+        """Shapes of the fused eval kernels (spline_coupling_kernel / spline_wide_kernel): scalar
+        bounds only (per-dimension ones take the any-shape path)."""
         return (not FORCE_GENERIC and self.data_dim <= MAX_D and self._hidden() <= MAX_H
-                and 1 <= self.num_bins <= MAX_K)
+                and 1 <= self.num_bins <= MAX_K and self._rescale_scalars() is not None)
 
     def _generic_ok(self):
-        """The any-shape path (csrc/nfx_generic.hip): GEMM conditioner + spline element kernels."""
-        return 2 <= self.num_bins <= MAX_K and (self.data_min is None or self.data_max is None)
+        """The any-shape path (csrc/nfx_generic.hip): GEMM conditioner + spline element kernels,
+        with scalar or per-dimension data_min/data_max bounds (nfx_spline_elem_*_bounded)."""
+        if not 2 <= self.num_bins <= MAX_K:
+            return False
+        if self.data_min is None or self.data_max is None:
+            return True
+        return all((not torch.is_tensor(t)) or t.numel() in (1, self.data_dim) for t in (self.data_min, self.data_max))
+
+    def _bounds(self, device):
+        """[4][d] float32 on the device = data_min | 2B/(max - min) | (max - min)/(2B) | mask * to,
+        the first three evaluated exactly as the reference's _rescale_to_spline /
+        _rescale_from_spline expressions (python floats in double, tensors in their fp32 ops; rows
+        0-2 are nfx_spline_elem_*_bounded's `bounds`, row 3 maps the conditioner's dL/dxr to dL/dx),
+        cached with the parameters and buffers (keyed on the bound objects too); None without
+        bounds."""
+        if self.data_min is None or self.data_max is None:
+            return None
+        key = (id(self.data_min), id(self.data_max), getattr(self.data_min, "_version", 0),
+               getattr(self.data_max, "_version", 0))
+        c = self.__dict__.get("_nfx_bounds_key")
+        if c != key:
+            self.__dict__.pop("_nfx_bounds_pack_cache", None)
+            object.__setattr__(self, "_nfx_bounds_key", key)
+        return self._packed(device, self._build_bounds, slot="_nfx_bounds_pack_cache")
+
+    def _build_bounds(self, device):
+        lo, hi, d = self.data_min, self.data_max, self.data_dim
+        cpu = lambda v: v.detach().cpu() if torch.is_tensor(v) else v  # noqa: E731
+        lo, hi = cpu(lo), cpu(hi)
+        to = (2 * self.bound) / (hi - lo)
+        fr = (hi - lo) / (2 * self.bound)
+        rows = [torch.as_tensor(v, dtype=torch.float32).reshape(-1).expand(d) for v in (lo, to, fr)]
+        rows.append(self.mask.detach().cpu().float() * rows[1])
+        return torch.stack(rows).to(device=device).contiguous()
 
     def _mask_dev(self, device):
         m = self.mask
         return m.detach().to(device=device, dtype=torch.float32).contiguous()
 
-    def _generic_params(self, x):
-        """Conditioner recompute on the any-shape path: (mask, h1, h2, params [B, d(3K-1)])."""
+    def _generic_params(self, x, bounds=None):
+        """Conditioner recompute on the any-shape path: (mask, conditioner input, h1, h2, params
+        [B, d(3K-1)]); with bounds the input is the rescaled x (nfx_spline_rescale)."""
         mask = self._mask_dev(x.device)
-        h1, h2, prm = _generic.mlp3_forward(x, self.param_net[0], self.param_net[2], self.param_net[4], mask)
-        return mask, h1, h2, prm
+        xin = x
+        if bounds is not None:
+            xin = torch.empty_like(x)
+            _lib.check(_lib.lib().nfx_spline_rescale(_lib.ptr(x), _lib.ptr(bounds), _lib.ptr(xin), x.shape[0],
+                                                     self.data_dim, float(self.bound), _lib.stream_of(x)),
+                       "nfx_spline_rescale")
+        h1, h2, prm = _generic.mlp3_forward(xin, self.param_net[0], self.param_net[2], self.param_net[4], mask)
+        return mask, xin, h1, h2, prm
 
     def _spline_scalars(self):
         return (float(self.bound), float(self.min_bin_width), float(self.min_bin_height),
                 float(self.min_derivative))
 
     def _generic_launch(self, x, out, log_det, direction, accumulate):
-        mask, _, _, prm = self._generic_params(x)
-        _lib.check(_lib.lib().nfx_spline_elem_forward(
-            _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(out), _lib.ptr(log_det), x.shape[0],
-            self.data_dim, self.num_bins, *self._spline_scalars(), int(direction), int(bool(accumulate)),
-            _lib.stream_of(x)), "nfx_spline_elem_forward")
+        bounds = self._bounds(x.device)
+        mask, _, _, _, prm = self._generic_params(x, bounds)
+        L = _lib.lib()
+        if bounds is None:
+            _lib.check(L.nfx_spline_elem_forward(
+                _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(out), _lib.ptr(log_det), x.shape[0],
+                self.data_dim, self.num_bins, *self._spline_scalars(), int(direction), int(bool(accumulate)),
+                _lib.stream_of(x)), "nfx_spline_elem_forward")
+        else:
+            _lib.check(L.nfx_spline_elem_forward_bounded(
+                _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(bounds), _lib.ptr(out), _lib.ptr(log_det),
+                x.shape[0], self.data_dim, self.num_bins, *self._spline_scalars(), int(direction),
+                int(bool(accumulate)), _lib.stream_of(x)), "nfx_spline_elem_forward_bounded")
 
     def _generic_backward(self, x, gy, gld, direction):
         """dL/dx and parameter gradients on the any-shape path: conditioner recompute (GEMMs),
         the spline adjoint per element (nfx_spline_elem_backward), then the conditioner's
         backward GEMMs (data gradient into dL/dx, weight gradients split over the batch)."""
         B, d = x.shape
-        mask, h1, h2, prm = self._generic_params(x)
+        bounds = self._bounds(x.device)
+        mask, xin, h1, h2, prm = self._generic_params(x, bounds)
         gprm = torch.empty_like(prm)
         gx = torch.empty_like(x)
-        _lib.check(_lib.lib().nfx_spline_elem_backward(
-            _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(gy), _lib.ptr(gld), _lib.ptr(gprm), _lib.ptr(gx),
-            B, d, self.num_bins, *self._spline_scalars(), int(direction), _lib.stream_of(x)),
-            "nfx_spline_elem_backward")
-        grads = _generic.mlp3_backward(x, self.param_net[0], self.param_net[2], self.param_net[4], mask, h1, h2,
-                                       gprm, gx)
+        L = _lib.lib()
+        if bounds is None:
+            _lib.check(L.nfx_spline_elem_backward(
+                _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(gy), _lib.ptr(gld), _lib.ptr(gprm),
+                _lib.ptr(gx), B, d, self.num_bins, *self._spline_scalars(), int(direction), _lib.stream_of(x)),
+                "nfx_spline_elem_backward")
+            out_scale = None
+        else:
+            _lib.check(L.nfx_spline_elem_backward_bounded(
+                _lib.ptr(x), _lib.ptr(prm), _lib.ptr(mask), _lib.ptr(bounds), _lib.ptr(gy), _lib.ptr(gld),
+                _lib.ptr(gprm), _lib.ptr(gx), B, d, self.num_bins, *self._spline_scalars(), int(direction),
+                _lib.stream_of(x)), "nfx_spline_elem_backward_bounded")
+            out_scale = bounds[3]
+        grads = _generic.mlp3_backward(xin, self.param_net[0], self.param_net[2], self.param_net[4], mask, h1, h2,
+                                       gprm, gx, out_scale=out_scale)
         return gx, grads
 
     def _build_pack(self, device):
@@ -273,7 +327,7 @@ class SplineCouplingLayer(HipFlow):
         nt = self._n_transformed()
         ntmax = 2 if H <= 32 else 1
         return (not FORCE_GENERIC and d <= MAX_D_BWD and H <= MAX_H_BWD and 2 <= K <= MAX_K and nt <= ntmax
-                and (self.data_min is None or self.data_max is None))
+                and (self.data_min is None or self.data_max is None))  # bounds: the any-shape path
 
     def _n_transformed(self):
         """Number of transformed (mask == 0) dimensions, cached per mask version (no sync)."""

@@ -100,3 +100,35 @@ def test_maf_batchnorm_train_sampling_vs_reference(cuda_device):
     for k, v in gpu.state_dict().items():
         if k.endswith(("running_mean", "running_var")):
             np.testing.assert_allclose(v.cpu().numpy(), g["mafbn.fwd.after." + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("dname", ["fwd", "inv"])
+def test_spline_per_dimension_bounds_vs_reference(cuda_device, dname):
+    """spldm: SplineCouplingLayer(3, 32, mask = 0, K = 6) with per-dimension data_min / data_max
+    tensors (spline_coupling_layer.py:78-94; the only mask the reference runs them with, see
+    make_golden.py:g17), eval, both directions under autograd, on the any-shape path with the
+    bounds (nfx_spline_rescale + nfx_spline_elem_*_bounded)."""
+    g = load_golden("g17_options.npz")
+    dmin, dmax = torch.from_numpy(g["spldm.data_min"]), torch.from_numpy(g["spldm.data_max"])
+    f = nfs_amd.SplineCouplingLayer(3, 32, torch.zeros(3), num_bins=6, data_min=dmin, data_max=dmax)
+    f = _load(f, g, "spldm.init.").eval()
+    f64 = copy.deepcopy(f).double()
+    f64.data_min, f64.data_max = dmin.double(), dmax.double()
+    gpu = f.to(cuda_device)
+    gpu.data_min, gpu.data_max = dmin.to(cuda_device), dmax.to(cuda_device)
+    x = torch.from_numpy(g["spldm.x"])
+    wy, wl = torch.from_numpy(g["spldm.wy"]), torch.from_numpy(g["spldm.wl"])
+    nfs_amd.reset_stats()
+    xr = x.to(cuda_device).requires_grad_(True)
+    y, ld = (gpu.forward if dname == "fwd" else gpu.inverse)(xr)
+    ((y * wy.to(cuda_device)).sum() + (ld * wl.to(cuda_device)).sum()).backward()
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 2, nfs_amd.STATS
+    x64 = x.double().requires_grad_(True)
+    y64, ld64 = (f64.forward if dname == "fwd" else f64.inverse)(x64)
+    ((y64 * wy.double()).sum() + (ld64 * wl.double()).sum()).backward()
+    pre = f"spldm.{dname}."
+    _gclose(y, g[pre + "y"], "y", y64, frac=2e-5)
+    _gclose(ld, g[pre + "ld"], "ld", ld64, frac=2e-5)
+    _gclose(xr.grad, g[pre + "gx"], "dL/dx", x64.grad)
+    for (k, p), (_, p64) in zip(gpu.named_parameters(), f64.named_parameters()):
+        _gclose(p.grad, g[pre + "grad." + k], what=k, ref32=p64.grad)
