@@ -500,6 +500,11 @@ int nfx_bn_backward_apply(const float* g, const float* z, const float* mean, con
 int nfx_arqs_step(const float* xr, const float* params, float* state, float* log_det, const float* gld, float* lam,
                   float* gparams, float* gx, int64_t B, int d, int K, int i, int direction, int mode,
                   float min_bin_width, float min_bin_height, float min_derivative, void* stream);
+/* ARQS data_min / data_max bounds on the any-shape path (arqs.py:28-42), element-wise with
+ * bounds = device [2][d] = data_min | data_max - data_min (scalar bounds broadcast), rounded as the
+ * reference's expressions: mode 0 out = (in - lo) / w (to the unit interval), 1 out = in * w + lo
+ * (back), and their adjoints 2 out = in / w, 3 out = in * w. */
+int nfx_arqs_bounds(const float* in, const float* bounds, float* out, int64_t B, int d, int mode, void* stream);
 /* SplineCouplingLayer element math for any d (spline_coupling_layer.py:96-180 with the spline
  * of :182-309): params [B][d][3K-1] = param_net output; dims with mask == 0 go through the RQ
  * spline (forward: direction +1, inverse: -1), the rest pass through; layer guards and the

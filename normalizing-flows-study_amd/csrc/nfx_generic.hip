@@ -1339,6 +1339,31 @@ extern "C" int nfx_spline_elem_backward_bounded(const float* x, const float* par
                                   min_bin_height, min_derivative, direction, (hipStream_t)stream);
 }
 
+// ARQS data_min / data_max bounds (arqs.py:28-42) and their adjoints, per element, fp32 ops as
+// the reference's tensor expressions: bounds = [lo | w][d] with w = data_max - data_min.
+//   mode 0: (x - lo) / w      mode 1: x * w + lo      mode 2: g / w      mode 3: g * w
+__global__ __launch_bounds__(256) void arqs_bounds_kernel(const float* __restrict__ in, const float* __restrict__ bnd,
+                                                          float* __restrict__ out, int64_t B, int d, int mode) {
+#pragma clang fp contract(off)
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < B * d; e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e % d);
+        const float v = in[e], lo = bnd[j], w = bnd[d + j];
+        out[e] = mode == 0 ? (v - lo) / w : mode == 1 ? v * w + lo : mode == 2 ? v / w : v * w;
+    }
+}
+
+extern "C" int nfx_arqs_bounds(const float* in, const float* bounds, float* out, int64_t B, int d, int mode,
+                               void* stream) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "arqs_bounds: bad shape B=%lld d=%d", (long long)B, d);
+    if (mode < 0 || mode > 3) return set_error(NFX_EINVAL, "arqs_bounds: mode %d", mode);
+    if (B == 0) return NFX_OK;
+    if (!in || !bounds || !out) return set_error(NFX_EINVAL, "arqs_bounds: null pointer");
+    const int64_t n = B * d;
+    arqs_bounds_kernel<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0, (hipStream_t)stream>>>(
+        in, bounds, out, B, d, mode);
+    return check_launch("arqs_bounds_kernel");
+}
+
 // xr = to (x - lo) - bound per element (spline_coupling_layer.py:78-85, fp32 ops in order):
 // the conditioner input of a layer with data_min / data_max bounds (times the mask in the GEMM).
 __global__ __launch_bounds__(256) void spline_rescale_kernel(const float* __restrict__ x, const float* __restrict__ rs,

@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = (
     "nfx_flowbn_backward",
     "nfx_linear_forward", "nfx_linear_backward_data", "nfx_linear_workspace_bytes", "nfx_linear_backward_weight",
     "nfx_spline_elem_forward", "nfx_spline_elem_backward", "nfx_spline_elem_forward_bounded",
-    "nfx_spline_elem_backward_bounded", "nfx_spline_rescale",
+    "nfx_spline_elem_backward_bounded", "nfx_spline_rescale", "nfx_arqs_bounds",
     "nfx_made_elem_forward", "nfx_made_elem_step", "nfx_made_elem_finish", "nfx_made_elem_backward",
     "nfx_made_elem_seq_backward", "nfx_made_elem_seq_step_backward", "nfx_made_elem_prefix",
     "nfx_affine_elem_forward", "nfx_affine_elem_backward", "nfx_bn_prepare", "nfx_bn_apply_relu",
@@ -129,6 +129,7 @@ _SIGNATURES = {
     "nfx_spline_elem_backward_bounded": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _f, _f, _f,
                                                 _f, _int, _vp]),
     "nfx_spline_rescale": (_int, [_vp, _vp, _vp, _i64, _int, _f, _vp]),
+    "nfx_arqs_bounds": (_int, [_vp, _vp, _vp, _i64, _int, _int, _vp]),
     "nfx_affine_chain_supported": (_int, [_i64, _int, _int]),
     "nfx_affine_chain": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,

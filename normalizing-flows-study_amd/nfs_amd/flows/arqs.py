@@ -13,9 +13,10 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .. import distributed as _dist
 from . import generic as _generic
-from .autoregressive import MADE
-from .flow import HipFlow
+from .autoregressive import MADE, bn_train_supported, made_bn_eval_params, made_bn_train_call
+from .flow import STATS, HipFlow
 from .spline import _rqs_unit_torch
 
 MAX_K = 11   # 3K-1 <= 32: one MFMA row tile of spline parameters per step
@@ -91,18 +92,46 @@ class ARQS(HipFlow):
             return False, f"input shape {tuple(x.shape)} vs dim={d}"
         if K > MAX_K or K < 2:
             return False, f"K={K} (2..{MAX_K})"
-        if self._rescale_scalars() is None:
-            return False, "per-dimension data_min/data_max tensors"
         if not self._fused_family() and not self._generic_ok():
-            return False, f"H={H} > {MAX_H} needs data_min/data_max None (any-shape path)"
+            return False, "data_min/data_max of a shape other than scalar or [dim]"
         return True, ""
 
     def _fused_family(self):
-        """Shapes of the fused ARQS kernel (nfx_arqs*.hip: H <= 128)."""
-        return not FORCE_GENERIC and self.conditioner.hidden_dim <= MAX_H
+        """Shapes of the fused ARQS kernel (nfx_arqs*.hip: H <= 128, scalar bounds)."""
+        return not FORCE_GENERIC and self.conditioner.hidden_dim <= MAX_H and self._rescale_scalars() is not None
 
     def _generic_ok(self):
-        return 2 <= self.num_bins <= MAX_K and (self.data_min is None or self.data_max is None)
+        """The any-shape path: 2 <= K <= 11, bounds None, scalar or per-dimension."""
+        if not 2 <= self.num_bins <= MAX_K:
+            return False
+        if self.data_min is None or self.data_max is None:
+            return True
+        return all((not torch.is_tensor(t)) or t.numel() in (1, self.dim) for t in (self.data_min, self.data_max))
+
+    def _bounds(self, device):
+        """[2][d] float32 on the device = data_min | data_max - data_min, rounded as the reference's
+        _rescale_to_unit / _rescale_from_unit expressions (python floats in double, tensors in
+        fp32), cached with the parameters (keyed on the bound objects too); None without bounds."""
+        if self.data_min is None or self.data_max is None:
+            return None
+        key = (id(self.data_min), id(self.data_max), getattr(self.data_min, "_version", 0),
+               getattr(self.data_max, "_version", 0))
+        if self.__dict__.get("_nfx_bounds_key") != key:
+            self.__dict__.pop("_nfx_bounds_pack_cache", None)
+            object.__setattr__(self, "_nfx_bounds_key", key)
+        return self._packed(device, self._build_bounds, slot="_nfx_bounds_pack_cache")
+
+    def _build_bounds(self, device):
+        cpu = lambda v: v.detach().cpu() if torch.is_tensor(v) else v  # noqa: E731
+        lo, hi = cpu(self.data_min), cpu(self.data_max)
+        rows = [torch.as_tensor(v, dtype=torch.float32).reshape(-1).expand(self.dim) for v in (lo, hi - lo)]
+        return torch.stack(rows).to(device=device).contiguous()
+
+    def _map(self, t, bounds, mode):
+        out = torch.empty_like(t)
+        _lib.check(_lib.lib().nfx_arqs_bounds(_lib.ptr(t), _lib.ptr(bounds), _lib.ptr(out), t.shape[0], self.dim,
+                                              mode, _lib.stream_of(t)), "nfx_arqs_bounds")
+        return out
 
     # -- any-shape path (csrc/nfx_generic.hip): the reference's d steps, MADE on MFMA GEMMs --------
     def _generic_pack(self, device):
@@ -137,7 +166,41 @@ class ARQS(HipFlow):
         return state, ld
 
     def _generic_launch(self, x, out, log_det, direction, accumulate):
-        self._generic_forward_state(x, direction, out, log_det if accumulate else log_det.zero_())
+        bounds = self._bounds(x.device)
+        if bounds is None:
+            self._generic_forward_state(x, direction, out, log_det if accumulate else log_det.zero_())
+            return
+        state, _ = self._generic_forward_state(self._map(x, bounds, 0), direction, None,
+                                               log_det if accumulate else log_det.zero_())
+        _lib.check(_lib.lib().nfx_arqs_bounds(_lib.ptr(state), _lib.ptr(bounds), _lib.ptr(out), x.shape[0], self.dim,
+                                              1, _lib.stream_of(x)), "nfx_arqs_bounds")
+
+    # -- train-mode BatchNorm in the MADE: the reference's d calls, each with batch statistics -----
+    def _dispatch(self, x, direction):
+        if bn_train_supported(self.conditioner, x, self.dim) and self._generic_ok():
+            STATS["hip"] += 1
+            if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+                return _ArqsTrainFunction.apply(self, direction, x, *list(self.parameters()))
+            return self._train_forward(x, direction)[:2]
+        return super()._dispatch(x, direction)
+
+    def _train_forward(self, x, direction):
+        """Returns (y, ld, state, bnps, counts): each step's MADE call normalises with the batch
+        statistics of the partial state and updates the running statistics (d updates)."""
+        x = x.detach().contiguous()
+        bounds = self._bounds(x.device)
+        xr = x if bounds is None else self._map(x, bounds, 0)
+        masks, _ = self._packed(x.device, self._generic_pack, slot="_nfx_generic_pack_cache")
+        state = torch.zeros_like(xr)
+        ld = torch.zeros(x.shape[0], device=x.device, dtype=torch.float32)
+        bnps, counts = [], []
+        for i in range(self.dim):
+            prm, bnp, cnt = made_bn_train_call(self.conditioner, masks, state)
+            self._step(xr, prm, state, ld, None, None, None, None, i, direction, 0)
+            bnps.append(bnp)
+            counts.append(cnt)
+        y = state.clone() if bounds is None else self._map(state, bounds, 1)
+        return y, ld, state, bnps, counts
 
     def _build_pack(self, device):
         d, H, K = self.dim, self.conditioner.hidden_dim, self.num_bins
@@ -152,31 +215,56 @@ class ARQS(HipFlow):
 
     # -- backward (training): reverse-mode through the reference's d steps ------------------------
     def _hip_backward_ok(self, x, direction):
-        return (x.dtype == torch.float32 and not self.conditioner.batchnorms() and self._generic_ok())
+        bns = self.conditioner.batchnorms()
+        if bns and any(bn.training or not bn.affine or bn.running_mean is None for bn in bns):
+            return False  # (train mode runs _ArqsTrainFunction)
+        return x.dtype == torch.float32 and self._generic_ok()
 
-    def _hip_backward(self, x, gy, gld, direction):
+    def _hip_backward(self, x, gy, gld, direction, train=None):
         """dL/dx and the parameter gradients (parameters() order) of one call, reverse-mode through
         the reference's d steps: the state before step i is the final state with columns >= i
-        zeroed (each column is written once), so step i's MADE is recomputed there (GEMMs), its
-        spline row differentiated (nfx_arqs_step mode 1: rqs_unit_adjoint), the MADE's weight
-        gradients accumulated and its input VJP added into the running state adjoint."""
+        zeroed (each column is written once), so step i's MADE is recomputed there (GEMMs; with
+        BatchNorm: eval running statistics, or call i's own batch statistics when train =
+        (state, bnps, counts) from _train_forward), its spline row differentiated (nfx_arqs_step
+        mode 1: rqs_unit_adjoint), the MADE's weight gradients accumulated and its input VJP added
+        into the running state adjoint. With bounds, dL/dstate = gy w and dL/dx = dL/dxr / w."""
         x = x.contiguous()
         B, d = x.shape
         gy = torch.zeros_like(x) if gy is None else gy.contiguous().float()
         gld = torch.zeros(B, device=x.device) if gld is None else gld.contiguous().float()
-        state, _ = self._generic_forward_state(x, direction)
-        lam = gy.clone()
+        bounds = self._bounds(x.device)
+        xr = x if bounds is None else self._map(x, bounds, 0)
+        if train is not None:
+            state = train[0].clone()
+        else:
+            state, _ = self._generic_forward_state(xr, direction)
+        lam = gy.clone() if bounds is None else self._map(gy, bounds, 3)
         gx = torch.empty_like(x)
         R = 3 * self.num_bins - 1
         gprm = torch.zeros(B, d * R, device=x.device, dtype=torch.float32)
         lins = self.conditioner.linears()
+        bns = self.conditioner.batchnorms()
+        if bns:
+            masks, _ = self._packed(x.device, self._generic_pack, slot="_nfx_generic_pack_cache")
+            eval_bnp = None if train is not None else self._packed(
+                x.device, lambda dev: made_bn_eval_params(self.conditioner, dev), slot="_nfx_generic_bn_pack_cache")
         grads = None
         for i in reversed(range(d)):
             self._step(None, None, state, None, None, None, None, None, i, direction, 2)
-            masks, (h1, h2, h3, prm) = self._generic_made(state)
-            self._step(x, prm, state, None, gld, lam, gprm, gx, i, direction, 1)
-            gi = _generic.made_backward(state, lins, masks, h1, h2, h3, gprm, lam)
+            if bns:
+                bnp = train[1][i] if train is not None else eval_bnp
+                acts, prm = _generic.made_bn_forward(state, lins, masks, bnp)
+                self._step(xr, prm, state, None, gld, lam, gprm, gx, i, direction, 1)
+                gi = _generic.made_bn_backward(state, lins, masks, bns, bnp, acts, gprm, lam, train is not None,
+                                               train[2][i] if train is not None else None,
+                                               _dist.allreduce_bn_sums if train is not None else None)
+            else:
+                masks, (h1, h2, h3, prm) = self._generic_made(state)
+                self._step(xr, prm, state, None, gld, lam, gprm, gx, i, direction, 1)
+                gi = _generic.made_backward(state, lins, masks, h1, h2, h3, gprm, lam)
             grads = gi if grads is None else [a.add_(b) for a, b in zip(grads, gi)]
+        if bounds is not None:
+            gx = self._map(gx, bounds, 2)
         return gx, grads
 
     def _hip_launch(self, x, out, log_det, direction, accumulate):
@@ -189,3 +277,24 @@ class ARQS(HipFlow):
             self.conditioner.hidden_dim, self.num_bins, float(self.min_bin_width),
             float(self.min_bin_height), float(self.min_derivative), rescale, lo, hi, int(direction),
             int(bool(accumulate)), _lib.stream_of(x)), "nfx_arqs")
+
+
+class _ArqsTrainFunction(torch.autograd.Function):
+    """ARQS with train-mode BatchNorm in the MADE: the reference's d calls, each normalising with
+    the batch statistics of the partial state (running statistics updated d times), then the
+    reverse sweep with each call's own statistics (ARQS._hip_backward(train=...))."""
+
+    @staticmethod
+    def forward(ctx, layer, direction, x, *params):
+        y, ld, state, bnps, counts = layer._train_forward(x, direction)
+        ctx.layer, ctx.direction, ctx.bnps, ctx.counts = layer, direction, bnps, counts
+        ctx.save_for_backward(x, state)
+        return y, ld
+
+    @staticmethod
+    def backward(ctx, gy, gld):
+        x, state = ctx.saved_tensors
+        gx, grads = ctx.layer._hip_backward(x.detach(), gy, gld, ctx.direction, train=(state, ctx.bnps, ctx.counts))
+        STATS["hip"] += 1
+        params = list(ctx.layer.parameters())
+        return (None, None, gx, *[g if p.requires_grad else None for p, g in zip(params, grads)])

@@ -166,17 +166,7 @@ class _MadeAffineFlow(HipFlow):
 
     def _generic_bn_eval(self, device):
         """Per MADE BatchNorm [mean, invstd, scale, shift] from the running statistics."""
-        L = _lib.lib()
-        out = []
-        for bn in self.conditioner.batchnorms():
-            H = bn.num_features
-            t = torch.empty(4, H, device=device, dtype=torch.float32)
-            _lib.check(L.nfx_bn_prepare(None, _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()),
-                                        _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var), float(bn.eps), 0.0, 0,
-                                        H, _lib.ptr(t[0]), _lib.ptr(t[1]), _lib.ptr(t[2]), _lib.ptr(t[3]),
-                                        _lib.stream_of(t)), "nfx_bn_prepare")
-            out.append(t)
-        return out
+        return made_bn_eval_params(self.conditioner, device)
 
     def _generic_made_bn(self, x, bnp=None):
         """MADE with BatchNorm (eval: running statistics unless bnp is given): (masks, acts, params)."""
@@ -191,13 +181,7 @@ class _MadeAffineFlow(HipFlow):
 
     # -- train-mode BatchNorm in the MADE (use_batch_norm=True) ---------------------------------------
     def _bn_train_any(self, x):
-        bns = self.conditioner.batchnorms()
-        if not bns or not all(bn.training for bn in bns) or x.device.type != "cuda" or x.dtype != torch.float32:
-            return False
-        if any(not bn.affine or not bn.track_running_stats or bn.momentum is None or bn.running_mean is None
-               or bn.num_features > _generic_bn_max() for bn in bns):
-            return False
-        return x.dim() == 2 and x.shape[1] == self.dim and x.shape[0] >= 2
+        return bn_train_supported(self.conditioner, x, self.dim)
 
     def _bn_train_ok(self, x, direction):
         """Parallel direction: one MADE call with batch statistics."""
@@ -223,36 +207,9 @@ class _MadeAffineFlow(HipFlow):
         return super()._dispatch(x, direction)
 
     def _generic_made_bn_train(self, h):
-        """One train-mode MADE call on h: batch moments per BatchNorm (nfx_flowbn_moments,
-        SyncBN-merged), running update + normalisation (nfx_bn_prepare), ReLU; returns (params,
-        bnp, counts)."""
-        L = _lib.lib()
-        B = h.shape[0]
-        dev = h.device
-        st = _lib.stream_of(h)
-        p = _lib.ptr
-        masks, _ = self._packed(dev, self._generic_pack, slot="_nfx_generic_pack_cache")
-        lins = self.conditioner.linears()
-        bns = self.conditioner.batchnorms()
-        bnp, counts = [], []
-        for i, bn in enumerate(bns):
-            z = _generic.linear_forward(h, lins[i], wmask=masks[i])
-            H = z.shape[1]
-            ws = torch.empty(max(1, L.nfx_flowbn_workspace_bytes(B, H)), device=dev, dtype=torch.uint8)
-            stats = torch.empty(H, 3, device=dev, dtype=torch.float64)
-            _lib.check(L.nfx_flowbn_moments(p(z), B, H, p(stats), p(ws), st), "nfx_flowbn_moments")
-            _dist.merge_bn_stats(stats)
-            t = torch.empty(4, H, device=dev, dtype=torch.float32)
-            _lib.check(L.nfx_bn_prepare(p(stats), p(bn.weight.detach()), p(bn.bias.detach()), p(bn.running_mean),
-                                        p(bn.running_var), float(bn.eps), float(bn.momentum), 1, H, p(t[0]), p(t[1]),
-                                        p(t[2]), p(t[3]), st), "nfx_bn_prepare")
-            torch.autograd.graph.increment_version(bn.running_mean)
-            torch.autograd.graph.increment_version(bn.running_var)
-            h = _generic.bn_apply_relu(z, t)
-            bnp.append(t)
-            counts.append(stats)  # stats[0, 0] = the global sample count
-        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
-        return _generic.linear_forward(h, lins[3], wmask=masks[3]), bnp, counts
+        """One train-mode MADE call on h (made_bn_train_call): (params, bnp, counts)."""
+        masks, _ = self._packed(h.device, self._generic_pack, slot="_nfx_generic_pack_cache")
+        return made_bn_train_call(self.conditioner, masks, h)
 
     def _generic_seq_train_forward(self, x, direction):
         """A sequential direction with train-mode BatchNorm, as the reference runs it: d MADE calls
@@ -312,40 +269,17 @@ class _MadeAffineFlow(HipFlow):
         return gx, acc
 
     def _generic_train_forward(self, x, direction):
-        """Batch moments per MADE BatchNorm (nfx_flowbn_moments, SyncBN-merged), normalisation and
-        running update (nfx_bn_prepare), then the parallel element map. Returns (y, ld, bnp, counts)."""
+        """One train-mode MADE call on x (made_bn_train_call: batch moments, SyncBN merge, running
+        update, normalisation), then the parallel element map. Returns (y, ld, bnp, counts)."""
         L = _lib.lib()
         x = x.detach().contiguous()
         B, d = x.shape
-        dev = x.device
-        st = _lib.stream_of(x)
         p = _lib.ptr
-        masks, _ = self._packed(dev, self._generic_pack, slot="_nfx_generic_pack_cache")
-        lins = self.conditioner.linears()
-        bns = self.conditioner.batchnorms()
-        bnp, counts, h = [], [], x
-        for i, bn in enumerate(bns):
-            z = _generic.linear_forward(h, lins[i], wmask=masks[i])
-            H = z.shape[1]
-            ws = torch.empty(max(1, L.nfx_flowbn_workspace_bytes(B, H)), device=dev, dtype=torch.uint8)
-            stats = torch.empty(H, 3, device=dev, dtype=torch.float64)
-            _lib.check(L.nfx_flowbn_moments(p(z), B, H, p(stats), p(ws), st), "nfx_flowbn_moments")
-            _dist.merge_bn_stats(stats)
-            t = torch.empty(4, H, device=dev, dtype=torch.float32)
-            _lib.check(L.nfx_bn_prepare(p(stats), p(bn.weight.detach()), p(bn.bias.detach()), p(bn.running_mean),
-                                        p(bn.running_var), float(bn.eps), float(bn.momentum), 1, H, p(t[0]), p(t[1]),
-                                        p(t[2]), p(t[3]), st), "nfx_bn_prepare")
-            torch.autograd.graph.increment_version(bn.running_mean)
-            torch.autograd.graph.increment_version(bn.running_var)
-            h = _generic.bn_apply_relu(z, t)
-            bnp.append(t)
-            counts.append(stats)  # stats[0, 0] = the global sample count
-        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
-        prm = _generic.linear_forward(h, lins[3], wmask=masks[3])
+        prm, bnp, counts = self._generic_made_bn_train(x)
         y = torch.empty_like(x)
-        ld = torch.empty(B, device=dev, dtype=torch.float32)
-        _lib.check(L.nfx_made_elem_forward(p(x), p(prm), p(y), p(ld), B, d, self._variant(direction), 0, st),
-                   "nfx_made_elem_forward")
+        ld = torch.empty(B, device=x.device, dtype=torch.float32)
+        _lib.check(L.nfx_made_elem_forward(p(x), p(prm), p(y), p(ld), B, d, self._variant(direction), 0,
+                                           _lib.stream_of(x)), "nfx_made_elem_forward")
         return y, ld, bnp, counts
 
     def _generic_bn_backward(self, x, gz, gld, direction, bnp=None, counts=None):
@@ -569,6 +503,66 @@ class _MadeAffineFlow(HipFlow):
             return False  # no fused kernel for this (d, H): nothing was launched
         _lib.check(rc, "nfx_made_affine_logprob")
         return True
+
+
+def made_bn_train_call(conditioner, masks, h):
+    """One train-mode call of a BatchNorm MADE (use_batch_norm=True, made.py:93-106) on h: per
+    BatchNorm the batch moments (nfx_flowbn_moments, SyncBN-merged), the running update and the
+    normalisation (nfx_bn_prepare), ReLU; returns (params, bnp, counts), bnp / counts being what the
+    batch-statistics backward (generic.made_bn_backward(train=True)) needs."""
+    L = _lib.lib()
+    B = h.shape[0]
+    dev = h.device
+    st = _lib.stream_of(h)
+    p = _lib.ptr
+    lins = conditioner.linears()
+    bns = conditioner.batchnorms()
+    bnp, counts = [], []
+    for i, bn in enumerate(bns):
+        z = _generic.linear_forward(h, lins[i], wmask=masks[i])
+        H = z.shape[1]
+        ws = torch.empty(max(1, L.nfx_flowbn_workspace_bytes(B, H)), device=dev, dtype=torch.uint8)
+        stats = torch.empty(H, 3, device=dev, dtype=torch.float64)
+        _lib.check(L.nfx_flowbn_moments(p(z), B, H, p(stats), p(ws), st), "nfx_flowbn_moments")
+        _dist.merge_bn_stats(stats)
+        t = torch.empty(4, H, device=dev, dtype=torch.float32)
+        _lib.check(L.nfx_bn_prepare(p(stats), p(bn.weight.detach()), p(bn.bias.detach()), p(bn.running_mean),
+                                    p(bn.running_var), float(bn.eps), float(bn.momentum), 1, H, p(t[0]), p(t[1]),
+                                    p(t[2]), p(t[3]), st), "nfx_bn_prepare")
+        torch.autograd.graph.increment_version(bn.running_mean)
+        torch.autograd.graph.increment_version(bn.running_var)
+        h = _generic.bn_apply_relu(z, t)
+        bnp.append(t)
+        counts.append(stats)  # stats[0, 0] = the global sample count
+    torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
+    return _generic.linear_forward(h, lins[3], wmask=masks[3]), bnp, counts
+
+
+def made_bn_eval_params(conditioner, device):
+    """Per MADE BatchNorm [mean, invstd, scale, shift] from the running statistics (eval mode)."""
+    L = _lib.lib()
+    out = []
+    for bn in conditioner.batchnorms():
+        H = bn.num_features
+        t = torch.empty(4, H, device=device, dtype=torch.float32)
+        _lib.check(L.nfx_bn_prepare(None, _lib.ptr(bn.weight.detach()), _lib.ptr(bn.bias.detach()),
+                                    _lib.ptr(bn.running_mean), _lib.ptr(bn.running_var), float(bn.eps), 0.0, 0,
+                                    H, _lib.ptr(t[0]), _lib.ptr(t[1]), _lib.ptr(t[2]), _lib.ptr(t[3]),
+                                    _lib.stream_of(t)), "nfx_bn_prepare")
+        out.append(t)
+    return out
+
+
+def bn_train_supported(conditioner, x, dim):
+    """Train-mode BatchNorm MADE on the HIP path: every BatchNorm affine, tracking running
+    statistics with a momentum, <= 1024 features; fp32 ROCm rows, B >= 2."""
+    bns = conditioner.batchnorms()
+    if not bns or not all(bn.training for bn in bns) or x.device.type != "cuda" or x.dtype != torch.float32:
+        return False
+    if any(not bn.affine or not bn.track_running_stats or bn.momentum is None or bn.running_mean is None
+           or bn.num_features > _generic_bn_max() for bn in bns):
+        return False
+    return x.dim() == 2 and x.shape[1] == dim and x.shape[0] >= 2
 
 
 def _generic_bn_max():

@@ -132,3 +132,80 @@ def test_spline_per_dimension_bounds_vs_reference(cuda_device, dname):
     _gclose(xr.grad, g[pre + "gx"], "dL/dx", x64.grad)
     for (k, p), (_, p64) in zip(gpu.named_parameters(), f64.named_parameters()):
         _gclose(p.grad, g[pre + "grad." + k], what=k, ref32=p64.grad)
+
+
+@pytest.mark.parametrize("dname", ["fwd", "inv"])
+def test_arqs_batchnorm_train_vs_reference(cuda_device, dname):
+    """arqsbn: ARQS(4, 32, K = 5, use_batch_norm=True) in TRAIN mode under autograd (arqs.py:44-114
+    with made.py:93-106): every one of the d steps' MADE calls normalises with the batch statistics
+    of the partial state and updates the running statistics; the backward differentiates call by
+    call with each call's statistics. Each direction starts from the fixture's initial state."""
+    from nfs_amd.flows.arqs import ARQS
+    g = load_golden("g17_options.npz")
+    f = _load(ARQS(4, 32, num_bins=5, use_batch_norm=True), g, "arqsbn.init.").train()
+    f64 = copy.deepcopy(f).double().train()
+    gpu = f.to(cuda_device)
+    x = torch.from_numpy(g["arqsbn.x"])
+    wy, wl = torch.from_numpy(g["arqsbn.wy"]), torch.from_numpy(g["arqsbn.wl"])
+    nfs_amd.reset_stats()
+    xr = x.to(cuda_device).requires_grad_(True)
+    y, ld = (gpu.forward if dname == "fwd" else gpu.inverse)(xr)
+    ((y * wy.to(cuda_device)).sum() + (ld * wl.to(cuda_device)).sum()).backward()
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 2, nfs_amd.STATS
+    x64 = x.double().requires_grad_(True)
+    y64, ld64 = (f64.forward if dname == "fwd" else f64.inverse)(x64)
+    ((y64 * wy.double()).sum() + (ld64 * wl.double()).sum()).backward()
+    pre = f"arqsbn.{dname}."
+    _gclose(y, g[pre + "y"], "y", y64, frac=2e-5)
+    _gclose(ld, g[pre + "ld"], "ld", ld64, frac=2e-5)
+    _gclose(xr.grad, g[pre + "gx"], "dL/dx", x64.grad)
+    for (k, p), (_, p64) in zip(gpu.named_parameters(), f64.named_parameters()):
+        _gclose(p.grad, g[pre + "grad." + k], what=k, ref32=p64.grad)
+    for k, v in gpu.state_dict().items():
+        if k.endswith(("running_mean", "running_var")):
+            np.testing.assert_allclose(v.cpu().numpy(), g[pre + "after." + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("dname", ["fwd", "inv"])
+@pytest.mark.parametrize("bn", [False, True])
+def test_arqs_per_dimension_bounds_and_eval_bn_backward(cuda_device, dname, bn):
+    """ARQS with per-dimension data_min / data_max tensors (arqs.py:28-42; the reference broadcasts
+    them over every dim) and, with bn, an eval-mode BatchNorm MADE, under autograd on the any-shape
+    path (nfx_arqs_bounds + the reverse sweep with the running statistics): y, log-det, dL/dx and
+    every parameter gradient vs float64 autograd of the same module, side by side with the fp32
+    composite on the CPU (parity unpinned by a reference fixture: G10 holds scalar bounds only)."""
+    from nfs_amd.flows.arqs import ARQS
+    torch.manual_seed(41)
+    f = ARQS(3, 24, num_bins=4, data_min=torch.tensor([-2.0, -1.0, -3.0]), data_max=torch.tensor([2.0, 3.0, 1.5]),
+             use_batch_norm=bn)
+    g = torch.Generator().manual_seed(42)
+    with torch.no_grad():
+        for p in f.parameters():
+            p.add_(0.2 * torch.randn(p.shape, generator=g))
+        for m in f.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.copy_(0.1 * torch.randn(m.running_mean.shape, generator=g))
+                m.running_var.copy_(0.5 + torch.rand(m.running_var.shape, generator=g))
+    f = f.eval()
+    f32, f64 = copy.deepcopy(f), copy.deepcopy(f).double()
+    f64.data_min, f64.data_max = f.data_min.double(), f.data_max.double()
+    x = torch.rand(300, 3, generator=g) * torch.tensor([3.5, 3.5, 4.0]) + torch.tensor([-1.7, -0.8, -2.8])
+    wy, wl = torch.randn(300, 3, generator=g), torch.randn(300, generator=g)
+
+    def run(mod, xx, ww, wwl):
+        xx = xx.clone().requires_grad_(True)
+        y, ld = (mod.forward if dname == "fwd" else mod.inverse)(xx)
+        ((y * ww).sum() + (ld * wwl).sum()).backward()
+        return y.detach(), ld.detach(), xx.grad, [p.grad for p in mod.parameters()]
+
+    r32 = run(f32, x, wy, wl)
+    r64 = run(f64, x.double(), wy.double(), wl.double())
+    gpu = f.to(cuda_device)
+    gpu.data_min, gpu.data_max = f.data_min.to(cuda_device), f.data_max.to(cuda_device)
+    nfs_amd.reset_stats()
+    rg = run(gpu, x.to(cuda_device), wy.to(cuda_device), wl.to(cuda_device))
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] == 2, nfs_amd.STATS
+    for a, b, r, what in ((rg[0], r64[0], r32[0], "y"), (rg[1], r64[1], r32[1], "ld"), (rg[2], r64[2], r32[2], "gx")):
+        _gclose(a, b, what, r, frac=2e-5)
+    for a, b, r in zip(rg[3], r64[3], r32[3]):
+        _gclose(a, b, "param grad", r)
