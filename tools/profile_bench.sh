@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # rocprofv3 around bench.py ITSELF (no launcher hop), one config per run, so the kernel trace and
 # the bench line's ms_per_step come from one process and one clock (run on the GPU box via gpurun):
-#   bash tools/profile_bench.sh <tag> [--pmc] <cfg>[:<batch>] ...
+#   bash tools/profile_bench.sh <tag> [--pmc] <cfg>[:<batch>][+graph] ...
 # Writes gpurun_out/prof_<tag>/<cfg>[_<batch>]/{trace/,bench.json,fetch/,write/}. The PMC passes
 # (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) are separate runs with --kernel-trace only.
 # Reconcile afterwards on the CPU: python tools/reconcile_profile.py gpurun_out/prof_<tag> <round tag>
@@ -14,13 +14,15 @@ export TMPDIR=/tmp
 out="$root/gpurun_out/prof_$tag"
 mkdir -p "$out"
 cd /tmp || exit 1
-for spec in "$@"; do
+for spec0 in "$@"; do
+  spec="${spec0%+graph}"   # a trailing +graph: replay the captured training step (--graph)
   c="${spec%%:*}"
   b=""
   name="$c"
   if [ "$spec" != "$c" ]; then b="${spec#*:}"; name="${c}_$b"; fi
   extra=()
   if [ -n "$b" ]; then extra=(--batch "$b"); fi
+  if [ "$spec0" != "$spec" ]; then extra+=(--graph); fi
   d="$out/$name"
   mkdir -p "$d"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/trace" -- \
