@@ -33,7 +33,11 @@
 extern "C" {
 #endif
 
-#define NFX_ABI_VERSION 1
+/* ABI 2: the log_prob workspace (nfx_gauss_workspace_bytes) must be zero-filled before its first
+ * use (the fused epilogues' last workgroup finishes the float64 sums in the same launch and resets
+ * a counter in it); nfx_made_affine_backward / nfx_made_seq_backward / nfx_made_backward_weights
+ * return NFX_EUNSUPPORTED above nfx_made_backward_max_batch(d, H) (callers split the batch). */
+#define NFX_ABI_VERSION 2
 
 #define NFX_OK 0
 #define NFX_EINVAL (-1)
@@ -364,7 +368,10 @@ int nfx_affine_eval_stats(float* const* running_mean, float* const* running_var,
  *   logp[i] = -0.5 * (fp32(d*log(2*pi)) + sum_j z[i,j]^2) + log_det[i]
  * (torch.distributions.MultivariateNormal(0, I).log_prob(z) + log_det).
  * sums[0] = sum_i logp[i] in float64, sums[1] = B (as double). `workspace` must hold
- * nfx_gauss_workspace_bytes(B) bytes. logp may be NULL (NLL-only).
+ * nfx_gauss_workspace_bytes(B) bytes, ZERO-FILLED before its first use: every call that writes
+ * sums (this one and the fused *_logprob epilogues) reduces the per-workgroup partials in its last
+ * workgroup and leaves the workspace's arrival counter at zero again, so one workspace serves any
+ * number of stream-ordered calls (not two concurrent ones). logp may be NULL (NLL-only).
  * ------------------------------------------------------------------------------------- */
 size_t nfx_gauss_workspace_bytes(int64_t B);
 int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,

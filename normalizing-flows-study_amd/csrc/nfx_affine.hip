@@ -117,7 +117,7 @@ static std::atomic<int>& affine_policy() {
 int affine_policy_get() { return affine_policy().load(std::memory_order_relaxed); }
 
 typedef void (*affine_wide_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t, float*,
-                              double*, float);
+                              double*, double*, float);
 
 template <int HT>
 static affine_wide_t wide_pick(int dir, bool logp) {
@@ -144,10 +144,8 @@ static int affine_wide_launch(const float* packed, const float* in, float* out, 
     if (grid > kMaxPartials) grid = kMaxPartials;
     double* partials = reinterpret_cast<double*>(workspace);
     k<<<grid, 64 * kWideWaves, lds, stream>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials,
-                                              gauss_const(d));
-    int rc = check_launch("affine_wide_kernel");
-    if (rc || !fused) return rc;
-    return gauss_finish(partials, grid, sums, B, stream);
+                                              sums, gauss_const(d));
+    return check_launch("affine_wide_kernel");  // (LOGP: the last workgroup wrote sums)
 }
 
 static int affine_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B,
@@ -185,10 +183,8 @@ static int affine_launch(const float* packed, const float* in, float* out, float
     if (small) {
         if (grid_small > kMaxPartials) grid_small = kMaxPartials;
         ks<<<grid_small, 128 * HT, 0, stream>>>(packed, in, out, log_det, B, accumulate, ntiles, logp,
-                                                partials, gauss_const(d));
-        rc = check_launch("affine_small_kernel");
-        if (rc || !fused) return rc;
-        return gauss_finish(partials, grid_small, sums, B, stream);
+                                                partials, sums, gauss_const(d));
+        return check_launch("affine_small_kernel");
     }
     // Up to one 32-sample half chunk per wave: when the resident waves outnumber the 64-sample
     // chunks (small batches, e.g. a strong-scaled 125k shard), the kernel's split gives every wave
@@ -196,10 +192,9 @@ static int affine_launch(const float* packed, const float* in, float* out, float
     // wave's chain: 64 -> 32 samples halves it)
     int grid = resident_grid((const void*)k, 256, lds, ((B + 31) / 32 + 3) / 4);
     if (grid > kMaxPartials) grid = kMaxPartials;
-    k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, accumulate, nchunks, logp, partials, gauss_const(d));
-    rc = check_launch("affine_coupling_kernel");
-    if (rc || !fused) return rc;
-    return gauss_finish(partials, grid, sums, B, stream);
+    k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, accumulate, nchunks, logp, partials, sums,
+                                  gauss_const(d));
+    return check_launch("affine_coupling_kernel");
 }
 
 // Grid: enough resident workgroups to fill every CU (occupancy from the runtime), never more

@@ -22,7 +22,7 @@ template <int HT, int D, int DIR, bool LOGP>
 __global__ __launch_bounds__(128 * HT) void affine_chain_kernel(NfxChainPacks packs, int nl, const float* __restrict__ in,
                                                                 float* __restrict__ out, float* __restrict__ logdet,
                                                                 int64_t B, int accumulate, int64_t ntiles, int tpw,
-                                                                float* __restrict__ logp, double* __restrict__ partials,
+                                                                float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums,
                                                                 float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
@@ -173,13 +173,12 @@ __global__ __launch_bounds__(128 * HT) void affine_chain_kernel(NfxChainPacks pa
         }
     }
     if constexpr (LOGP) {
-        const double tsum = block_sum_f64<NTHR>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+        logp_commit<NTHR>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*affine_chain_t)(NfxChainPacks, int, const float*, float*, float*, int64_t, int, int64_t, int, float*,
-                               double*, float);
+                               double*, double*, float);
 
 template <int HT, int D>
 static affine_chain_t chain_pick_d(int dir, bool logp) {
@@ -260,10 +259,8 @@ static int chain_launch(const float* const* packs, int nl, const float* in, floa
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
     k<<<(unsigned)grid, 128 * HT, lds, s>>>(P, nl, in, out, log_det, B, accumulate, ntiles, (int)tpw, logp,
-                                            reinterpret_cast<double*>(workspace), gauss_const(d));
-    rc = check_launch("affine_chain_kernel");
-    if (rc || !fused) return rc;
-    return gauss_finish(reinterpret_cast<double*>(workspace), (int)grid, sums, B, s);
+                                            reinterpret_cast<double*>(workspace), sums, gauss_const(d));
+    return check_launch("affine_chain_kernel");
 }
 
 }  // namespace nfx

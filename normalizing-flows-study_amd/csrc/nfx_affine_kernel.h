@@ -148,7 +148,7 @@ template <int HT, int D, int DIR, bool LOGP>
 __global__ __launch_bounds__(256) void affine_coupling_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int accumulate, int64_t nchunks,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
     extern __shared__ f32x4 lds4[];
@@ -271,8 +271,7 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
     }
     if (half) unit(std::integral_constant<int, 1>{}, half_base, cur);
     if constexpr (LOGP) {
-        const double t = block_sum_f64<256>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<256>(lpacc, partials, sums, B);
     }
 }
 
@@ -345,7 +344,7 @@ template <int HT, int DIR, bool LOGP>
 __global__ __launch_bounds__(64 * kWideWaves) void affine_wide_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     const AffineLayout L = affine_layout(d, HT);
     const int S = d | 1;
     extern __shared__ f32x4 lds4[];
@@ -414,13 +413,12 @@ __global__ __launch_bounds__(64 * kWideWaves) void affine_wide_kernel(
         wave_lds_sync();
     }
     if constexpr (LOGP) {
-        const double tsum = block_sum_f64<64 * kWideWaves>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+        logp_commit<64 * kWideWaves>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*affine_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int64_t,
-                                float*, double*, float);
+                                float*, double*, double*, float);
 
 template <int HT>
 affine_kernel_t affine_pick_ht(int d, int dir, bool logp);

@@ -32,7 +32,7 @@ template <int HT, int D, int DIR, bool LOGP, int NW>
 __global__ __launch_bounds__(64 * NW) void affine_schain_kernel(
     NfxChainPacks packs, int nl, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int accumulate, int64_t nchunks, int slice_chunks,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
     constexpr int WPAD = schain_wpad<HT, D>();
@@ -167,13 +167,12 @@ __global__ __launch_bounds__(64 * NW) void affine_schain_kernel(
         __syncthreads();  // the next slice overwrites the rows
     }
     if constexpr (LOGP) {
-        const double t = block_sum_f64<NT>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<NT>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*schain_t)(NfxChainPacks, int, const float*, float*, float*, int64_t, int, int64_t, int, float*,
-                         double*, float);
+                         double*, double*, float);
 
 // Waves per workgroup: one workgroup per CU (its LDS holds two weight images + the row slice),
 // 3 waves per SIMD as the per-layer kernel runs (<= 168 VGPRs).
@@ -230,10 +229,9 @@ int schain_launch(const NfxChainPacks& P, int nl, const float* in, float* out, f
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
     k<<<(unsigned)grid, 64 * kSchainWaves, lds, s>>>(P, nl, in, out, log_det, B, accumulate, nchunks, (int)slice,
-                                                      logp, reinterpret_cast<double*>(workspace), gauss_const(d));
-    rc = check_launch("affine_schain_kernel");
-    if (rc || !fused) return rc;
-    return gauss_finish(reinterpret_cast<double*>(workspace), (int)grid, sums, B, s);
+                                                      logp, reinterpret_cast<double*>(workspace), sums,
+                                                      gauss_const(d));
+    return check_launch("affine_schain_kernel");
 }
 
 }  // namespace nfx

@@ -24,7 +24,7 @@ template <int HT, int D, int DIR, bool LOGP>
 __global__ __launch_bounds__(128 * HT) void affine_small_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int accumulate, int64_t ntiles,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
     constexpr int NB1 = HT * 32;            // b1 of one net
@@ -173,8 +173,7 @@ __global__ __launch_bounds__(128 * HT) void affine_small_kernel(
         for (int ks = 0; ks < KS1; ++ks) xcur[ks] = xnxt[ks];
     }
     if constexpr (LOGP) {
-        const double tsum = block_sum_f64<NTHR>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+        logp_commit<NTHR>(lpacc, partials, sums, B);
     }
 }
 

@@ -147,7 +147,50 @@ __device__ __forceinline__ float gauss_lp(float m, float c, float ld) {
 
 // Capacity (doubles) of the partial-sum workspace shared by nfx_gauss_logprob and the fused
 // *_logprob layer epilogues; every launch that writes partials uses at most this many blocks.
+// The workspace holds kMaxPartials doubles of partials, then the arrival counter of
+// logp_commit (zero between launches: the caller zero-fills the workspace once, every launch's
+// last workgroup resets it).
 constexpr int kMaxPartials = 4096;
+
+// End of a fused log_prob epilogue: each workgroup's float64 sum of its log-densities goes to
+// partials[blockIdx.x]; the LAST workgroup to arrive (agent-scope counter after the workspace's
+// partials) reduces them into sums = [sum, (double)B] and resets the counter — no separate finish
+// launch. The reduction replays gauss_finish_kernel's order exactly (256 strided accumulators, a
+// shuffle-down tree per 64, the four wave sums in order), so fused and unfused results agree bit
+// for bit whatever the workgroup size NT (a multiple of 64).
+template <int NT>
+__device__ __forceinline__ void logp_commit(double v, double* partials, double* sums, int64_t B) {
+    static_assert(NT % 64 == 0, "whole waves");
+    const double t = block_sum_f64<NT>(v);
+    __shared__ int last;
+    __shared__ double red4[4];
+    unsigned* cnt = reinterpret_cast<unsigned*>(partials + kMaxPartials);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = t;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int n = (int)gridDim.x, lane = threadIdx.x & 63;
+    for (int vw = threadIdx.x >> 6; vw < 4; vw += NT / 64) {
+        double acc = 0.0;
+        for (int i = vw * 64 + lane; i < n; i += 256) acc += partials[i];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+        if (lane == 0) red4[vw] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int w = 0; w < 4; ++w) s += red4[w];
+        sums[0] = s;
+        sums[1] = (double)B;
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 }  // namespace nfx
 

@@ -20,7 +20,7 @@ __device__ __forceinline__ double block_sum_f64(double v) { return block_sum_f64
 
 __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
     const float* __restrict__ z, const float* __restrict__ ld, float* __restrict__ logp,
-    double* __restrict__ partials, int64_t B, int d, float c) {
+    double* __restrict__ partials, double* __restrict__ sums, int64_t B, int d, float c) {
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kGaussThreads + threadIdx.x; i < B;
          i += (int64_t)gridDim.x * kGaussThreads) {
@@ -31,8 +31,7 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
         if (logp) logp[i] = lp;
         acc += (double)lp;
     }
-    const double t = block_sum_f64(acc);
-    if (threadIdx.x == 0) partials[blockIdx.x] = t;
+    logp_commit<kGaussThreads>(acc, partials, sums, B);
 }
 
 // d > 8: a thread-per-sample walk over [B, d] rows is uncoalesced (64 lanes hit 64 lines per
@@ -41,7 +40,7 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_kernel(
 // then every lane sums its own row from LDS (stride-33 rows: conflict-free).
 __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_tiled_kernel(
     const float* __restrict__ z, const float* __restrict__ ld, float* __restrict__ logp,
-    double* __restrict__ partials, int64_t B, int d, float c) {
+    double* __restrict__ partials, double* __restrict__ sums, int64_t B, int d, float c) {
     __shared__ float stage[kGaussThreads / 64][64 * 33];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float* st = stage[wave];
@@ -77,8 +76,7 @@ __global__ __launch_bounds__(kGaussThreads) void gauss_logprob_tiled_kernel(
             acc += (double)lp;
         }
     }
-    const double tsum = block_sum_f64(acc);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    logp_commit<kGaussThreads>(acc, partials, sums, B);
 }
 
 __global__ __launch_bounds__(kGaussThreads) void gauss_finish_kernel(const double* __restrict__ partials,
@@ -104,7 +102,7 @@ using namespace nfx;
 
 extern "C" size_t nfx_gauss_workspace_bytes(int64_t B) {
     (void)B;
-    return (size_t)kMaxPartials * sizeof(double);
+    return (size_t)(kMaxPartials + 1) * sizeof(double);  // partials + logp_commit's arrival counter
 }
 
 extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
@@ -121,15 +119,15 @@ extern "C" int nfx_gauss_logprob(const float* z, const float* log_det, float* lo
     if (B > 0 && d > 8) {
         int64_t tb = ((B + 63) / 64 + 3) / 4;
         blocks = (int)(tb < kGaussMaxBlocks ? tb : kGaussMaxBlocks);
-        gauss_logprob_tiled_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, B, d, c);
+        gauss_logprob_tiled_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, sums, B, d, c);
         int rc = check_launch("gauss_logprob_tiled_kernel");
         if (rc) return rc;
     } else if (B > 0) {
-        gauss_logprob_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, B, d, c);
+        gauss_logprob_kernel<<<blocks, kGaussThreads, 0, s>>>(z, log_det, logp, partials, sums, B, d, c);
         int rc = check_launch("gauss_logprob_kernel");
         if (rc) return rc;
     } else {
-        blocks = 0;
+        return gauss_finish(partials, 0, sums, B, s);
     }
-    return gauss_finish(partials, blocks, sums, B, s);
+    return NFX_OK;  // the kernels' last workgroup wrote sums (logp_commit)
 }

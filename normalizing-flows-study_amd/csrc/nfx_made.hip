@@ -235,8 +235,8 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
 
 namespace nfx {
 int made_seqw_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d, int H,
-                     int variant, int accumulate, float* logp, double* partials, bool fused, int* grid_out,
-                     hipStream_t s);
+                     int variant, int accumulate, float* logp, double* partials, double* sums, bool fused,
+                     int* grid_out, hipStream_t s);
 }  // namespace nfx
 
 // Sequential-direction kernel choice (nfx_made_seq_policy): NFX_MADE_SEQ_AUTO (default, or
@@ -297,10 +297,8 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         int grid = resident_grid((const void*)k, 64 * nw, lds_nw, (nchunks + nw - 1) / nw);
         if (grid > kMaxPartials) grid = kMaxPartials;
         k<<<grid, 64 * nw, lds_nw, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, logp, partials,
-                                        gauss_const(d));
-        rc = check_launch("made_wide_kernel");
-        if (rc || !fused) return rc;
-        return gauss_finish(partials, grid, sums, B, s);
+                                        sums, gauss_const(d));
+        return check_launch("made_wide_kernel");  // (LOGP: the last workgroup wrote sums)
     }
     if ((variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) && d <= kTileMaxD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
@@ -314,11 +312,9 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         const int64_t ntiles = (B + 31) / 32;
         int grid = resident_grid((const void*)k, 512, lds, (ntiles + 7) / 8);
         if (grid > kMaxPartials) grid = kMaxPartials;
-        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials,
+        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials, sums,
                                  gauss_const(d));
-        rc = check_launch("made_tile_kernel");
-        if (rc || !fused) return rc;
-        return gauss_finish(partials, grid, sums, B, s);
+        return check_launch("made_tile_kernel");
     }
     if (variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) {
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
@@ -333,7 +329,8 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         const int64_t nchunks = (B + 63) / 64;
         const int nw = threads / 64;
         const int grid = resident_grid((const void*)k, threads, lds, (nchunks + nw - 1) / nw);
-        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, nullptr, nullptr, 0.f);
+        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, accumulate, nchunks, nullptr, nullptr, nullptr,
+                                     0.f);
         return check_launch("made_parallel_kernel");
     }
     // AUTO: the wave-per-sample kernel while the batch leaves the segment kernel's 4-sample waves
@@ -342,10 +339,8 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     const int seq_pol = made_seq_policy().load(std::memory_order_relaxed);
     if (seqs && (seq_pol == NFX_MADE_SEQ_WAVE || (seq_pol == NFX_MADE_SEQ_AUTO && B <= 2048 * (int64_t)num_cus() / 256))) {
         int grid = 0;
-        int rc = made_seqw_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, partials, fused, &grid,
-                                  s);
-        if (rc || !fused) return rc;
-        return gauss_finish(partials, grid, sums, B, s);
+        return made_seqw_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, partials, sums, fused,
+                                &grid, s);
     }
     if (seqs) {
         made_seqs_kernel_t k = HT == 1 ? made_seqs_pick_ht<1>(variant, fused) : made_seqs_pick_ht<2>(variant, fused);
@@ -355,10 +350,9 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         const int threads = kSeqsThreads;
         int grid = resident_grid((const void*)k, threads, lds, (B + 4 * kSeqsWaves - 1) / (4 * kSeqsWaves));
         if (grid > kMaxPartials) grid = kMaxPartials;
-        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials, gauss_const(d));
-        rc = check_launch("made_seqs_kernel");
-        if (rc || !fused) return rc;
-        return gauss_finish(partials, grid, sums, B, s);
+        k<<<grid, threads, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials, sums,
+                                     gauss_const(d));
+        return check_launch("made_seqs_kernel");
     }
     made_seq_kernel_t k = pick_seq(HT, variant);
     if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no sequential kernel for H=%d", H);

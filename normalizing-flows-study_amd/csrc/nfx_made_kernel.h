@@ -205,7 +205,8 @@ template <int HT, bool WLDS, int VAR>
 __global__ __launch_bounds__(WLDS ? 512 : 256) void made_parallel_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t nchunks,
-    float* __restrict__ /*logp*/, double* __restrict__ /*partials*/, float /*cgauss*/) {
+    float* __restrict__ /*logp*/, double* __restrict__ /*partials*/, double* __restrict__ /*sums*/,
+    float /*cgauss*/) {
     constexpr int NWAVE = WLDS ? 8 : 4;
     const MadeLayout L = made_layout(d, HT);
     extern __shared__ f32x4 lds4[];
@@ -583,7 +584,7 @@ template <int HT, bool WLDS, int VAR, bool LOGP>
 __global__ __launch_bounds__(512) void made_tile_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t ntiles,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     const MadeLayout L = made_layout(d, HT);
     constexpr int S = kTileStride;
     extern __shared__ f32x4 lds4[];
@@ -731,13 +732,12 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
         wave_lds_sync();
     }
     if constexpr (LOGP) {
-        const double tsum = block_sum_f64<512>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+        logp_commit<512>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*made_par_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int64_t,
-                                  float*, double*, float);
+                                  float*, double*, double*, float);
 
 template <int HT>
 made_par_kernel_t made_pick_ht(bool wlds, int variant);

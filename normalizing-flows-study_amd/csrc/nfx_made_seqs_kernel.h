@@ -221,7 +221,7 @@ template <int HT, int VAR, bool LOGP>
 __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int H, int accumulate, float* __restrict__ logp,
-    double* __restrict__ partials, float cgauss) {
+    double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr int Hp = 32 * HT;
     constexpr int UPL = Hp / 16;  // hidden-unit slots per lane
     constexpr int RS4 = seqs_w4_stride(Hp);
@@ -557,8 +557,7 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
         for (int k = 0; k < 7; ++k) out[k] = (float)tacc[k];
 #endif
     if constexpr (LOGP) {
-        const double t = block_sum_f64<kSeqsThreads>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<kSeqsThreads>(lpacc, partials, sums, B);
     }
 }
 
@@ -685,7 +684,7 @@ __global__ __launch_bounds__(64) void made_seqs_chunk_kernel(float* __restrict__
 }
 
 typedef void (*made_seqs_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int, float*,
-                                   double*, float);
+                                   double*, double*, float);
 
 template <int HT>
 made_seqs_kernel_t made_seqs_pick_ht(int variant, bool logp);

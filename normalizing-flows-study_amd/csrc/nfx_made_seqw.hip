@@ -28,8 +28,8 @@ static int seqw_waves(int64_t B) {
 }
 
 int made_seqw_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d, int H,
-                     int variant, int accumulate, float* logp, double* partials, bool fused, int* grid_out,
-                     hipStream_t s) {
+                     int variant, int accumulate, float* logp, double* partials, double* sums, bool fused,
+                     int* grid_out, hipStream_t s) {
     const int HT = (H + 31) / 32;
     const int nwv = seqw_waves(B);
     made_seqw_kernel_t k = HT == 1 ? seqw_pick<1>(variant, fused, nwv) : seqw_pick<2>(variant, fused, nwv);
@@ -39,7 +39,7 @@ int made_seqw_launch(const float* packed, const float* in, float* out, float* lo
     int64_t grid = (B + nwv - 1) / nwv;
     if (grid > kMaxPartials) grid = kMaxPartials;
     k<<<(unsigned)grid, (nwv + 1) * 64, lds, s>>>(packed, in, out, log_det, B, d, H, accumulate, logp, partials,
-                                           gauss_const(d));
+                                           sums, gauss_const(d));
     *grid_out = (int)grid;
     return check_launch("made_seqw_kernel");
 }

@@ -83,7 +83,7 @@ template <int HT, int VAR, bool LOGP, int NWV>
 __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int H, int accumulate, float* __restrict__ logp,
-    double* __restrict__ partials, float cgauss) {
+    double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr int Hp = 32 * HT;
     constexpr int UPL = Hp / 16;
     constexpr int NM = Hp / 16;  // rank groups of 16: h3r[4 m + c] = h3 of rank 16 m + 4 rq + c
@@ -427,12 +427,11 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
 #endif
     }
     if constexpr (LOGP) {
-        const double t = block_sum_f64<(NWV + 1) * 64>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<(NWV + 1) * 64>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*made_seqw_kernel_t)(const float*, const float*, float*, float*, int64_t, int, int, int, float*,
-                                   double*, float);
+                                   double*, double*, float);
 
 }  // namespace nfx

@@ -167,7 +167,7 @@ template <int HT, int VAR, bool LOGP, int NW>
 __global__ __launch_bounds__(64 * NW) void made_wide_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, int accumulate, int64_t nchunks,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     const MadeLayout L = made_layout(d, HT);
     constexpr int NT = 64 * NW;
     const WideLds S = wide_lds(L, HT, NW);
@@ -429,8 +429,7 @@ __global__ __launch_bounds__(64 * NW) void made_wide_kernel(
         }
     }
     if constexpr (LOGP) {
-        const double t = block_sum_f64<NT>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<NT>(lpacc, partials, sums, B);
     }
 }
 

@@ -146,10 +146,8 @@ static int spline_launch(const float* packed, const float* in, float* out, float
         if (gw > kMaxPartials) gw = kMaxPartials;
         double* pw = reinterpret_cast<double*>(workspace);
         k<<<gw, 64 * kSplineWideWaves, ldsw, stream>>>(packed, in, out, log_det, B, d, C, accumulate, ntiles, logp, pw,
-                                                        gauss_const(d));
-        int rcw = check_launch("spline_wide_kernel");
-        if (rcw || !fused) return rcw;
-        return gauss_finish(pw, gw, sums, B, stream);
+                                                        sums, gauss_const(d));
+        return check_launch("spline_wide_kernel");
     }
     const size_t lds = (size_t)spline_layout(HT, d).total * sizeof(float);
     int rc = prepare_lds((const void*)k, lds);
@@ -159,11 +157,9 @@ static int spline_launch(const float* packed, const float* in, float* out, float
     int grid = resident_grid((const void*)k, 256, lds, ((B + 31) / 32 + 3) / 4);
     if (grid > kMaxPartials) grid = kMaxPartials;
     double* partials = reinterpret_cast<double*>(workspace);
-    k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, d, C, accumulate, nchunks, logp, partials,
+    k<<<grid, 256, lds, stream>>>(packed, in, out, log_det, B, d, C, accumulate, nchunks, logp, partials, sums,
                                   gauss_const(d));
-    rc = check_launch("spline_coupling_kernel");
-    if (rc || !fused) return rc;
-    return gauss_finish(partials, grid, sums, B, stream);
+    return check_launch("spline_coupling_kernel");
 }
 
 extern "C" int nfx_spline_coupling(const float* packed, const float* in, float* out, float* log_det,

@@ -381,7 +381,7 @@ template <int HT, int K, int DIR, bool LOGP, int DS>
 __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coupling_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d_rt, SplineConsts C, int accumulate,
-    int64_t nchunks, float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    int64_t nchunks, float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
 #pragma clang fp contract(off)
     constexpr int DMAX = DS ? DS : 8;
     const int d = DS ? DS : d_rt;
@@ -610,13 +610,12 @@ __global__ __launch_bounds__(256, (DS == 2 && HT <= 2) ? 3 : 1) void spline_coup
     }
     if (half) unit(std::integral_constant<int, 1>{}, half_base, cur);
     if constexpr (LOGP) {
-        const double t = block_sum_f64<256>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<256>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*spline_kernel_t)(const float*, const float*, float*, float*, int64_t, int,
-                                SplineConsts, int, int64_t, float*, double*, float);
+                                SplineConsts, int, int64_t, float*, double*, double*, float);
 
 // DS = 0: runtime d <= 8; DS = 2: the d = 2 specialisation (nfx_spline_d2_h*.hip)
 template <int HT, int DS>
@@ -637,7 +636,7 @@ template <int HT, int K, int DIR, bool LOGP>
 __global__ __launch_bounds__(64 * kSplineWideWaves) void spline_wide_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, int d, SplineConsts C, int accumulate, int64_t ntiles,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
 #pragma clang fp contract(off)
     const SplineLayout L = spline_layout(HT, d);
     const int KS = spline_ks1(d);
@@ -760,8 +759,7 @@ __global__ __launch_bounds__(64 * kSplineWideWaves) void spline_wide_kernel(
         wave_lds_sync();
     }
     if constexpr (LOGP) {
-        const double tsum = block_sum_f64<64 * kSplineWideWaves>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+        logp_commit<64 * kSplineWideWaves>(lpacc, partials, sums, B);
     }
 }
 

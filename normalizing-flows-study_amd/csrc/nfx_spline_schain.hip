@@ -56,10 +56,8 @@ static int spline_chain_launch(const float* const* packs, int nl, const float* i
     if (rc) return rc;
     k<<<(unsigned)grid, 64 * kSplineSchainWaves, lds, s>>>(P, nl, in, out, log_det, B, C, accumulate, nchunks,
                                                             (int)slice, logp, reinterpret_cast<double*>(workspace),
-                                                            gauss_const(d));
-    rc = check_launch("spline_schain_kernel");
-    if (rc || !fused) return rc;
-    return gauss_finish(reinterpret_cast<double*>(workspace), (int)grid, sums, B, s);
+                                                            sums, gauss_const(d));
+    return check_launch("spline_schain_kernel");
 }
 
 }  // namespace nfx

@@ -22,7 +22,7 @@ template <int HT, int K, int DIR, bool LOGP, int NW>
 __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
     NfxChainPacks packs, int nl, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, SplineConsts C, int accumulate, int64_t nchunks, int slice_chunks,
-    float* __restrict__ logp, double* __restrict__ partials, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
 #pragma clang fp contract(off)
     constexpr int D = 2;
     constexpr SplineLayout L = spline_layout(HT, D);
@@ -132,13 +132,12 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
         __syncthreads();
     }
     if constexpr (LOGP) {
-        const double t = block_sum_f64<NTH>(lpacc);
-        if (threadIdx.x == 0) partials[blockIdx.x] = t;
+        logp_commit<NTH>(lpacc, partials, sums, B);
     }
 }
 
 typedef void (*spline_schain_t)(NfxChainPacks, int, const float*, float*, float*, int64_t, SplineConsts, int, int64_t,
-                                int, float*, double*, float);
+                                int, float*, double*, double*, float);
 
 constexpr int kSplineSchainWaves = 12;
 

@@ -219,9 +219,23 @@ class NormalizingFlowModel(nn.Module):
         return -(s[0] / s[1]).item()
 
 
+_GAUSS_WS = {}
+
+
 def gauss_workspace(B, device):
-    """Scratch for the per-workgroup float64 partial sums (nfx_gauss_workspace_bytes)."""
-    return torch.empty(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
+    """The per-workgroup float64 partial sums + arrival counter of the fused log_prob epilogues
+    (nfx_gauss_workspace_bytes): zero-filled once and cached per device — every launch's last
+    workgroup resets the counter, so the buffer stays valid call after call and inside captured
+    graphs. Launches are stream-ordered; callers running log_prob concurrently on two streams of
+    one device pass their own zero-filled workspace."""
+    dev = torch.device(device)
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    n = _lib.lib().nfx_gauss_workspace_bytes(B)
+    ws = _GAUSS_WS.get(key)
+    if ws is None or ws.numel() < n:
+        ws = torch.zeros(n, device=dev, dtype=torch.uint8)
+        _GAUSS_WS[key] = ws
+    return ws
 
 
 def gauss_logprob(z, ld, logp=None, sums=None, ws=None):

@@ -133,7 +133,7 @@ def test_fused_path_taken(cuda_device, kind):
     x = torch.randn(1000, d, device=cuda_device)
     with torch.no_grad():
         logp, sums = torch.empty(1000, device=cuda_device), torch.empty(2, device=cuda_device, dtype=torch.float64)
-        ws = torch.empty(1 << 16, device=cuda_device, dtype=torch.uint8)
+        ws = torch.zeros(1 << 16, device=cuda_device, dtype=torch.uint8)  # (zero-filled: logp_commit's counter)
         chain = getattr(m, "flow", m)  # RealNVP wraps a NormalizingFlowModel
         _, _, fused = chain._hip_chain(x, -1, logprob=(logp, sums, ws))
     assert fused == fused_expected
