@@ -519,36 +519,47 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         # pass (eager: ~20 us of Python + ctypes per layer), so an event pair brackets the kernel
         # itself, not the host's launch latency (which dominated short kernels: a 22 us layer read
         # 35 us without it).
+        # The spin kernel idles the chip, and its clocks drop with it: one untimed pass right after
+        # it brings the clocks back to the timed loop's steady state before the recorded pass (a
+        # compute-bound layer read 4% slower straight after the spin than in the timed loop).
         def preroll():
             torch.cuda._sleep(int(1.2e7 if training else 2e6))
         if coupling_train:
             from nfs_amd.flows import coupling as _cp
-            _cp.TRAIN_EVENTS = []
+            rec = []
             for _ in range(a.steps):
                 preroll()
+                _cp.TRAIN_EVENTS = None
+                step()
+                _cp.TRAIN_EVENTS = rec
                 step()
             torch.cuda.synchronize()
-            events = [e for e in _cp.TRAIN_EVENTS if e[0].endswith("<BWD2>")]
+            events = [e for e in rec if e[0].endswith("<BWD2>")]
             _cp.TRAIN_EVENTS = None
         elif training:
-            bwd_mod.BACKWARD_EVENTS = []
+            rec = []
             for _ in range(a.steps):
                 preroll()
+                bwd_mod.BACKWARD_EVENTS = None
+                step()
+                bwd_mod.BACKWARD_EVENTS = rec
                 step()
             torch.cuda.synchronize()
-            events = [e for e in bwd_mod.BACKWARD_EVENTS if e[0] != "made_wgrad_kernel"]
-            aux_events = [e for e in bwd_mod.BACKWARD_EVENTS if e[0] == "made_wgrad_kernel"]
+            events = [e for e in rec if e[0] != "made_wgrad_kernel"]
+            aux_events = [e for e in rec if e[0] == "made_wgrad_kernel"]
             bwd_mod.BACKWARD_EVENTS = None
         else:
-            flow.layer_events = []
+            rec = []
             for _ in range(a.steps):
                 preroll()
-                if sampling:
-                    flow.forward(x)
-                else:
-                    flow.log_prob(x, return_sums=True)
+                for r in (None, rec):
+                    flow.layer_events = r
+                    if sampling:
+                        flow.forward(x)
+                    else:
+                        flow.log_prob(x, return_sums=True)
             torch.cuda.synchronize()
-            events = flow.layer_events
+            events = rec
             flow.layer_events = None
     if torch_calls != 0 or (hip_calls == 0 and graphed is None and graphed_train is None):
         raise RuntimeError(f"hot path did not run on the HIP kernels: {nfs_amd.STATS}")

@@ -38,6 +38,9 @@ HOT = {
     "sample4k_spline": ("spline_coupling_kernel", "spline_schain_kernel"),
     "sample4k_maf": ("made_seqs_kernel", "made_seqw_kernel", "made_seq_kernel"),
     "sample4k_iaf": ("made_tile_kernel",),
+    "trainfig_iaf": ("made_seq_bwd_kernel", "made_seqw_bwd_kernel"),
+    "trainfig_maf": ("made_bwd_kernel",),
+    "trainfig_spline": ("spline_bwd_kernel",),
 }
 PER_PASS = ("gauss_finish_kernel",)  # once per log_prob pass besides the layer kernels
 
@@ -66,8 +69,7 @@ def _counter(path, counter):
 
 def reconcile(cdir, rtag):
     name = os.path.basename(cdir.rstrip("/"))
-    cfg = name.split("_")[0] if not name.startswith("sample4k") else "_".join(
-        p for p in name.split("_") if not p.isdigit())
+    cfg = "_".join(p for p in name.split("_") if not p.isdigit())  # cfg2_125000 -> cfg2
     with open(os.path.join(cdir, "bench.json")) as fh:
         bench = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
     ks_path = glob.glob(os.path.join(cdir, "trace", "*", "*_kernel_stats.csv"))[0]
