@@ -24,6 +24,7 @@ for spec0 in "$@"; do
   if [ -n "$b" ]; then extra=(--batch "$b"); fi
   if [ "$spec0" != "$spec" ]; then extra+=(--graph); fi
   d="$out/$name"
+  rm -rf "$d"
   mkdir -p "$d"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d/trace" -- \
     python3 "$root/bench.py" --config "$c" "${extra[@]}" --steps 20 --warmup 5 --no-cpu --no-secondary \

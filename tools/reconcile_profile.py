@@ -45,6 +45,12 @@ HOT = {
 PER_PASS = ("gauss_finish_kernel",)  # once per log_prob pass besides the layer kernels
 
 
+def _newest(pattern):
+    """The newest match (a re-profiled config leaves the previous run's pid-named files beside it)."""
+    m = glob.glob(pattern)
+    return max(m, key=os.path.getmtime) if m else None
+
+
 def _kernel_stats(path):
     out = {}
     with open(path) as fh:
@@ -72,16 +78,16 @@ def reconcile(cdir, rtag):
     cfg = "_".join(p for p in name.split("_") if not p.isdigit())  # cfg2_125000 -> cfg2
     with open(os.path.join(cdir, "bench.json")) as fh:
         bench = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
-    ks_path = glob.glob(os.path.join(cdir, "trace", "*", "*_kernel_stats.csv"))[0]
+    ks_path = _newest(os.path.join(cdir, "trace", "*", "*_kernel_stats.csv"))
     ks = _kernel_stats(ks_path)
     frags = HOT.get(cfg, ())
     rf = bench["roofline"]
     win = bench.get("timed_window_monotonic_ns")
-    tr = glob.glob(os.path.join(cdir, "trace", "*", "*_kernel_trace.csv"))
+    tr = _newest(os.path.join(cdir, "trace", "*", "*_kernel_trace.csv"))
     if win and tr:
         # exactly the kernels of the timed steps: dispatches inside the bench's timed window
         # (bench.py stamps it with time.monotonic_ns, the clock rocprofv3 stamps kernels with)
-        with open(tr[0]) as fh:
+        with open(tr) as fh:
             rows = [r for r in csv.DictReader(fh)
                     if int(r["Start_Timestamp"]) >= win[0] and int(r["End_Timestamp"]) <= win[1]]
         win_k = {}
@@ -126,17 +132,20 @@ def reconcile(cdir, rtag):
         "rocprof_ms_per_step": hot_ms + extra_ms,
         "fits_bench_step": hot_ms + extra_ms <= bench["ms_per_step"],
         "rocprof_achieved_tflops": ach, "rocprof_frac": ach / PEAK,
-        "event_frac": rf["frac"], "frac_rel_diff": abs(ach / PEAK - rf["frac"]) / rf["frac"],
+        # dense-count fracs on both sides (cfg4's headline frac is the executed one)
+        "event_frac": rf.get("frac_dense", rf["frac"]),
+        "frac_rel_diff": abs(ach / PEAK - rf.get("frac_dense", rf["frac"])) / rf.get("frac_dense", rf["frac"]),
         "source": {"kernel_stats": os.path.relpath(ks_path, ROOT),
                    "bench": os.path.relpath(os.path.join(cdir, "bench.json"), ROOT)},
     }
     if rf.get("frac_executed"):
         fe = rf["flop_per_sample_executed"]
         res["rocprof_frac_executed"] = fe * spl / (mean_us * 1e-6) / 1e12 / PEAK
-    fetch = glob.glob(os.path.join(cdir, "fetch", "*", "*counter_collection.csv"))
-    write = glob.glob(os.path.join(cdir, "write", "*", "*counter_collection.csv"))
+        res["event_frac_executed"] = rf["frac_executed"]
+    fetch = _newest(os.path.join(cdir, "fetch", "*", "*counter_collection.csv"))
+    write = _newest(os.path.join(cdir, "write", "*", "*counter_collection.csv"))
     if fetch and write:
-        fv, wv = _counter(fetch[0], "FETCH_SIZE"), _counter(write[0], "WRITE_SIZE")
+        fv, wv = _counter(fetch, "FETCH_SIZE"), _counter(write, "WRITE_SIZE")
         fs = [v for k, vs in fv.items() if k in hot for v in vs]
         ws = [v for k, vs in wv.items() if k in hot for v in vs]
         if fs and ws:
