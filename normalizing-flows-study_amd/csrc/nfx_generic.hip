@@ -19,6 +19,7 @@
 // tile's MFMAs. The weight gradient contracts over the batch: split-K over workgroups into a
 // [split][M][N] float workspace summed in a fixed order (deterministic, no atomics).
 #include <cstdlib>
+#include <type_traits>
 
 #include "nfx_common.h"
 #include "nfx_rqs_unit.h"           // rqs_unit_eval, rqs_unit_adjoint (ARQS)
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 // the same sums.
 constexpr int kG2M = 128, kG2K = 16, kG2RS = 12;
 
-template <int TA, int TB, bool VA, bool VB, int BN>
+template <int TA, int TB, bool VA, bool VB, int BN, bool EXTRA>
 __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
     constexpr int NJ = BN / 64;                 // 32-column tiles per wave
     constexpr int ASZ = 2 * kG2M * kG2RS;       // floats of one A stage
@@ -226,82 +227,141 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(16))) float sm[2 * (ASZ + BSZ)];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, h = lane >> 5, col = lane & 31;
     const int wm = wave >> 1, wn = wave & 1;
-    const int64_t m0 = (int64_t)blockIdx.x * kG2M, n0 = (int64_t)blockIdx.y * BN;
+    // XCD-aware tile order: workgroup b runs on XCD b % 8, so the bijective remap gives each XCD a
+    // contiguous run of tile ids, and tile ids walk the N tiles of one 128-row band first: the
+    // workgroups that share an A band share that XCD's L2 (A is read once from HBM, not N/BN times).
+    const int64_t gmt = (g.M + kG2M - 1) / kG2M, gnt = (g.N + BN - 1) / BN, nwg = gmt * gnt;
+    const int64_t bx = blockIdx.x, xcd = bx % 8, q8 = nwg / 8, r8 = nwg % 8;
+    const int64_t wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bx / 8;
+    const int64_t m0 = (wgid / gnt) * kG2M, n0 = (wgid % gnt) * BN;
     const int64_t kb = (int64_t)blockIdx.z * g.kchunk;
     const int64_t ke = kb + g.kchunk < g.K ? kb + g.kchunk : g.K;
-    // A tile: 128 x 16 = 512 float4 -> 2 per thread; B tile: BN x 16 -> BN / 64 per thread
-    constexpr int NA = 2, NB = BN / 64;
-    float ra[NA][4], rb[NB][4];
+    // Operand tiles: 128 x 16 (A) and BN x 16 (B) floats per K tile. A k-contiguous operand (A with
+    // TA = 0, B with TB = 1) is read as float4s along k by all 256 threads (2 resp. BN / 64 each) and
+    // parked as float2 pairs. A k-major operand (A with TA = 1, B with TB = 0: rows are k) is read as
+    // float4s along its row index by R threads (R = its tile rows), each taking the 4 same-parity
+    // rows k = 8 sq + 2 j + h (j = 0..3) of one 4-wide column group: a 4 x 4 register transpose then
+    // gives 4 consecutive s of one row, parked with ONE 16-byte store per row (the old per-element
+    // transposed stores hit 4 banks per 32 lanes: 8-way conflicts on the weight-gradient's park).
+    constexpr bool AKM = TA == 1, BKM = TB == 0;
+    constexpr int NA = AKM ? 4 : 2, NB = BKM ? 4 : BN / 64;
+    float ra[NA][4], rb_own[(AKM && BKM) ? 1 : NB][4];
+    // both k-major: a thread stages A or B, never both, so they share one register set
+    auto& rb = [&]() -> auto& {
+        if constexpr (AKM && BKM) return ra;
+        else return rb_own;
+    }();
+    // k-major roles: A on threads [0, 128), B on threads [128, 128 + BN) when both are k-major,
+    // else the k-major operand on threads [0, R)
+    constexpr int BKM0 = AKM ? 128 : 0;
+    const bool a_role = !AKM || t < 128;
+    const bool b_role = !BKM || (t >= BKM0 && t < BKM0 + BN);
     auto ld4 = [](const float* p, const float* msk, int64_t r, int64_t c, int64_t ld, int64_t rmax, int64_t cmax,
                   bool vec, float (&o)[4]) {
         if (vec && r < rmax && c + 3 < cmax) {
             f32x4 v = *reinterpret_cast<const f32x4*>(p + r * ld + c);
-            if (msk) v *= *reinterpret_cast<const f32x4*>(msk + r * ld + c);
+            if (EXTRA && msk) v *= *reinterpret_cast<const f32x4*>(msk + r * ld + c);
             o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const bool ok = r < rmax && c + q < cmax;
-                o[q] = ok ? p[r * ld + c + q] * (msk ? msk[r * ld + c + q] : 1.f) : 0.f;
+                o[q] = ok ? p[r * ld + c + q] * (EXTRA && msk ? msk[r * ld + c + q] : 1.f) : 0.f;
             }
         }
     };
-    // A: TA = 0 -> thread q owns row m = q >> 2, k = 4 (q & 3) .. +3; TA = 1 -> row k = q >> 5, m = 4 (q & 31) .. +3
-    auto load = [&](int64_t k0) {
+    // unguarded float4 (interior tiles of a plain GEMM: no bounds, no scales, no branches)
+    auto ldf = [](const float* p, int64_t r, int64_t c, int64_t ld, float (&o)[4]) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(p + r * ld + c);
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+    };
+    auto load = [&](int64_t k0, auto fast) {
+        constexpr bool F = decltype(fast)::value;
+        if constexpr (AKM) {  // A(m, k) = a[k * lda + m]; thread u: column group mq, parity h, half sq
+            if (a_role) {
+                const int u = t, mq = u & 31, h2 = (u >> 5) & 1, sq = u >> 6;
 #pragma unroll
-        for (int e = 0; e < NA; ++e) {
-            const int q = e * 256 + t;
-            if (TA == 0) {
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t k = k0 + 8 * sq + 2 * j + h2, m = m0 + 4 * mq;
+                    if constexpr (F) {
+                        ldf(g.a, k, m, g.lda, ra[j]);
+                    } else {
+                        ld4(g.a, nullptr, k, m, g.lda, ke, g.M, VA, ra[j]);
+                        if (EXTRA && g.kscale && k < ke)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) ra[j][c] *= g.kscale[k];
+                    }
+                }
+            }
+        } else {  // thread q owns row m = q >> 2, k = 4 (q & 3) .. +3
+#pragma unroll
+            for (int e = 0; e < NA; ++e) {
+                const int q = e * 256 + t;
                 const int64_t m = m0 + (q >> 2), k = k0 + (q & 3) * 4;
-                ld4(g.a, nullptr, m, k, g.lda, g.M, ke, VA, ra[e]);
-                if (g.kscale)
+                if constexpr (F) {
+                    ldf(g.a, m, k, g.lda, ra[e]);
+                } else {
+                    ld4(g.a, nullptr, m, k, g.lda, g.M, ke, VA, ra[e]);
+                    if (EXTRA && g.kscale)
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) ra[e][c] *= (k + c < ke) ? g.kscale[k + c] : 0.f;
-            } else {
-                const int64_t k = k0 + (q >> 5), m = m0 + (q & 31) * 4;
-                ld4(g.a, nullptr, k, m, g.lda, ke, g.M, VA, ra[e]);
-                if (g.kscale && k < ke)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) ra[e][c] *= g.kscale[k];
+                        for (int c = 0; c < 4; ++c) ra[e][c] *= (k + c < ke) ? g.kscale[k + c] : 0.f;
+                }
             }
         }
+        if constexpr (BKM) {  // B(k, n) = b[k * ldb + n]
+            if (b_role) {
+                const int u = t - BKM0, nq = u % (BN / 4), h2 = (u / (BN / 4)) & 1, sq = u / (BN / 2);
 #pragma unroll
-        for (int e = 0; e < NB; ++e) {
-            const int q = e * 256 + t;
-            if (TB == 1) {  // k contiguous: row n, 4 k's
-                ld4(g.b, g.bmask, n0 + (q >> 2), k0 + (q & 3) * 4, g.ldb, g.N, ke, VB, rb[e]);
-            } else {        // n contiguous: row k, 4 n's
-                ld4(g.b, g.bmask, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, g.ldb, ke, g.N, VB, rb[e]);
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t k = k0 + 8 * sq + 2 * j + h2, n = n0 + 4 * nq;
+                    if constexpr (F) ldf(g.b, k, n, g.ldb, rb[j]);
+                    else ld4(g.b, g.bmask, k, n, g.ldb, ke, g.N, VB, rb[j]);
+                }
+            }
+        } else {  // k contiguous: row n, 4 k's
+#pragma unroll
+            for (int e = 0; e < NB; ++e) {
+                const int q = e * 256 + t;
+                if constexpr (F) ldf(g.b, n0 + (q >> 2), k0 + (q & 3) * 4, g.ldb, rb[e]);
+                else ld4(g.b, g.bmask, n0 + (q >> 2), k0 + (q & 3) * 4, g.ldb, g.N, ke, VB, rb[e]);
             }
         }
     };
     auto park = [&](int buf) {
         float* As = sm + buf * (ASZ + BSZ);
         float* Bs = As + ASZ;
+        if constexpr (AKM) {
+            if (a_role) {
+                const int u = t, mq = u & 31, h2 = (u >> 5) & 1, sq = u >> 6;
 #pragma unroll
-        for (int e = 0; e < NA; ++e) {
-            const int q = e * 256 + t;
-            if (TA == 0) {  // k = 4 (q & 3) + c -> (h = c & 1, s = 2 (q & 3) + (c >> 1))
+                for (int c = 0; c < 4; ++c)
+                    *reinterpret_cast<f32x4*>(As + (h2 * kG2M + 4 * mq + c) * kG2RS + 4 * sq) =
+                        f32x4{ra[0][c], ra[1][c], ra[2][c], ra[3][c]};
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < NA; ++e) {  // k = 4 (q & 3) + c -> (h = c & 1, s = 2 (q & 3) + (c >> 1))
+                const int q = e * 256 + t;
                 const int m = q >> 2, s0 = 2 * (q & 3);
                 *reinterpret_cast<f32x2*>(As + (0 * kG2M + m) * kG2RS + s0) = f32x2{ra[e][0], ra[e][2]};
                 *reinterpret_cast<f32x2*>(As + (1 * kG2M + m) * kG2RS + s0) = f32x2{ra[e][1], ra[e][3]};
-            } else {
-                const int k = q >> 5, m = (q & 31) * 4;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) As[((k & 1) * kG2M + m + c) * kG2RS + (k >> 1)] = ra[e][c];
             }
         }
+        if constexpr (BKM) {
+            if (b_role) {
+                const int u = t - BKM0, nq = u % (BN / 4), h2 = (u / (BN / 4)) & 1, sq = u / (BN / 2);
 #pragma unroll
-        for (int e = 0; e < NB; ++e) {
-            const int q = e * 256 + t;
-            if (TB == 1) {
+                for (int c = 0; c < 4; ++c)
+                    *reinterpret_cast<f32x4*>(Bs + (h2 * BN + 4 * nq + c) * kG2RS + 4 * sq) =
+                        f32x4{rb[0][c], rb[1][c], rb[2][c], rb[3][c]};
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < NB; ++e) {
+                const int q = e * 256 + t;
                 const int n = q >> 2, s0 = 2 * (q & 3);
                 *reinterpret_cast<f32x2*>(Bs + (0 * BN + n) * kG2RS + s0) = f32x2{rb[e][0], rb[e][2]};
                 *reinterpret_cast<f32x2*>(Bs + (1 * BN + n) * kG2RS + s0) = f32x2{rb[e][1], rb[e][3]};
-            } else {
-                const int k = q / (BN / 4), n = (q % (BN / 4)) * 4;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) Bs[((k & 1) * BN + n + c) * kG2RS + (k >> 1)] = rb[e][c];
             }
         }
     };
@@ -310,37 +370,43 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
-    int buf = 0;
-    if (kb < ke) {
-        load(kb);
-        park(0);
-    }
-    __syncthreads();
-    for (int64_t k0 = kb; k0 < ke; k0 += kG2K) {
-        const bool more = k0 + kG2K < ke;
-        if (more) load(k0 + kG2K);  // in flight during this tile's MFMAs
-        const float* As = sm + buf * (ASZ + BSZ);
-        const float* Bs = As + ASZ;
+    auto kloop = [&](auto fast) {
+        int buf = 0;
+        if (kb < ke) {
+            load(kb, fast);
+            park(0);
+        }
+        __syncthreads();
+        for (int64_t k0 = kb; k0 < ke; k0 += kG2K) {
+            const bool more = k0 + kG2K < ke;
+            if (more) load(k0 + kG2K, fast);  // in flight during this tile's MFMAs
+            const float* As = sm + buf * (ASZ + BSZ);
+            const float* Bs = As + ASZ;
 #pragma unroll
-        for (int sh = 0; sh < 2; ++sh) {  // k-steps 4 sh .. 4 sh + 3
-            f32x4 fa[2], fb[NJ];
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-                fa[i] = *reinterpret_cast<const f32x4*>(As + (h * kG2M + wm * 64 + i * 32 + col) * kG2RS + 4 * sh);
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                fb[j] = *reinterpret_cast<const f32x4*>(Bs + (h * BN + wn * (BN / 2) + j * 32 + col) * kG2RS + 4 * sh);
-#pragma unroll
-            for (int ss = 0; ss < 4; ++ss)
+            for (int sh = 0; sh < 2; ++sh) {  // k-steps 4 sh .. 4 sh + 3
+                f32x4 fa[2], fb[NJ];
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
+                    fa[i] = *reinterpret_cast<const f32x4*>(As + (h * kG2M + wm * 64 + i * 32 + col) * kG2RS + 4 * sh);
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(fa[i][ss], fb[j][ss], acc[i][j]);
+                for (int j = 0; j < NJ; ++j)
+                    fb[j] = *reinterpret_cast<const f32x4*>(Bs + (h * BN + wn * (BN / 2) + j * 32 + col) * kG2RS + 4 * sh);
+#pragma unroll
+                for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma32(fa[i][ss], fb[j][ss], acc[i][j]);
+            }
+            if (more) park(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
         }
-        if (more) park(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-    }
+    };
+    // interior tile of a plain GEMM with whole K tiles: the branch-free loader
+    const bool inner = VA && VB && !EXTRA && m0 + kG2M <= g.M && n0 + BN <= g.N && (ke - kb) % kG2K == 0;
+    if (inner) kloop(std::true_type{});
+    else kloop(std::false_type{});
     float* c = g.c + (int64_t)blockIdx.z * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -377,22 +443,30 @@ static int gemm_tile_bn(int64_t M, int64_t N) {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+template <int TA, int TB, int BN, bool EXTRA>
+static void gemm2_go(const GemmArgs& g, dim3 grid, bool va, bool vb, hipStream_t s) {
+    if (va && vb) gemm2_kernel<TA, TB, true, true, BN, EXTRA><<<grid, 256, 0, s>>>(g);
+    else if (va) gemm2_kernel<TA, TB, true, false, BN, EXTRA><<<grid, 256, 0, s>>>(g);
+    else if (vb) gemm2_kernel<TA, TB, false, true, BN, EXTRA><<<grid, 256, 0, s>>>(g);
+    else gemm2_kernel<TA, TB, false, false, BN, EXTRA><<<grid, 256, 0, s>>>(g);
+}
+
 template <int TA, int TB>
 static void gemm_go(const GemmArgs& g, dim3 grid, int bn, hipStream_t s) {
     const bool va = g.lda % 4 == 0 && aligned16(g.a);
     const bool vb = g.ldb % 4 == 0 && aligned16(g.b) && (!g.bmask || aligned16(g.bmask));
-    if (bn == 128) {
-        if (va && vb) gemm2_kernel<TA, TB, true, true, 128><<<grid, 256, 0, s>>>(g);
-        else if (va) gemm2_kernel<TA, TB, true, false, 128><<<grid, 256, 0, s>>>(g);
-        else if (vb) gemm2_kernel<TA, TB, false, true, 128><<<grid, 256, 0, s>>>(g);
-        else gemm2_kernel<TA, TB, false, false, 128><<<grid, 256, 0, s>>>(g);
-        return;
-    }
-    if (bn == 64) {
-        if (va && vb) gemm2_kernel<TA, TB, true, true, 64><<<grid, 256, 0, s>>>(g);
-        else if (va) gemm2_kernel<TA, TB, true, false, 64><<<grid, 256, 0, s>>>(g);
-        else if (vb) gemm2_kernel<TA, TB, false, true, 64><<<grid, 256, 0, s>>>(g);
-        else gemm2_kernel<TA, TB, false, false, 64><<<grid, 256, 0, s>>>(g);
+    const bool extra = g.kscale || g.bmask;
+    if (bn) {
+        // one-dimensional grid of M x N tiles (the kernel orders them per XCD), split-K on z
+        const int64_t tiles = ((g.M + kG2M - 1) / kG2M) * ((g.N + bn - 1) / bn);
+        const dim3 g1((unsigned)tiles, 1, grid.z);
+        if (bn == 128) {
+            if (extra) gemm2_go<TA, TB, 128, true>(g, g1, va, vb, s);
+            else gemm2_go<TA, TB, 128, false>(g, g1, va, vb, s);
+        } else {
+            if (extra) gemm2_go<TA, TB, 64, true>(g, g1, va, vb, s);
+            else gemm2_go<TA, TB, 64, false>(g, g1, va, vb, s);
+        }
         return;
     }
     if (va && vb) gemm_kernel<TA, TB, true, true><<<grid, 256, 0, s>>>(g);
@@ -406,7 +480,7 @@ static int gemm_launch(const GemmArgs& g, int ta, int tb, int64_t splits, hipStr
     const int bn = gemm_tile_bn(g.M, g.N);
     const int64_t tm = bn ? kG2M : kGBM, tn = bn ? bn : kGBN;
     const int64_t gm = (g.M + tm - 1) / tm, gn = (g.N + tn - 1) / tn;
-    if (gm > 0x7fffffff || gn > 65535 || splits > 65535)
+    if (gm > 0x7fffffff || gn > 65535 || splits > 65535 || (bn && gm * gn > 0x7fffffff))
         return set_error(NFX_EUNSUPPORTED, "linear: grid %lld x %lld x %lld out of range", (long long)gm,
                          (long long)gn, (long long)splits);
     dim3 grid((unsigned)gm, (unsigned)gn, (unsigned)splits);
@@ -430,30 +504,69 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, int64_t nz, 
 }
 
 // Column sums of D [M][N] over row range z: part[z][n] (8 row groups x 32 columns per block,
-// the 8 group sums combined in a fixed order)
+// the 8 group sums combined in a fixed order). VEC: a lane sums 4 adjacent columns read as one
+// float4 (128 columns per block, N % 4 == 0 and D 16-byte aligned), 4 rows in flight per lane.
+template <bool VEC>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ d, int64_t M, int64_t N,
                                                      int64_t rchunk, float* __restrict__ part) {
-    __shared__ float red[8][33];
+    constexpr int W = VEC ? 4 : 1;
+    __shared__ float red[8][32 * W + 1];
     const int cx = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    const int64_t n = (int64_t)blockIdx.x * 32 + cx;
+    const int64_t n = ((int64_t)blockIdx.x * 32 + cx) * W;
     const int64_t rb = (int64_t)blockIdx.y * rchunk, re = rb + rchunk < M ? rb + rchunk : M;
-    float v = 0.f;
-    if (n < N)
-        for (int64_t m = rb + rg; m < re; m += 8) v += d[m * N + n];
-    red[rg][cx] = v;
-    __syncthreads();
-    if (rg == 0 && n < N) {
-        float s = 0.f;
-        for (int q = 0; q < 8; ++q) s += red[q][cx];
-        part[(int64_t)blockIdx.y * N + n] = s;
+    float v[W];
+#pragma unroll
+    for (int c = 0; c < W; ++c) v[c] = 0.f;
+    if (n < N) {
+        if constexpr (VEC) {
+            int64_t m = rb + rg;
+            for (; m + 24 < re; m += 32) {  // 4 rows in flight, summed in row order
+                f32x4 x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f32x4*>(d + (m + 8 * u) * N + n);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) v[c] += x[u][c];
+            }
+            for (; m < re; m += 8) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(d + m * N + n);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[c] += x[c];
+            }
+        } else {
+            for (int64_t m = rb + rg; m < re; m += 8) v[0] += d[m * N + n];
+        }
     }
+#pragma unroll
+    for (int c = 0; c < W; ++c) red[rg][cx * W + c] = v[c];
+    __syncthreads();
+    if (rg == 0) {
+#pragma unroll
+        for (int c = 0; c < W; ++c) {
+            if (n + c >= N) break;
+            float acc = 0.f;
+            for (int q = 0; q < 8; ++q) acc += red[q][cx * W + c];
+            part[(int64_t)blockIdx.y * N + n + c] = acc;
+        }
+    }
+}
+
+// row chunks of the bias-gradient column sum: ~1024 rows each (>= 4 waves per SIMD at the
+// batch sizes the generic path serves), at most 1024 chunks
+static int64_t colsum_chunks(int64_t M) {
+    const int64_t c = (M + 1023) / 1024;
+    return c < 1 ? 1 : (c > 1024 ? 1024 : c);
 }
 
 static int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) {
     const int bn = gemm_tile_bn(M, N);
     const int64_t tm = bn ? kG2M : kGBM, tn = bn ? bn : kGBN;
     const int64_t tiles = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
-    const int64_t want = (4 * (int64_t)num_cus() + tiles - 1) / tiles;
+    // one full round of resident workgroups (gemm2: 3 per CU at BN = 128, 4 at BN = 64, by LDS and
+    // VGPRs): a split count that leaves a partial second round idles most of the chip for it
+    const int64_t slots = (bn == 128 ? 3 : 4) * (int64_t)num_cus();
+    const int64_t want = tiles >= slots ? 1 : slots / tiles;
     const int64_t maxs = (K + 1023) / 1024;  // at least 1024 rows per split
     int64_t s = want < maxs ? want : maxs;
     if (s < 1) s = 1;
@@ -1197,7 +1310,7 @@ extern "C" size_t nfx_linear_workspace_bytes(int64_t M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0) return 0;
     if (K <= kThin || N <= kThin) return (size_t)(thin_splits(M, N, K) * (int64_t)N * (K + 1) * sizeof(float));
     const int64_t s = wgrad_splits(N, K, M);
-    const int64_t cs = (M + 4095) / 4096 < 1024 ? (M + 4095) / 4096 : 1024;
+    const int64_t cs = colsum_chunks(M);
     const int64_t a = s * (int64_t)N * K, b = (cs < 1 ? 1 : cs) * (int64_t)N;
     return (size_t)((a > b ? a : b) * sizeof(float));
 }
@@ -1251,12 +1364,13 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
     split_reduce_kernel<<<(unsigned)((NK + 255) / 256 < 4096 ? (NK + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, NK, gw, 0, wmask);
     rc = check_launch("split_reduce_kernel");
     if (rc || !gb) return rc;
-    int64_t cs = (M + 4095) / 4096;
-    if (cs > 1024) cs = 1024;
-    if (cs < 1) cs = 1;
+    const int64_t cs = colsum_chunks(M);
     const int64_t rchunk = (M + cs - 1) / cs;
     const int64_t ncs = (M + rchunk - 1) / rchunk;
-    colsum_kernel<<<dim3((unsigned)((N + 31) / 32), (unsigned)ncs), 256, 0, s>>>(gy, M, N, rchunk, ws);
+    if (N % 4 == 0 && aligned16(gy))
+        colsum_kernel<true><<<dim3((unsigned)((N + 127) / 128), (unsigned)ncs), 256, 0, s>>>(gy, M, N, rchunk, ws);
+    else
+        colsum_kernel<false><<<dim3((unsigned)((N + 31) / 32), (unsigned)ncs), 256, 0, s>>>(gy, M, N, rchunk, ws);
     rc = check_launch("colsum_kernel");
     if (rc) return rc;
     split_reduce_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(ws, ncs, N, gb, 0, nullptr);

@@ -39,6 +39,7 @@ def timed(fn, steps, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--gemm-only", action="store_true", help="only the GEMM cases (profiling runs)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -63,6 +64,10 @@ def main():
     # 2) whole layers beyond the fused families
     B = 262144
     cases = []
+    if a.gemm_only:
+        for o in out:
+            print(json.dumps(o), flush=True)
+        return
     m = nfs_amd.MaskedAutoregressiveFlow(63, 512).to(dev).eval()
     cases.append(("MAF(63,512) inverse (log-density direction), eval", m, B, -1, False))
     c = nfs_amd.CouplingLayer(2, 256, torch.tensor([1.0, 0.0])).to(dev).eval()
