@@ -45,6 +45,7 @@ struct GemmArgs {
     const float* nscale;     // optional, length N: C(m, n) *= nscale[n]
     int relu, accumulate;
     int64_t kchunk;          // split-K: workgroup z covers k in [z * kchunk, (z + 1) * kchunk)
+    float* asum;             // optional (gemm2, TA = 1): asum[z * M + m] = sum over the z slice's k of A(m, k)
 };
 
 // VA / VB: the operand's contiguous index is 16-byte aligned (ld % 4 == 0, aligned base): tiles
@@ -217,10 +218,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 // loads are in flight during the current tile's MFMAs and are parked into the other buffer after
 // them, one barrier per K tile. The k-steps run in increasing k like gemm_kernel's, so both produce
 // the same sums.
-constexpr int kG2M = 128, kG2K = 16, kG2RS = 12;
+constexpr int kG2M = 128, kG2K = 16, kG2RS = 8;
+// LDS float offset of 16-byte chunk `ch` (0/1: s = 4 ch .. 4 ch + 3) of operand row `row`: rows of 8
+// floats, chunks swapped on odd 8-row groups, so the 16 rows of a ds_read_b128 lane group
+// ({0-3, 12-15, 20-27} + base) land on 16 different 16-byte bank slots
+__device__ __forceinline__ int g2_off(int row, int ch) { return row * kG2RS + 4 * (ch ^ ((row >> 3) & 1)); }
 
-template <int TA, int TB, bool VA, bool VB, int BN, bool EXTRA>
-__global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
+template <int TA, int TB, bool VA, bool VB, int BN, bool EXTRA, int WPE = (TA == 0 && TB == 1) ? 4 : 3>
+__global__ __launch_bounds__(256, WPE) void gemm2_kernel(GemmArgs g) {
     constexpr int NJ = BN / 64;                 // 32-column tiles per wave
     constexpr int ASZ = 2 * kG2M * kG2RS;       // floats of one A stage
     constexpr int BSZ = 2 * BN * kG2RS;
@@ -327,6 +332,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
             }
         }
     };
+    float asv[4] = {0.f, 0.f, 0.f, 0.f};  // row sums of A (TA = 1, g.asum): columns m0 + 4 mq + c
     auto park = [&](int buf) {
         float* As = sm + buf * (ASZ + BSZ);
         float* Bs = As + ASZ;
@@ -335,16 +341,21 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
                 const int u = t, mq = u & 31, h2 = (u >> 5) & 1, sq = u >> 6;
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    *reinterpret_cast<f32x4*>(As + (h2 * kG2M + 4 * mq + c) * kG2RS + 4 * sq) =
+                    *reinterpret_cast<f32x4*>(As + g2_off(h2 * kG2M + 4 * mq + c, sq)) =
                         f32x4{ra[0][c], ra[1][c], ra[2][c], ra[3][c]};
+                if (g.asum)  // the bias gradient: this thread's 4 rows, in row order
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) asv[c] += ra[j][c];
             }
         } else {
 #pragma unroll
             for (int e = 0; e < NA; ++e) {  // k = 4 (q & 3) + c -> (h = c & 1, s = 2 (q & 3) + (c >> 1))
                 const int q = e * 256 + t;
                 const int m = q >> 2, s0 = 2 * (q & 3);
-                *reinterpret_cast<f32x2*>(As + (0 * kG2M + m) * kG2RS + s0) = f32x2{ra[e][0], ra[e][2]};
-                *reinterpret_cast<f32x2*>(As + (1 * kG2M + m) * kG2RS + s0) = f32x2{ra[e][1], ra[e][3]};
+                *reinterpret_cast<f32x2*>(As + g2_off(0 * kG2M + m, s0 >> 2) + (s0 & 3)) = f32x2{ra[e][0], ra[e][2]};
+                *reinterpret_cast<f32x2*>(As + g2_off(1 * kG2M + m, s0 >> 2) + (s0 & 3)) = f32x2{ra[e][1], ra[e][3]};
             }
         }
         if constexpr (BKM) {
@@ -352,7 +363,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
                 const int u = t - BKM0, nq = u % (BN / 4), h2 = (u / (BN / 4)) & 1, sq = u / (BN / 2);
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    *reinterpret_cast<f32x4*>(Bs + (h2 * BN + 4 * nq + c) * kG2RS + 4 * sq) =
+                    *reinterpret_cast<f32x4*>(Bs + g2_off(h2 * BN + 4 * nq + c, sq)) =
                         f32x4{rb[0][c], rb[1][c], rb[2][c], rb[3][c]};
             }
         } else {
@@ -360,8 +371,8 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
             for (int e = 0; e < NB; ++e) {
                 const int q = e * 256 + t;
                 const int n = q >> 2, s0 = 2 * (q & 3);
-                *reinterpret_cast<f32x2*>(Bs + (0 * BN + n) * kG2RS + s0) = f32x2{rb[e][0], rb[e][2]};
-                *reinterpret_cast<f32x2*>(Bs + (1 * BN + n) * kG2RS + s0) = f32x2{rb[e][1], rb[e][3]};
+                *reinterpret_cast<f32x2*>(Bs + g2_off(0 * BN + n, s0 >> 2) + (s0 & 3)) = f32x2{rb[e][0], rb[e][2]};
+                *reinterpret_cast<f32x2*>(Bs + g2_off(1 * BN + n, s0 >> 2) + (s0 & 3)) = f32x2{rb[e][1], rb[e][3]};
             }
         }
     };
@@ -387,10 +398,10 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
                 f32x4 fa[2], fb[NJ];
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
-                    fa[i] = *reinterpret_cast<const f32x4*>(As + (h * kG2M + wm * 64 + i * 32 + col) * kG2RS + 4 * sh);
+                    fa[i] = *reinterpret_cast<const f32x4*>(As + g2_off(h * kG2M + wm * 64 + i * 32 + col, sh));
 #pragma unroll
                 for (int j = 0; j < NJ; ++j)
-                    fb[j] = *reinterpret_cast<const f32x4*>(Bs + (h * BN + wn * (BN / 2) + j * 32 + col) * kG2RS + 4 * sh);
+                    fb[j] = *reinterpret_cast<const f32x4*>(Bs + g2_off(h * BN + wn * (BN / 2) + j * 32 + col, sh));
 #pragma unroll
                 for (int ss = 0; ss < 4; ++ss)
 #pragma unroll
@@ -407,7 +418,37 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
     const bool inner = VA && VB && !EXTRA && m0 + kG2M <= g.M && n0 + BN <= g.N && (ke - kb) % kG2K == 0;
     if (inner) kloop(std::true_type{});
     else kloop(std::false_type{});
+    if constexpr (AKM) {
+        // the A row sums of this K slice, once per 128-row band (the N-tile-0 workgroup): the 4
+        // (parity, half) thread groups combined in a fixed order through LDS
+        if (g.asum && n0 == 0) {
+            float* red = sm;  // the last tile's barrier has retired every read of the stages
+            if (a_role) {
+                const int u = t, mq = u & 31, grp = u >> 5;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) red[grp * kG2M + 4 * mq + c] = asv[c];
+            }
+            __syncthreads();
+            if (t < kG2M && m0 + t < g.M) {
+                // groups (h, sq) = 0: rows 8 sq + 2 j + h; summed in group order
+                const float v = ((red[t] + red[kG2M + t]) + red[2 * kG2M + t]) + red[3 * kG2M + t];
+                g.asum[(int64_t)blockIdx.z * g.M + m0 + t] = v;
+            }
+        }
+    }
     float* c = g.c + (int64_t)blockIdx.z * g.M * g.N;
+    // per-column epilogue constants, read once per column (the output stores could alias them, so
+    // the compiler would re-read them after every store)
+    float cb[NJ], cs[NJ], ch[NJ], cn[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int64_t n = n0 + wn * (BN / 2) + j * 32 + col;
+        const bool ok = n < g.N;
+        cb[j] = g.bias && ok ? g.bias[n] : 0.f;
+        cs[j] = g.pscale && ok ? g.pscale[n] : 1.f;
+        ch[j] = g.pshift && ok ? g.pshift[n] : 0.f;
+        cn[j] = g.nscale && ok ? g.nscale[n] : 1.f;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -417,11 +458,11 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmArgs g) {
                 const int64_t m = m0 + wm * 64 + i * 32 + crow(r, h), n = n0 + wn * (BN / 2) + j * 32 + col;
                 if (m < g.M && n < g.N) {
                     float v = acc[i][j][r];
-                    if (g.bias) v += g.bias[n];
-                    if (g.pscale) v = v * g.pscale[n] + g.pshift[n];
+                    if (g.bias) v += cb[j];
+                    if (g.pscale) v = v * cs[j] + ch[j];
                     if (g.relu) v = trelu(v);
                     if (g.act) v = g.act[m * g.ldact + n] > 0.f ? v : 0.f;
-                    if (g.nscale) v *= g.nscale[n];
+                    if (g.nscale) v *= cn[j];
                     float* p = c + m * g.ldc + n;
                     if (g.accumulate) v += *p;
                     *p = v;
@@ -445,6 +486,17 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <int TA, int TB, int BN, bool EXTRA>
 static void gemm2_go(const GemmArgs& g, dim3 grid, bool va, bool vb, hipStream_t s) {
+    // $NFX_GEMM_WPE=3: the forward layout at 3 waves per SIMD instead of 4 (A/B measurements)
+    static const int wpe = [] {
+        const char* e = getenv("NFX_GEMM_WPE");
+        return e ? atoi(e) : 0;
+    }();
+    if constexpr (TA == 0 && TB == 1 && !EXTRA) {
+        if (wpe == 3 && va && vb) {
+            gemm2_kernel<TA, TB, true, true, BN, EXTRA, 3><<<grid, 256, 0, s>>>(g);
+            return;
+        }
+    }
     if (va && vb) gemm2_kernel<TA, TB, true, true, BN, EXTRA><<<grid, 256, 0, s>>>(g);
     else if (va) gemm2_kernel<TA, TB, true, false, BN, EXTRA><<<grid, 256, 0, s>>>(g);
     else if (vb) gemm2_kernel<TA, TB, false, true, BN, EXTRA><<<grid, 256, 0, s>>>(g);
@@ -1311,7 +1363,8 @@ extern "C" size_t nfx_linear_workspace_bytes(int64_t M, int N, int K) {
     if (K <= kThin || N <= kThin) return (size_t)(thin_splits(M, N, K) * (int64_t)N * (K + 1) * sizeof(float));
     const int64_t s = wgrad_splits(N, K, M);
     const int64_t cs = colsum_chunks(M);
-    const int64_t a = s * (int64_t)N * K, b = (cs < 1 ? 1 : cs) * (int64_t)N;
+    // the large-tile GEMM also writes the bias partials [s][N] beside the weight partials
+    const int64_t a = s * (int64_t)N * K + (gemm_tile_bn(N, K) ? s * (int64_t)N : 0), b = (cs < 1 ? 1 : cs) * (int64_t)N;
     return (size_t)((a > b ? a : b) * sizeof(float));
 }
 
@@ -1359,11 +1412,18 @@ extern "C" int nfx_linear_backward_weight(const float* gy, const float* x, const
     g.kchunk = kchunk;
     // x * in_scale applies to B's n index here (the input features): scale after the sum
     g.nscale = in_scale;
+    // the large-tile GEMM sums gy's columns (the bias gradient) from the tiles it stages anyway
+    const bool fused_bias = gb && gemm_tile_bn(N, K);
+    if (fused_bias) g.asum = ws + nz * NK;
     int rc = gemm_launch(g, 1, 0, nz, s);
     if (rc) return rc;
     split_reduce_kernel<<<(unsigned)((NK + 255) / 256 < 4096 ? (NK + 255) / 256 : 4096), 256, 0, s>>>(ws, nz, NK, gw, 0, wmask);
     rc = check_launch("split_reduce_kernel");
     if (rc || !gb) return rc;
+    if (fused_bias) {
+        split_reduce_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(g.asum, nz, N, gb, 0, nullptr);
+        return check_launch("split_reduce_kernel");
+    }
     const int64_t cs = colsum_chunks(M);
     const int64_t rchunk = (M + cs - 1) / cs;
     const int64_t ncs = (M + rchunk - 1) / rchunk;

@@ -1,6 +1,6 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT/gpurun_out/r04f
+R=$GRAFT_REPO_ROOT/gpurun_out/${1:-gemmprof}
 mkdir -p $R
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/trace -- python3 $GRAFT_REPO_ROOT/tools/generic_bench.py --gemm-only > $R/bench.jsonl 2> $R/trace.err || exit $?
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU --output-format csv -d $R/pmc1 -- python3 $GRAFT_REPO_ROOT/tools/generic_bench.py --gemm-only --steps 2 > $R/pmc1.log 2>&1 || exit $?
