@@ -40,12 +40,14 @@ namespace nfx {
 
 constexpr int kSeqsWaves = 8;  // compute waves per workgroup (4 samples each)
 // + one staging wave that issues the blocks' LDS-DMA (else the compute waves share it)
-constexpr bool kSeqsStager = true;
+constexpr bool kSeqsStager = true;  // required: the staging wave also owns the block sums
 constexpr int kSeqsThreads = 64 * (kSeqsWaves + (kSeqsStager ? 1 : 0));
 constexpr int kSeqsStep = 64;  // steps per staged block
 constexpr int kSeqsH3 = 68;  // per-sample h3 row (by rank, Hp <= 64) + 4 pad floats
-// per wave: x, z, alpha block tiles; h3 rows; 64 floats where the lanes past a chunk store
-constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * kSeqsH3 + 64;
+// per wave: the x block tile; z and alpha block tiles, double-buffered (the staging wave sums and
+// stores block k while the wave computes block k + 1); h3 rows; 64 floats where the lanes past a
+// chunk store
+constexpr int kSeqsTile = 4 * kSeqsStep + 2 * 2 * 4 * kSeqsStep + 4 * kSeqsH3 + 64;
 
 // seqs_w4_stride (nfx_made_kernel.h): row stride of the interleaved (mu, alpha) W4 block rows,
 // 2 Hp + 4, so that the 16 lanes of a row group, reading the same 16-byte column of 16
@@ -53,8 +55,8 @@ constexpr int kSeqsTile = 3 * 4 * kSeqsStep + 4 * kSeqsH3 + 64;
 static_assert(kSeqsPadRows == kSeqsStep, "a staged block is copied whole from the padded rows");
 
 struct SeqsLds {
-    int w2, w3, tab;                                   // rank-ordered image in global memory
-    int b1, b2, b3, deg, gend, blk, blkf, wv, total;  // LDS
+    int w2, w3, tab;                                         // rank-ordered image in global memory
+    int b1, b2, b3, deg, gend, tabn, wv, blk, blkf, total;  // LDS
 };
 
 // Rank-ordered image in global memory (P + L.rimg, built at pack time by made_seqs_image_kernel):
@@ -62,8 +64,9 @@ struct SeqsLds {
 // pos(p) = (p % 16) * UPL + p / 16: lane sub's slots k = 0..UPL-1 are contiguous), then the
 // tables (b1 by position; b2, b3, degree, group end by rank). The completion chain reads its W2 /
 // W3 rows from there (L2-resident, issued at the chunk start).
-// LDS (floats): the tables | two staged blocks: w1t [64][Hp] by position | w4 [64][Hp][mu, alpha]
-// by RANK (+4 pad floats per row) | b4 [mu 64 | alpha 64] | per-wave tiles.
+// LDS (floats): the tables | per-wave tiles (low addresses, so every tile access is a base VGPR +
+// immediate offset) | two staged blocks: w1t [64][Hp] by position | w4 [64][Hp][mu, alpha] by RANK
+// (+4 pad floats per row) | b4 [mu 64 | alpha 64].
 __host__ __device__ inline SeqsLds seqs_lds(int Hp) {
     SeqsLds S{};
     S.w2 = 0;
@@ -75,8 +78,9 @@ __host__ __device__ inline SeqsLds seqs_lds(int Hp) {
     S.b3 = o; o += Hp;    // by rank
     S.deg = o; o += Hp;   // degree by rank (padded units 1e9)
     S.gend = o; o += Hp;  // first rank after rank p's degree group
-    S.blk = o; S.blkf = kSeqsStep * Hp + kSeqsStep * seqs_w4_stride(Hp) + 2 * kSeqsStep; o += 2 * S.blkf;
+    S.tabn = o;
     S.wv = o; o += kSeqsWaves * kSeqsTile;
+    S.blk = o; S.blkf = kSeqsStep * Hp + kSeqsStep * seqs_w4_stride(Hp) + 2 * kSeqsStep; o += 2 * S.blkf;
     S.total = o;
     return S;
 }
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
     const float* img = P + L.rimg;
     {
         const f32x4* src = reinterpret_cast<const f32x4*>(img + S.tab);
-        for (int i = threadIdx.x; i < S.blk / 4; i += kSeqsThreads) lds4[i] = src[i];
+        for (int i = threadIdx.x; i < S.tabn / 4; i += kSeqsThreads) lds4[i] = src[i];
     }
     __syncthreads();
     // Per-rank tables held one entry per lane (Hp <= 64) and read with v_readlane at a uniform
@@ -249,10 +253,12 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
     const int degv = (int)lds[S.deg + tl];
     const int b2v = __float_as_int(lds[S.b2 + tl]);
     const int b3v = __float_as_int(lds[S.b3 + tl]);
-    float* xin_t = lds + S.wv + wave * kSeqsTile;  // [4][64] inputs of the block
-    float* zout_t = xin_t + 4 * kSeqsStep;         // [4][64] guarded outputs of the block
-    float* at_t = zout_t + 4 * kSeqsStep;          // [4][64] clamped alphas of the block
-    float* h3_t = at_t + 4 * kSeqsStep;            // [4][kSeqsH3] h3 by rank (0 until complete)
+    // compute wave w's tiles; the staging wave reads every wave's z / alpha tiles
+    auto wtile = [&](int w) { return lds + S.wv + w * kSeqsTile; };
+    float* xin_t = wtile(wave);                     // [4][64] inputs of the block
+    float* zt2 = xin_t + 4 * kSeqsStep;             // [2][4][64] guarded outputs of the block (by parity)
+    float* at2 = zt2 + 2 * 4 * kSeqsStep;           // [2][4][64] clamped alphas of the block (by parity)
+    float* h3_t = at2 + 2 * 4 * kSeqsStep;          // [4][kSeqsH3] h3 by rank (0 until complete)
     // Staged blocks end where a segment ends (after the step of a completion degree) whenever a
     // segment boundary falls within kSeqsStep steps, so that no chunk is cut by a block boundary
     // (at cfg5i: 65 chunks per sample instead of 77). Block [i0, blk_end(i0)), uniform.
@@ -309,11 +315,38 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
 #else
 #define NFX_TMARK(k) do { } while (0)
 #endif
+    static_assert(kSeqsStager, "the staging wave sums the blocks and writes the results");
     double lpacc = 0.0;
-    if (kSeqsStager && wave == kSeqsWaves) {
-        // staging wave: the LDS-DMA of every block (the compute waves never wait for it)
+    if (wave == kSeqsWaves) {
+        // staging wave: the LDS-DMA of every block, and — one block behind the compute waves — the
+        // block's log-det / z^2 terms in step order for all 32 samples (serial chains the compute
+        // waves would otherwise run on all 64 lanes for 4 samples). Lane l < 32 owns sample l
+        // (compute wave l / 4, row l % 4). No global stores here but the per-sample results: the
+        // DMA waits (vmcnt) would otherwise also wait for the stores' write acknowledgements.
+        const int lane = lane_id();
+        const int sw = (lane & 31) >> 2, sq = lane & 3;
+        auto sums = [&](int i0b, int nb, int pb, float& ld, float& zsq) {
+            const float* zt = wtile(sw) + 4 * kSeqsStep + pb * 4 * kSeqsStep + sq * kSeqsStep;
+            const float* at = zt + 2 * 4 * kSeqsStep;
+            auto step = [&](float a, float z) {
+                if constexpr (VAR == NFX_MAF_FORWARD) ld = ld + a;
+                else ld = ld - a;
+                if constexpr (LOGP) zsq = gauss_sq(zsq, z);
+            };
+            int j = 0;
+            for (; j + 4 <= nb; j += 4) {
+                const f32x4 a4 = *reinterpret_cast<const f32x4*>(at + j);
+                const f32x4 z4 = *reinterpret_cast<const f32x4*>(zt + j);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) step(a4[c], z4[c]);
+            }
+            for (; j < nb; ++j) step(at[j], zt[j]);
+            (void)i0b;
+        };
         for (int64_t gb = (int64_t)blockIdx.x * kSeqsWaves * 4; gb < B; gb += (int64_t)gridDim.x * kSeqsWaves * 4) {
+            float ld = 0.f, zsq = 0.f;
             int i0 = 0, n = blk_end(0), buf = 0;
+            int i0p = 0, np = 0;  // the previous block (its tiles have parity buf ^ 1)
             seqs_lds_barrier();  // A: the previous group is done with the staging buffers
             blk_stage(0, 0);
             seqs_dma_wait();
@@ -322,11 +355,28 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
                 const int i0n = i0 + n;
                 const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
                 if (nn > 0) blk_stage(i0n, buf ^ 1);
+                if (np > 0) sums(i0p, np, buf ^ 1, ld, zsq);
                 seqs_dma_wait();
                 seqs_lds_barrier();  // C: every compute wave is done with the block; the next is in
+                i0p = i0;
+                np = n;
                 i0 = i0n;
                 n = nn;
                 buf ^= 1;
+            }
+            // the group's last block (parity buf ^ 1), then the per-sample results
+            sums(i0p, np, buf ^ 1, ld, zsq);
+            const int64_t s = gb + (lane & 31);
+            if (lane < 32 && s < B) {
+                if (nonfinite(ld)) ld = 0.f;
+                ld = (VAR == NFX_MAF_FORWARD) ? tclamp(ld, -100.f, 100.f) : tclamp(ld, -50.f, 50.f);
+                const float ldt = accumulate ? logdet[s] + ld : ld;
+                logdet[s] = ldt;
+                if constexpr (LOGP) {
+                    const float lp = gauss_lp(zsq, cgauss, ldt);
+                    logp[s] = lp;
+                    lpacc += (double)lp;
+                }
             }
         }
     } else {
@@ -342,40 +392,34 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
             h1v[k] = h2v[k] = 0.f;
         }
         for (int e = lane; e < 4 * kSeqsH3; e += 64) h3_t[e] = 0.f;
-        float ld = 0.f, zsq = 0.f;
         bool poisoned = false;
         int kc = 0;  // chunk index into the schedule (made_seqs_chunk_kernel)
 
         float xr[4];
         int i0 = 0, n = blk_end(0), buf = 0;
         x_load(gb, i0, n, xr);
-        if constexpr (kSeqsStager) {
-            seqs_lds_barrier();  // A
-            seqs_lds_barrier();  // B
-        } else {
-            __syncthreads();  // previous group's readers of the staging buffers are done
-            blk_stage(i0, 0);
-            seqs_dma_wait();
-            __syncthreads();
-        }
+        seqs_lds_barrier();  // A
+        seqs_lds_barrier();  // B
 
         while (i0 < d) {
-            const float* blk = lds + S.blk + buf * S.blkf;
+            // The block's LDS offset is laundered through an empty asm: the staged blocks sit above
+            // 64 KiB, past the reach of a ds_read's immediate offset, and with the constant visible
+            // the compiler re-adds it to every read (8 v_add per 16 ranks of the dot products)
+            // instead of keeping the whole base in the address VGPR.
+            int blk_off = S.blk + buf * S.blkf;
+            asm volatile("" : "+v"(blk_off));
+            const float* blk = lds + blk_off;
             const float* w1b = blk;
             const float* w4b = blk + W4F;
             const float* bmb = blk + B4F;
             const float* bab = bmb + kSeqsStep;
+            float* zout_t = zt2 + buf * 4 * kSeqsStep;  // this block's z / alpha tiles (the staging
+            float* at_t = at2 + buf * 4 * kSeqsStep;    // wave reads them during the next block)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                xin_t[q * kSeqsStep + lane] = xr[q];
-                if (lane >= n) zout_t[q * kSeqsStep + lane] = at_t[q * kSeqsStep + lane] = 0.f;
-            }
+            for (int q = 0; q < 4; ++q) xin_t[q * kSeqsStep + lane] = xr[q];
             const int i0n = i0 + n;
             const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
-            if (nn > 0) {
-                if constexpr (!kSeqsStager) blk_stage(i0n, buf ^ 1);  // its readers finished the previous block
-                x_load(gb, i0n, nn, xr);
-            }
+            if (nn > 0) x_load(gb, i0n, nn, xr);
             seqs_lds_order();
             SeqsDesc da, db;
             seqs_desc_load(ctab + 8 * kc, da);
@@ -508,47 +552,20 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
                 if (chunk(db, da)) break;
             }
             seqs_lds_order();
-            // log-det and z^2 of the block in step order (steps past d hold exact zeros)
-#pragma unroll 4
-            for (int j = 0; j < kSeqsStep; j += 4) {
-                const f32x4 ta = *reinterpret_cast<const f32x4*>(at_t + slot * kSeqsStep + j);
-                const f32x4 tz = *reinterpret_cast<const f32x4*>(zout_t + slot * kSeqsStep + j);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    if constexpr (VAR == NFX_MAF_FORWARD) ld = ld + ta[c];
-                    else ld = ld - ta[c];
-                    if constexpr (LOGP) zsq = gauss_sq(zsq, tz[c]);
-                }
-            }
-            // this wave's 4 output rows for the block (coalesced)
+            // this wave's 4 output rows for the block (coalesced; the sums: the staging wave)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t so = gb + wave * 4 + q;
                 if (so < B && lane < n) out[so * d + i0 + lane] = zout_t[q * kSeqsStep + lane];
             }
-            NFX_TMARK(4);  // log-det / z^2 sums of the block, output rows
-            if constexpr (kSeqsStager) {
-                seqs_lds_barrier();  // C: the next block is in LDS, every wave is done with this one
-            } else {
-                seqs_dma_wait();  // the next block's LDS-DMA has landed
-                __syncthreads();  // ... for every wave; and every wave is done with this block
-            }
+            NFX_TMARK(4);  // output rows
+            seqs_lds_barrier();  // C: the next block is in LDS, every wave is done with this one
             NFX_TMARK(5);  // barrier
             i0 = i0n;
             n = nn;
             buf ^= 1;
         }
-        if (valid && sub == 0) {
-            if (nonfinite(ld)) ld = 0.f;
-            ld = (VAR == NFX_MAF_FORWARD) ? tclamp(ld, -100.f, 100.f) : tclamp(ld, -50.f, 50.f);
-            const float ldt = accumulate ? logdet[s] + ld : ld;
-            logdet[s] = ldt;
-            if constexpr (LOGP) {
-                const float lp = gauss_lp(zsq, cgauss, ldt);
-                logp[s] = lp;
-                lpacc += (double)lp;
-            }
-        }
+        (void)valid;
     }
     }
 #ifdef NFX_SEQS_TIMING
