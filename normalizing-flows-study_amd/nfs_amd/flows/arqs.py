@@ -261,7 +261,12 @@ class ARQS(HipFlow):
             else:
                 masks, (h1, h2, h3, prm) = self._generic_made(state)
                 self._step(xr, prm, state, None, gld, lam, gprm, gx, i, direction, 1)
-                gi = _generic.made_backward(state, lins, masks, h1, h2, h3, gprm, lam)
+                # only step i's R output columns carry a gradient: the output layer's backward on
+                # those rows alone (O(d R H B) per call instead of O(d^2 R H B))
+                gsl = gprm[:, i * R:(i + 1) * R].contiguous()
+                grads = _generic.made_backward_rows(state, lins, masks, h1, h2, h3, gsl, i * R, (i + 1) * R, lam,
+                                                    grads)
+                continue
             grads = gi if grads is None else [a.add_(b) for a, b in zip(grads, gi)]
         if bounds is not None:
             gx = self._map(gx, bounds, 2)

@@ -106,6 +106,45 @@ def made_backward(x, lins, masks, h1, h2, h3, gp, gx):
     return [*g1, *g2, *g3, *g4]
 
 
+class _LinRows:
+    """Output rows [r0, r1) of an nn.Linear / MaskedLinear (contiguous views of weight and bias)."""
+
+    def __init__(self, lin, r0, r1):
+        self.weight = lin.weight[r0:r1]
+        self.bias = None if lin.bias is None else lin.bias[r0:r1]
+        self.in_features = lin.in_features
+        self.out_features = r1 - r0
+
+
+def made_backward_rows(x, lins, masks, h1, h2, h3, gp_rows, r0, r1, gx, grads=None):
+    """made_backward for a dL/dparams that is zero outside output columns [r0, r1) (gp_rows: those
+    columns, contiguous [B, r1 - r0]; e.g. one ARQS step's spline row): the output layer's weight
+    and data gradients run on its rows [r0, r1) only, not on all of them. The parameter gradients
+    are accumulated into `grads` (parameters() order, full shapes; created when None) and
+    returned; dL/dx is added into gx."""
+    l4 = _LinRows(lins[3], r0, r1)
+    m4 = masks[3][r0:r1]
+    gw4, gb4 = linear_backward_weight(gp_rows, h3, l4, wmask=m4)
+    g = linear_backward_data(gp_rows, l4, act=h3, wmask=m4)
+    g3 = linear_backward_weight(g, h2, lins[2], wmask=masks[2])
+    g = linear_backward_data(g, lins[2], act=h2, wmask=masks[2])
+    g2 = linear_backward_weight(g, h1, lins[1], wmask=masks[1])
+    g = linear_backward_data(g, lins[1], act=h1, wmask=masks[1])
+    g1 = linear_backward_weight(g, x, lins[0], wmask=masks[0])
+    linear_backward_data(g, lins[0], wmask=masks[0], out=gx)
+    if grads is None:
+        grads = [*g1, *g2, *g3, torch.zeros_like(lins[3].weight, dtype=torch.float32),
+                 None if lins[3].bias is None else torch.zeros_like(lins[3].bias, dtype=torch.float32)]
+    else:
+        for a, b in zip(grads[:6], [*g1, *g2, *g3]):
+            if a is not None:
+                a.add_(b)
+    grads[6][r0:r1].add_(gw4)
+    if gb4 is not None:
+        grads[7][r0:r1].add_(gb4)
+    return grads
+
+
 # ---- MADE with BatchNorm1d (use_batch_norm=True): activations kept pre- and post-BatchNorm ------
 def bn_apply_relu(z, t):
     """relu(z * scale + shift) with t = [mean, invstd, scale, shift] (nfx_bn_prepare)."""
