@@ -210,6 +210,12 @@ int nfx_arqs(const float* packed, const float* in, float* out, float* log_det, i
  * ------------------------------------------------------------------------------------- */
 size_t nfx_made_packed_floats(int d, int H);
 int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
+/* nfx_made_pack in two parts: the parallel directions' image (+ degree tables and structural-zero
+ * extents), then — required before an NFX_MAF_FORWARD / NFX_IAF_INVERSE nfx_made_affine(_logprob)
+ * call on the buffer — the sequential directions' rank-ordered image and chunk schedule.
+ * nfx_made_pack = both. */
+int nfx_made_pack_parallel(const NfxMlpRaw* net, int d, int H, float* packed, void* stream);
+int nfx_made_pack_sequential(int d, int H, float* packed, void* stream);
 int nfx_made_affine(const float* packed, const float* in, float* out, float* log_det,
                     int64_t B, int d, int H, int variant, int accumulate, void* stream);
 /* Density direction + fused log_prob epilogue (see nfx_affine_coupling_logprob):

@@ -10,14 +10,6 @@
 
 namespace nfx {
 
-// Degree of hidden unit a from the input->hidden mask: M1[a][j] = (j <= deg(a)) (made.py:56).
-__device__ inline int made_unit_degree(const NfxMlpRaw& net, int d, int a) {
-    if (!net.mask[0]) return 0;
-    int n = 0;
-    for (int j = 0; j < d; ++j) n += net.mask[0][(size_t)a * d + j] != 0.f ? 1 : 0;
-    return n - 1;
-}
-
 __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
@@ -90,12 +82,29 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
 __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
-    // hidden-unit degrees (row sums of the input mask) and the stable by-degree completion
+    // hidden-unit degrees (M1[a][j] = (j <= deg(a)), made.py:56: row sums of the input mask - 1)
+    // and the stable by-degree completion
     // order of the sequential kernels: s_deg [unit degree | degrees in order | units in order]
     {
         __shared__ int deg[256];
         const int Hp = L.Hp;
-        for (int a = threadIdx.x; a < Hp; a += 256) deg[a] = a < H ? made_unit_degree(net, d, a) : 1000000000;
+        // 16 lanes per unit (16 units per pass of the block), each counting a strided slice of the
+        // unit's mask row with its loads independent, then a 16-lane sum: the serial row walk per
+        // thread was most of this kernel's time at every training step's re-pack
+        for (int a0 = 0; a0 < Hp; a0 += 16) {
+            const int a = a0 + (threadIdx.x >> 4), q = threadIdx.x & 15;
+            int n = 0;
+            if (a < H && net.mask[0]) {
+                const float* row = net.mask[0] + (size_t)a * d;
+#pragma unroll 4
+                for (int j = q; j < d; j += 16) n += row[j] != 0.f ? 1 : 0;
+            }
+            n += __shfl_xor(n, 1);
+            n += __shfl_xor(n, 2);
+            n += __shfl_xor(n, 4);
+            n += __shfl_xor(n, 8);
+            if (q == 0 && a < Hp) deg[a] = a < H ? (net.mask[0] ? n - 1 : 0) : 1000000000;
+        }
         __syncthreads();
         for (int a = threadIdx.x; a < Hp; a += 256) {
             const int da = deg[a];
@@ -106,11 +115,26 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
             packed[L.s_deg + 2 * Hp + rank] = (float)a;
         }
     }
+    // the extent words (made_extent_kernel, launched next, max-es into them)
+    int* nk = reinterpret_cast<int*>(packed);
+    for (int i = threadIdx.x; i < 3 * HT + L.NJ; i += 256) nk[L.nk1 + i] = 0;
+    // overflow bound
+    __shared__ double red[256];
+    const int rows[4] = {H, H, H, 2 * d}, cols[4] = {d, H, H, H};
+    const double tsafe = block_mlp_tsafe(net, 4, rows, cols, 1.0e37, red);
+    if (threadIdx.x == 0) packed[L.tsafe] = (float)fmin(tsafe, 3.0e38);
+}
+
+// The k-block extents of the packed parallel image (made_live_kernel's structural zeros): one
+// wave per 256-float weight group (32 rows x 8 k-steps), one float4 per lane and a ballot, the
+// group's extent max-ed into its tile's word (zeroed by made_live_kernel, launched before).
+__global__ __launch_bounds__(256) void made_extent_kernel(int d, int H, float* packed) {
+    const int HT = (H + 31) / 32;
+    const MadeLayout L = made_layout(d, HT);
     int* nk = reinterpret_cast<int*>(packed);
     const int n1 = HT * 4 * L.NKC, n23 = HT * HT * 4, n4 = L.NJ * 2 * HT * 4;
-    for (int i = threadIdx.x; i < 3 * HT + L.NJ; i += 256) nk[L.nk1 + i] = 0;
-    __syncthreads();
-    for (int gi = threadIdx.x; gi < n1 + 2 * n23 + n4; gi += 256) {
+    const int lane = lane_id();
+    for (int gi = blockIdx.x * 4 + (threadIdx.x >> 6); gi < n1 + 2 * n23 + n4; gi += gridDim.x * 4) {
         int off, word, ext;  // 256-float weight group (32 rows x 8 k-steps) -> its k-block extent
         if (gi < n1) {
             const int ht = gi / (4 * L.NKC), g = gi % (4 * L.NKC);
@@ -128,15 +152,10 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
             word = L.nk4 + t / (2 * HT * 4);
             ext = (t % (HT * 4)) / 4 + 1;
         }
-        bool nz = false;
-        for (int e = 0; e < 256; ++e) nz |= packed[off + e] != 0.f;  // NaN != 0: kept
-        if (nz) atomicMax(&nk[word], ext);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(packed + off + 4 * lane);
+        const bool nzl = v[0] != 0.f || v[1] != 0.f || v[2] != 0.f || v[3] != 0.f;  // NaN != 0: kept
+        if (__ballot(nzl) != 0 && lane == 0) atomicMax(&nk[word], ext);
     }
-    // overflow bound
-    __shared__ double red[256];
-    const int rows[4] = {H, H, H, 2 * d}, cols[4] = {d, H, H, H};
-    const double tsafe = block_mlp_tsafe(net, 4, rows, cols, 1.0e37, red);
-    if (threadIdx.x == 0) packed[L.tsafe] = (float)fmin(tsafe, 3.0e38);
 }
 
 template <int HT>
@@ -206,7 +225,23 @@ extern "C" size_t nfx_made_packed_floats(int d, int H) {
     return (size_t)made_layout(d, (H + 31) / 32).total;
 }
 
-extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
+namespace nfx {
+// the sequential directions' part of a pack (HT <= 2): the rank-ordered image and the chunk
+// schedule, from the degree tables made_live_kernel wrote
+static int made_pack_seq(int d, int H, float* packed, hipStream_t s) {
+    const int HT = (H + 31) / 32;
+    if (HT > 2) return NFX_OK;
+    if (HT == 1) made_seqs_image_kernel<1><<<64, 256, 0, s>>>(packed, d, H);
+    else made_seqs_image_kernel<2><<<64, 256, 0, s>>>(packed, d, H);
+    int rc = check_launch("made_seqs_image_kernel");
+    if (rc) return rc;
+    if (HT == 1) made_seqs_chunk_kernel<1><<<1, 64, 0, s>>>(packed, d, H);
+    else made_seqs_chunk_kernel<2><<<1, 64, 0, s>>>(packed, d, H);
+    return check_launch("made_seqs_chunk_kernel");
+}
+}  // namespace nfx
+
+extern "C" int nfx_made_pack_parallel(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
     if (!net || !packed) return set_error(NFX_EINVAL, "made_pack: null pointer");
     if (d <= 0 || d > 4096 || H <= 0 || H > 256)
         return set_error(NFX_EUNSUPPORTED, "made_pack: d=%d H=%d outside d<=4096, H<=256", d, H);
@@ -222,15 +257,26 @@ extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, 
     made_live_kernel<<<1, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
     rc = check_launch("made_live_kernel");
     if (rc) return rc;
-    const int HT = (H + 31) / 32;
-    if (HT > 2) return NFX_OK;
-    if (HT == 1) made_seqs_image_kernel<1><<<64, 256, 0, (hipStream_t)stream>>>(packed, d, H);
-    else made_seqs_image_kernel<2><<<64, 256, 0, (hipStream_t)stream>>>(packed, d, H);
-    rc = check_launch("made_seqs_image_kernel");
+    {
+        const int HT = (H + 31) / 32;
+        const MadeLayout L = made_layout(d, HT);
+        const int groups = HT * 4 * L.NKC + 2 * HT * HT * 4 + L.NJ * 2 * HT * 4;
+        made_extent_kernel<<<(groups + 3) / 4, 256, 0, (hipStream_t)stream>>>(d, H, packed);
+    }
+    return check_launch("made_extent_kernel");
+}
+
+extern "C" int nfx_made_pack_sequential(int d, int H, float* packed, void* stream) {
+    if (!packed) return set_error(NFX_EINVAL, "made_pack_sequential: null pointer");
+    if (d <= 0 || d > 4096 || H <= 0 || H > 256)
+        return set_error(NFX_EUNSUPPORTED, "made_pack_sequential: d=%d H=%d outside d<=4096, H<=256", d, H);
+    return made_pack_seq(d, H, packed, (hipStream_t)stream);
+}
+
+extern "C" int nfx_made_pack(const NfxMlpRaw* net, int d, int H, float* packed, void* stream) {
+    const int rc = nfx_made_pack_parallel(net, d, H, packed, stream);
     if (rc) return rc;
-    if (HT == 1) made_seqs_chunk_kernel<1><<<1, 64, 0, (hipStream_t)stream>>>(packed, d, H);
-    else made_seqs_chunk_kernel<2><<<1, 64, 0, (hipStream_t)stream>>>(packed, d, H);
-    return check_launch("made_seqs_chunk_kernel");
+    return made_pack_seq(d, H, packed, (hipStream_t)stream);
 }
 
 namespace nfx {

@@ -52,19 +52,27 @@ __device__ inline double block_mlp_tsafe(const NfxMlpRaw& net, int nl, const int
                 cmax = (b > cmax || b != b) ? b : cmax;
             }
         }
-        for (int k = 0; k < 2; ++k) {
-            red[threadIdx.x] = k == 0 ? nmax : cmax;
-            __syncthreads();
-            for (int w = 128; w > 0; w >>= 1) {
-                if (threadIdx.x < w) {
-                    const double a = red[threadIdx.x], b = red[threadIdx.x + w];
-                    red[threadIdx.x] = (b > a || b != b) ? b : a;
-                }
-                __syncthreads();
-            }
-            if (k == 0) nmax = red[0]; else cmax = red[0];
-            __syncthreads();
+        // NaN-propagating max over the block: within each wave by shuffles, then the 4 wave
+        // results through LDS (two barriers instead of one per tree level)
+        auto nmaxd = [](double a, double b) { return (b > a || b != b) ? b : a; };
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            nmax = nmaxd(nmax, __shfl_xor(nmax, o));
+            cmax = nmaxd(cmax, __shfl_xor(cmax, o));
         }
+        const int wv = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) {
+            red[2 * wv] = nmax;
+            red[2 * wv + 1] = cmax;
+        }
+        __syncthreads();
+        nmax = red[0];
+        cmax = red[1];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            nmax = nmaxd(nmax, red[2 * w]);
+            cmax = nmaxd(cmax, red[2 * w + 1]);
+        }
+        __syncthreads();
         alpha = nmax * alpha;
         beta = nmax * beta + cmax;
         if (!(beta < lim) || !(alpha < 1e300)) tsafe = 0.0;

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "nfx_spline_chain_supported", "nfx_spline_chain", "nfx_spline_chain_logprob",
     "nfx_rqs_unit",
     "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
-    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_affine", "nfx_made_affine_logprob", "nfx_made_seq_policy",
+    "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_pack_parallel", "nfx_made_pack_sequential", "nfx_made_affine", "nfx_made_affine_logprob", "nfx_made_seq_policy",
     "nfx_made_pack_backward", "nfx_made_backward_factor_floats", "nfx_made_backward_max_batch",
     "nfx_made_affine_backward",
     "nfx_made_seq_backward", "nfx_made_factor_pitch", "nfx_made_param_floats", "nfx_made_wgrad_workspace_bytes", "nfx_made_backward_weights",
@@ -152,6 +152,8 @@ _SIGNATURES = {
     "nfx_rqs_unit": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int, _vp]),
     "nfx_made_packed_floats": (_sz, [_int, _int]),
     "nfx_made_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
+    "nfx_made_pack_parallel": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _vp, _vp]),
+    "nfx_made_pack_sequential": (_int, [_int, _int, _vp, _vp]),
     "nfx_made_seq_policy": (_int, [_int]),
     "nfx_made_affine": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_made_affine_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),

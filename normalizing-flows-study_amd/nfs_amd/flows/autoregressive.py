@@ -389,10 +389,24 @@ class _MadeAffineFlow(HipFlow):
         lins = self.conditioner.linears()
         bns = self.conditioner.batchnorms() or ()
         raw, keep = _lib.mlp_raw(lins, bns, masks=[lin.mask for lin in lins])
-        _lib.check(L.nfx_made_pack(raw, d, H, _lib.ptr(packed), _lib.stream_of(packed)), "nfx_made_pack")
+        # the parallel image (+ degree tables, extents); the sequential directions' image and chunk
+        # schedule are added on the first sequential launch of this pack (_seq_packed): a training
+        # step re-packs every layer, and the parallel directions never read them
+        _lib.check(L.nfx_made_pack_parallel(raw, d, H, _lib.ptr(packed), _lib.stream_of(packed)),
+                   "nfx_made_pack_parallel")
         _lib.check(L.nfx_made_pack_backward(raw, d, H, _lib.ptr(packed), _lib.stream_of(packed)),
                    "nfx_made_pack_backward")
         packed._nfx_keep = keep
+        packed._nfx_seq = False
+        return packed
+
+    def _seq_packed(self, packed, variant):
+        """`packed` with the sequential part built (nfx_made_pack_sequential) when `variant` is a
+        sequential direction."""
+        if variant in (_lib.NFX_MAF_FORWARD, _lib.NFX_IAF_INVERSE) and not getattr(packed, "_nfx_seq", True):
+            _lib.check(_lib.lib().nfx_made_pack_sequential(self.dim, self.conditioner.hidden_dim, _lib.ptr(packed),
+                                                           _lib.stream_of(packed)), "nfx_made_pack_sequential")
+            packed._nfx_seq = True
         return packed
 
     # -- training: fused backward of every direction (§8(f) item 1) --------------------------
@@ -484,17 +498,18 @@ class _MadeAffineFlow(HipFlow):
     def _hip_launch(self, x, out, log_det, direction, accumulate):
         if not self._fused_family():
             return self._generic_launch(x, out, log_det, direction, accumulate)
-        packed = self._packed(x.device, self._build_pack)
+        variant = self._variant(direction)
+        packed = self._seq_packed(self._packed(x.device, self._build_pack), variant)
         _lib.check(_lib.lib().nfx_made_affine(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), x.shape[0], self.dim,
-            self.conditioner.hidden_dim, self._variant(direction), int(bool(accumulate)),
+            self.conditioner.hidden_dim, variant, int(bool(accumulate)),
             _lib.stream_of(x)), "nfx_made_affine")
 
     def _hip_launch_logprob(self, x, out, log_det, logp, sums, workspace, accumulate):
         if not self._fused_family():
             return False
         variant = self._variant(-1)
-        packed = self._packed(x.device, self._build_pack)
+        packed = self._seq_packed(self._packed(x.device, self._build_pack), variant)
         rc = _lib.lib().nfx_made_affine_logprob(
             _lib.ptr(packed), _lib.ptr(x), _lib.ptr(out), _lib.ptr(log_det), _lib.ptr(logp),
             _lib.ptr(sums), _lib.ptr(workspace), x.shape[0], self.dim,
