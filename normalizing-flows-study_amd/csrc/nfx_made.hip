@@ -79,7 +79,9 @@ __global__ void made_pack_kernel(NfxMlpRaw net, int d, int H, float* packed) {
 // dense product. tsafe: with n_l = max row sum |W'_l| and c_l = max |b'_l|, every partial sum
 // of layer l is bounded by A_l = n_l*A_{l-1} + c_l (A_0 = max|x|); tsafe is the largest A_0
 // keeping every A_l <= 1e37 (0 when a weight is non-finite: dense path always).
-__global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, int H, float* packed) {
+constexpr int kLiveThreads = 1024;  // made_live_kernel: one block, 8 threads per weight row
+
+__global__ __launch_bounds__(kLiveThreads) void made_live_kernel(NfxMlpRaw net, int d, int H, float* packed) {
     const int HT = (H + 31) / 32;
     const MadeLayout L = made_layout(d, HT);
     // hidden-unit degrees (M1[a][j] = (j <= deg(a)), made.py:56: row sums of the input mask - 1)
@@ -88,10 +90,10 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
     {
         __shared__ int deg[256];
         const int Hp = L.Hp;
-        // 16 lanes per unit (16 units per pass of the block), each counting a strided slice of the
+        // 16 lanes per unit (64 units per pass of the block), each counting a strided slice of the
         // unit's mask row with its loads independent, then a 16-lane sum: the serial row walk per
         // thread was most of this kernel's time at every training step's re-pack
-        for (int a0 = 0; a0 < Hp; a0 += 16) {
+        for (int a0 = 0; a0 < Hp; a0 += kLiveThreads / 16) {
             const int a = a0 + (threadIdx.x >> 4), q = threadIdx.x & 15;
             int n = 0;
             if (a < H && net.mask[0]) {
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
             if (q == 0 && a < Hp) deg[a] = a < H ? (net.mask[0] ? n - 1 : 0) : 1000000000;
         }
         __syncthreads();
-        for (int a = threadIdx.x; a < Hp; a += 256) {
+        for (int a = threadIdx.x; a < Hp; a += kLiveThreads) {
             const int da = deg[a];
             int rank = 0;
             for (int b = 0; b < Hp; ++b) rank += (deg[b] < da || (deg[b] == da && b < a)) ? 1 : 0;
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(256) void made_live_kernel(NfxMlpRaw net, int d, in
     }
     // the extent words (made_extent_kernel, launched next, max-es into them)
     int* nk = reinterpret_cast<int*>(packed);
-    for (int i = threadIdx.x; i < 3 * HT + L.NJ; i += 256) nk[L.nk1 + i] = 0;
+    for (int i = threadIdx.x; i < 3 * HT + L.NJ; i += kLiveThreads) nk[L.nk1 + i] = 0;
     // overflow bound
     __shared__ double red[256];
     const int rows[4] = {H, H, H, 2 * d}, cols[4] = {d, H, H, H};
@@ -254,7 +256,7 @@ extern "C" int nfx_made_pack_parallel(const NfxMlpRaw* net, int d, int H, float*
     made_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
     int rc = check_launch("made_pack_kernel");
     if (rc) return rc;
-    made_live_kernel<<<1, 256, 0, (hipStream_t)stream>>>(*net, d, H, packed);
+    made_live_kernel<<<1, kLiveThreads, 0, (hipStream_t)stream>>>(*net, d, H, packed);
     rc = check_launch("made_live_kernel");
     if (rc) return rc;
     {

@@ -26,19 +26,19 @@ __device__ inline float mlp_bias(const NfxMlpRaw& net, int layer, int row) {
     return b;
 }
 
-// Overflow-safe input bound of an MLP, computed by one 256-thread block (every thread gets the
-// result). With n_l = max row sum |W'_l| and c_l = max |b'_l|, every partial sum of layer l is
+// Overflow-safe input bound of an MLP, computed by one block of up to 1024 threads (every thread
+// gets the result; 8 threads per weight row). With n_l = max row sum |W'_l| and c_l = max |b'_l|, every partial sum of layer l is
 // bounded by A_l = n_l*A_{l-1} + c_l (A_0 = max|x|): returns the largest A_0 keeping every
 // A_l <= lim (0 when a weight or bias is non-finite). ReLU/clamps only shrink magnitudes, so
 // inputs within the bound produce finite activations everywhere.
 __device__ inline double block_mlp_tsafe(const NfxMlpRaw& net, int nl, const int* rows, const int* cols,
-                                         double lim, double* red /* [256] shared */) {
+                                         double lim, double* red /* [>= 2 * waves] shared */) {
     double alpha = 1.0, beta = 0.0, tsafe = 3.0e38;
     for (int l = 0; l < nl; ++l) {
         double nmax = 0.0, cmax = 0.0;
         // 8 threads per row, each over a strided slice of the columns: independent loads in
         // flight instead of one serial row walk per thread
-        for (int r0 = 0; r0 < rows[l]; r0 += 32) {
+        for (int r0 = 0; r0 < rows[l]; r0 += (int)(blockDim.x >> 3)) {
             const int r = r0 + (threadIdx.x >> 3), q = threadIdx.x & 7;
             double sum = 0.0;
             if (r < rows[l])
