@@ -32,9 +32,9 @@
 
 namespace nfx {
 
-// per compute wave: the x block tile, two z block tiles (alternate blocks) and 64 floats where
+// per compute wave: two x block tiles and two z block tiles (alternate blocks) and 64 floats where
 // masked lanes' stores land; then one z^2 sum per sample slot
-constexpr int kSeqwTile = 4 * kSeqsStep;
+constexpr int kSeqwTile = 5 * kSeqsStep;
 
 __host__ __device__ inline int seqw_blkf(int Hp) { return kSeqsStep * Hp + kSeqsStep * seqs_w4_stride(Hp) + 2 * kSeqsStep; }
 // LDS: tables (5 Hp) | W2, W3 rank-ordered images (2 Hp^2) | two staged blocks | per-wave tiles | z^2 sums
@@ -138,7 +138,11 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
 
     if (wave == NWV) {
         // ---------------- staging wave ----------------
-        auto stage = [&](int i0, int buf) {
+        // a block's weight rows, and every compute wave's inputs for it (the x tile of the block's
+        // parity: no global loads in the compute waves, whose vmcnt waits would also wait for
+        // their output stores' acknowledgements). Lanes past the block read later inputs of the
+        // row (finite; their steps are masked), rows past B read row 0.
+        auto stage = [&](int64_t gb, int i0, int buf) {
             float* dst = blk0 + buf * BLKF;
             const float* sw1 = P + L.sw1 + (size_t)i0 * Hp;
             const float* sw4 = P + L.sw4 + (size_t)i0 * RS4;
@@ -148,11 +152,17 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             for (int j = 0; j < N4; ++j) seqs_dma_x4(sw4 + 256 * j + 4 * lane, dst + W4F + 256 * j);
             seqs_dma_dword(P + L.sb4 + i0 + lane, dst + B4F);
             seqs_dma_dword(P + L.sb4 + (size_t)(d + kSeqsPadRows) + i0 + lane, dst + B4F + 64);
+            const int col = i0 + lane < d ? i0 + lane : d - 1;
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) {
+                const int64_t sw = gb + w < B ? gb + w : 0;
+                seqs_dma_dword(in + sw * d + col, tiles + w * kSeqwTile + kSeqsStep * buf);
+            }
         };
         // step-order z^2 of sample slot `lane` over the block in tile `par`
         auto zsq_block = [&](int par, float z) -> float {
             if (lane < NWV) {
-                const float* zt = tiles + lane * kSeqwTile + kSeqsStep * (1 + par);
+                const float* zt = tiles + lane * kSeqwTile + kSeqsStep * (2 + par);
 #pragma unroll 4
                 for (int j = 0; j < kSeqsStep; j += 4) {
                     const f32x4 tz = *reinterpret_cast<const f32x4*>(zt + j);
@@ -166,14 +176,14 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             float z = 0.f;
             int i0 = 0, n = blk_end(0), buf = 0, par = 0;
             seqs_lds_barrier();  // A: the previous group is done with the staging buffers
-            stage(0, 0);
+            stage(gb, 0, 0);
             seqs_dma_wait();
             seqs_lds_barrier();  // B: block 0 is in LDS
             bool prev = false;
             while (i0 < d) {
                 const int i0n = i0 + n;
                 const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
-                if (nn > 0) stage(i0n, buf ^ 1);
+                if (nn > 0) stage(gb, i0n, buf ^ 1);
                 if (LOGP && prev) z = zsq_block(par ^ 1, z);  // the block before this one
                 seqs_dma_wait();
                 seqs_lds_barrier();  // C: block done by every compute wave; the next one is in LDS
@@ -193,12 +203,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
         // ---------------- compute waves: one sample each ----------------
         const float b1u = own ? lds[S.b1 + posu] : 0.f;
         float* xin_t = tiles + wave * kSeqwTile;
-        auto x_load = [&](int64_t s, int i0, int n) -> float {
-            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in) + (s < B ? s : 0) * d, 0,
-                                                              s < B ? d * 4 : 0, 0x00020000);
-            const int voff = lane < n ? (i0 + lane) * 4 : (int)0x7FFFFFF0;
-            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0));
-        };
+        const float* xt = xin_t;  // the block's x tile (parity par)
         // operands of the chunk at block position ii (rows past the block clamp to its last row:
         // their steps are masked out)
         const uint32_t* ctab = reinterpret_cast<const uint32_t*>(P + L.ctab);
@@ -213,7 +218,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             }
             o.bmu = blk[B4F + rj];
             o.bal = blk[B4F + kSeqsStep + rj];
-            o.xin = xin_t[rj];
+            o.xin = xt[rj];
         };
 #ifdef NFX_SEQW_TIMING
         long long tacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -238,18 +243,16 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             int kc = 0;  // chunk index into the schedule
 
             int i0 = 0, n = blk_end(0), buf = 0, par = 0;
-            float xr = x_load(s, 0, n);
             seqs_lds_barrier();  // A
             seqs_lds_barrier();  // B
             while (i0 < d) {
                 const float* blk = blk0 + buf * BLKF;
-                const int zoff = kSeqsStep * (1 + par);
+                const int zoff = kSeqsStep * (2 + par);
                 float* zt = xin_t + zoff;
-                xin_t[lane] = xr;
+                xt = xin_t + kSeqsStep * par;
                 if (LOGP && lane >= n) zt[lane] = 0.f;
                 const int i0n = i0 + n;
                 const int nn = i0n < d ? blk_end(i0n) - i0n : 0;
-                if (nn > 0) xr = x_load(s, i0n, nn);
                 seqs_lds_order();
                 SeqwOps<NM> opa, opb;
                 SeqsDesc da, db;
@@ -350,7 +353,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                         const bool st = vj && rq == 0;
                         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), orsrc, st ? (i + jl) * 4 : (int)0x7FFFFFF0,
                                                               0, 0);
-                        if constexpr (LOGP) xin_t[st ? zoff + rj : 3 * kSeqsStep + lane] = vo;
+                        if constexpr (LOGP) xin_t[st ? zoff + rj : 4 * kSeqsStep + lane] = vo;
                     }
                     // 5. rank-1 updates of every owned unit's layer-1 pre-activation
                     float cv[16];
