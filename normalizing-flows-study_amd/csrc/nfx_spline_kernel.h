@@ -370,6 +370,112 @@ __device__ __forceinline__ void spline_unit_apply(const float* P, const SplineLa
     }
 }
 
+// spline_unit_apply's body in three parts (the same operations in the same order), for the stage
+// clocks of the streaming chain's timing build (NFX_SCHAIN_TIMING): layers 1 and 2 (h2), layer 3's
+// tile t with the half-wave exchange (the lane's 32 spline parameters), and dim t's spline. The
+// product path keeps the single inline body (split, the allocation of the 8-wave chain kernel
+// grew from 189 to 212 VGPRs).
+template <int HT, int TILES>
+__device__ __forceinline__ void spline_unit_hidden(const float* P, const SplineLayout& L, int KS1,
+                                                   const float (&xb)[2][4], f32x16 (&h2)[HT][2]) {
+#pragma clang fp contract(off)
+    const int lane = lane_id(), h = lane >> 5;
+    // Layer 1 + ReLU
+    f32x16 h1[HT][2];
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) {
+        f32x16 a0, a1;
+        load_bias16_x2(P + L.b1 + ht * 32, h, a0, a1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            if (ks < KS1) {
+                const float w = P[L.w1 + (ht * 4 + ks) * 64 + lane];
+                a0 = mfma32(w, xb[0][ks], a0);
+                if constexpr (TILES == 2) a1 = mfma32(w, xb[1][ks], a1);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            a1[r] = trelu(a1[r]);
+        }
+        h1[ht][0] = a0;
+        h1[ht][1] = a1;
+    }
+    // Layer 2 + ReLU
+#pragma unroll
+    for (int hto = 0; hto < HT; ++hto) {
+        f32x16 a0, a1;
+        load_bias16_x2(P + L.b2 + hto * 32, h, a0, a1);
+#pragma unroll
+        for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+            for (int rq = 0; rq < 4; ++rq) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(
+                    P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    a0 = mfma32(w[rr], h1[kt][0][4 * rq + rr], a0);
+                    if constexpr (TILES == 2) a1 = mfma32(w[rr], h1[kt][1][4 * rq + rr], a1);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            a1[r] = trelu(a1[r]);
+        }
+        h2[hto][0] = a0;
+        h2[hto][1] = a1;
+    }
+}
+
+// Layer 3, tile t: the 3K-1 parameters of transformed dim tdim[t]; after the half-wave exchange
+// every lane holds rows 0..31 of its own sample.
+template <int HT, int TILES>
+__device__ __forceinline__ void spline_unit_params(const float* P, const SplineLayout& L, const f32x16 (&h2)[HT][2],
+                                                   int t, float (&prm)[32]) {
+#pragma clang fp contract(off)
+    const int lane = lane_id(), h = lane >> 5;
+    f32x16 a0, a1;
+    load_bias16_x2(P + L.b3 + t * 32, h, a0, a1);
+#pragma unroll
+    for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(P + L.w3 + (((t * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                a0 = mfma32(w[rr], h2[kt][0][4 * rq + rr], a0);
+                if constexpr (TILES == 2) a1 = mfma32(w[rr], h2[kt][1][4 * rq + rr], a1);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0[r]), __float_as_uint(a1[r]), false, false);
+        prm[crow(r, 0)] = __uint_as_float(sw[0]);
+        prm[crow(r, 1)] = __uint_as_float(sw[1]);
+    }
+}
+
+// Dim dt's spline on the lane's own sample: y[dt] and the log-det term (ld = l at t = 0, else +=).
+template <int K, int DIR, int DMAX>
+__device__ __forceinline__ void spline_unit_dim(const SplineConsts& C, int dt, int t, const float (&prm)[32],
+                                                const float (&xr)[DMAX], float (&y)[DMAX], float& ld) {
+#pragma clang fp contract(off)
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < DMAX; ++j) v = (j == dt) ? xr[j] : v;
+    if (C.rescale) v = C.rs_to_scale * (v - C.rs_lo) - C.bound;
+    float o, l;
+    rq_spline_elem<K, (DIR < 0)>(v, prm, C, o, l);
+    if (C.rescale) o = (o + C.bound) * C.rs_from_scale + C.rs_lo;
+#pragma unroll
+    for (int j = 0; j < DMAX; ++j) y[j] = (j == dt) ? o : y[j];
+    ld = (t == 0) ? l : ld + l;
+}
+
 // DS = the data dimension when it is fixed at compile time (2: the two-moons-shaped BASELINE
 // cfg3 / RealNVPSpline path), 0 = runtime d <= 8. With DS = 2 a lane's sample row is one
 // 8-byte load and the layer-1 operands of the two sample tiles come out of one

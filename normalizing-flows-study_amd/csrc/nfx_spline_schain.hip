@@ -1,6 +1,8 @@
 // Streaming spline chain: launch + C-ABI (kernel: nfx_spline_schain_kernel.h).
 #include "nfx_spline_schain_kernel.h"
 
+#include <cstdlib>
+
 namespace nfx {
 
 static int spline_schain_wpad_rt(int HT) { return (spline_layout(HT, 2).total + 255) & ~255; }
@@ -40,21 +42,29 @@ static int spline_chain_launch(const float* const* packs, int nl, const float* i
         P.p[l] = packs[l];
     }
     const int HT = (H + 31) / 32;
-    spline_schain_t k = HT == 1 ? spline_schain_pick_ht<1>(K, direction, fused) : spline_schain_pick_ht<2>(K, direction, fused);
-    if (!k) return set_error(NFX_EUNSUPPORTED, "spline_chain: no kernel for K=%d", K);
     const SplineConsts C = spline_consts(K, bound, min_w, min_h, min_d, 0, 0.f, 0.f);
     const int64_t nchunks = (B + 63) / 64;
     int64_t grid = num_cus();
     if (grid > nchunks) grid = nchunks;
     if (grid > kMaxPartials) grid = kMaxPartials;
     const int64_t per_wg = (nchunks + grid - 1) / grid;
+    // $NFX_SCHAIN_WAVES=8 / 12 forces one kernel (A/B measurements)
+    static const int force = [] {
+        const char* e = getenv("NFX_SCHAIN_WAVES");
+        return e ? atoi(e) : 0;
+    }();
+    const bool small = force ? force == kSplineSchainWavesSmall : per_wg <= kSplineSchainWavesSmall;
+    const int nw = small ? kSplineSchainWavesSmall : kSplineSchainWaves;
+    spline_schain_t k = HT == 1 ? spline_schain_pick_ht<1>(K, direction, fused, small)
+                                : spline_schain_pick_ht<2>(K, direction, fused, small);
+    if (!k) return set_error(NFX_EUNSUPPORTED, "spline_chain: no kernel for K=%d", K);
     const int64_t cap = spline_schain_slice_cap(HT);
     const int64_t nslices = (per_wg + cap - 1) / cap;
     const int64_t slice = (per_wg + nslices - 1) / nslices;
     const size_t lds = (2 * (size_t)spline_schain_wpad_rt(HT) + (size_t)slice * 64 * 3) * sizeof(float);
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
-    k<<<(unsigned)grid, 64 * kSplineSchainWaves, lds, s>>>(P, nl, in, out, log_det, B, C, accumulate, nchunks,
+    k<<<(unsigned)grid, 64 * nw, lds, s>>>(P, nl, in, out, log_det, B, C, accumulate, nchunks,
                                                             (int)slice, logp, reinterpret_cast<double*>(workspace),
                                                             sums, gauss_const(d));
     return check_launch("spline_schain_kernel");

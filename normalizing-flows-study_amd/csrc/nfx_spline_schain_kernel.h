@@ -47,6 +47,15 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
         }
     };
 
+#ifdef NFX_SCHAIN_TIMING
+    // timing build only (tools/schain_timing.py): workgroup 0's waves 0 and 4 accumulate clock64
+    // ticks per stage
+    long long tacc[6] = {0, 0, 0, 0, 0, 0};
+    long long tmark = clock64();
+#define NFX_CMARK(k) do { const long long t_ = clock64(); tacc[k] += t_ - tmark; tmark = t_; } while (0)
+#else
+#define NFX_CMARK(k) do { } while (0)
+#endif
     double lpacc = 0.0;
     int g = 0;  // layers run so far by this workgroup: weight buffer g & 1
     if (c0 < c1) stage(0, 0);
@@ -63,9 +72,12 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
         const bool half = split && wave < 2 * R;
         const int half_base = F * NW * 64 + wave * 32;
 
+        NFX_CMARK(4);  // slice prologue
         for (int li = 0; li < nl; ++li) {
+            NFX_CMARK(3);  // layer start + row io
             lds_dma_wait();
             __syncthreads();
+            NFX_CMARK(0);  // barrier
             if (li + 1 < nl)
                 stage(li + 1, (g + 1) & 1);
             else if (s0 + slice_chunks < c1)
@@ -102,7 +114,23 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
                 }
                 float y[D];
                 float ld;
+#ifdef NFX_SCHAIN_TIMING
+                {
+                    const float* Wz = W + opaque_zero();
+                    f32x16 h2[HT][2];
+                    spline_unit_hidden<HT, TILES>(Wz, L, 1, xb, h2);
+                    float prm[32];
+                    spline_unit_params<HT, TILES>(Wz, L, h2, 0, prm);
+                    NFX_CMARK(1);  // MFMA part (one transformed dim)
+#pragma unroll
+                    for (int j = 0; j < D; ++j) y[j] = xr[j];
+                    ld = 0.f;
+                    spline_unit_dim<K, DIR, D>(C, (int)Wz[L.tdim], 0, prm, xr, y, ld);
+                    NFX_CMARK(2);  // spline
+                }
+#else
                 spline_unit_apply<HT, K, DIR, D, TILES>(W + opaque_zero(), L, C, 1, NT, xb, xr, y, ld);
+#endif
                 if (act) {
                     float yo[D];
 #pragma unroll
@@ -116,6 +144,7 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
             if (half) unit(std::integral_constant<int, 1>{}, half_base);
             ++g;
         }
+        NFX_CMARK(3);
         __syncthreads();
         for (int e = threadIdx.x; e < rows * D; e += NTH) out[r0 * D + e] = sx[e];
         for (int e = threadIdx.x; e < rows; e += NTH) {
@@ -131,6 +160,11 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
         }
         __syncthreads();
     }
+    NFX_CMARK(5);  // slice epilogue
+#ifdef NFX_SCHAIN_TIMING
+    if (blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 4))
+        for (int k = 0; k < 6; ++k) out[(wave ? 6 : 0) + k] = (float)tacc[k];
+#endif
     if constexpr (LOGP) {
         logp_commit<NTH>(lpacc, partials, sums, B);
     }
@@ -140,8 +174,12 @@ typedef void (*spline_schain_t)(NfxChainPacks, int, const float*, float*, float*
                                 int, float*, double*, double*, float);
 
 constexpr int kSplineSchainWaves = 12;
+// Strong-scaled shards (at most one 64-row unit per wave and layer): 8 waves, two per SIMD, which
+// leaves the unit body 256 VGPRs instead of 168 (no scratch spills); the twelve-wave kernel would
+// leave a third of its waves idle there anyway.
+constexpr int kSplineSchainWavesSmall = 8;
 
 template <int HT>
-spline_schain_t spline_schain_pick_ht(int K, int dir, bool logp);
+spline_schain_t spline_schain_pick_ht(int K, int dir, bool logp, bool small);
 
 }  // namespace nfx
