@@ -5,7 +5,7 @@ log_prob), from a timing build:
 Workgroup 0's waves 0 and 4 write their accumulated clock64 ticks per stage into the first 12
 outputs (stage names below, NFX_CMARK order of csrc/nfx_spline_schain_kernel.h). The timing build
 assumes one transformed dim per layer (d = 2). The round-4 stagger experiment's numbers
-(gpurun_out/r04_sct) came from the same marks in that variant of the kernel."""
+(profiles/r04f_stage_clocks/) came from the same marks in that variant of the kernel."""
 import json
 import os
 import sys
