@@ -132,6 +132,11 @@ typedef uint32_t SeqsDesc __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ void seqs_desc_load(const uint32_t* p, SeqsDesc& o) {
     asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(o) : "s"(p) : "memory");
 }
+// Entry at byte offset `off` from the table base (an SGPR offset: one s_add per chunk for the
+// address instead of the 64-bit index arithmetic).
+__device__ __forceinline__ void seqs_desc_load_at(const uint32_t* base, int off, SeqsDesc& o) {
+    asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(o) : "s"(base), "s"(off) : "memory");
+}
 __device__ __forceinline__ void seqs_desc_wait(SeqsDesc& o) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(o)); }
 
 // Keeps the compiler from moving LDS accesses across this point. A wave's DS operations execute
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
         }
         for (int e = lane; e < 4 * kSeqsH3; e += 64) h3_t[e] = 0.f;
         bool poisoned = false;
-        int kc = 0;  // chunk index into the schedule (made_seqs_chunk_kernel)
+        int kc = 0;  // byte offset of the chunk's entry in the schedule (made_seqs_chunk_kernel)
 
         float xr[4];
         int i0 = 0, n = blk_end(0), buf = 0;
@@ -422,12 +427,12 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
             if (nn > 0) x_load(gb, i0n, nn, xr);
             seqs_lds_order();
             SeqsDesc da, db;
-            seqs_desc_load(ctab + 8 * kc, da);
+            seqs_desc_load_at(ctab, kc, da);
 
             NFX_TMARK(6);  // block start: input tile, block end, LDS-DMA and x issue
             auto chunk = [&](SeqsDesc& dc, SeqsDesc& dn) -> bool {
                 seqs_desc_wait(dc);
-                seqs_desc_load(ctab + 8 * (kc + 1), dn);
+                seqs_desc_load_at(ctab, kc + 32, dn);
                 // the chunk's schedule: first step, size, completion, completed units before it
                 const int ii = dc[0] & 0xff, nc = (dc[0] >> 8) & 0xff;
                 const bool completes = (dc[0] >> 16) & 1u, last = (dc[0] >> 18) & 1u;
@@ -544,7 +549,7 @@ __global__ __launch_bounds__(kSeqsThreads) void made_seqs_kernel(
                 }
                 NFX_TMARK(3);  // completion
                 (void)i;
-                ++kc;
+                kc += 32;
                 return last;
             };
             for (;;) {  // two schedule entries alternate: no copy of a scalar load in flight

@@ -207,7 +207,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
         // operands of the chunk at block position ii (rows past the block clamp to its last row:
         // their steps are masked out)
         const uint32_t* ctab = reinterpret_cast<const uint32_t*>(P + L.ctab);
-        auto load_desc = [&](int k, SeqsDesc& o) { seqs_desc_load(ctab + 8 * k, o); };
+        auto load_desc = [&](int kb, SeqsDesc& o) { seqs_desc_load_at(ctab, kb, o); };
         auto load_ops = [&](const float* blk, int ii, SeqwOps<NM>& o) {
             const int rj = ii + jl < kSeqsStep ? ii + jl : kSeqsStep - 1;
             const float* wr = blk + W4F + rj * RS4 + 8 * rq;
@@ -240,7 +240,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
             for (int k = 0; k < 4 * NM; ++k) h3r[k] = 0.f;
             float ldl = 0.f;  // per-lane log-det partial (steps ii + jl of every chunk)
             bool poisoned = false;
-            int kc = 0;  // chunk index into the schedule
+            int kc = 0;  // byte offset of the chunk's entry in the schedule
 
             int i0 = 0, n = blk_end(0), buf = 0, par = 0;
             seqs_lds_barrier();  // A
@@ -262,7 +262,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                 bool done = false;
                 auto chunk = [&](SeqwOps<NM>& c, SeqwOps<NM>& nx, SeqsDesc& dc, SeqsDesc& dn) {
                     seqs_desc_wait(dc);
-                    load_desc(kc + 1, dn);
+                    load_desc(kc + 32, dn);
                     // the chunk's schedule (made_seqs_chunk_kernel): no per-chunk bookkeeping
                     const int ii = dc[0] & 0xff, nc = (dc[0] >> 8) & 0xff;
                     const bool completes = (dc[0] >> 16) & 1u, one = (dc[0] >> 17) & 1u;
@@ -390,7 +390,7 @@ __global__ __launch_bounds__((NWV + 1) * 64) void made_seqw_kernel(
                         }
                     }
                     NFX_WMARK(3);  // completion
-                    ++kc;
+                    kc += 32;
                 };
                 for (;;) {  // two operand / schedule sets alternate: no register copies of loads in flight
                     chunk(opa, opb, da, db);
