@@ -253,10 +253,16 @@ __device__ __forceinline__ f32x16 tchain_from(int k0, const float* wl, int strid
     }
 }
 
-constexpr int kBwdWaves = 8;  // 2 per SIMD; LDS: the padded forward weight image + one x tile per wave
+// Waves per workgroup (LDS: the padded forward weight image + one x tile per wave, one workgroup per
+// CU): 8 (2 per SIMD) for large batches; 4 (1 per SIMD, 512 registers: no scratch spills) when
+// the batch has at most one 32-sample tile per wave of 4-wave workgroups on every CU — the figure
+// models' 2,000 points then run on 16 CUs instead of 8 (0.88 vs 1.04 ms per trainfig_maf step),
+// while cfg4t's 15.6k tiles run faster at 2 waves per SIMD (89.9 vs 85.9 M samples/s).
+constexpr int kBwdWaves = 8;
+constexpr int kBwdWavesSmall = 4;
 
-template <int HT, int VAR>
-__global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
+template <int HT, int VAR, int NW>
+__global__ __launch_bounds__(64 * NW) void made_bwd_kernel(
     const float* __restrict__ packed, const float* __restrict__ in, const float* __restrict__ gout,
     const float* __restrict__ gld_in, float* __restrict__ gin, float* __restrict__ acts, int64_t B, int d,
     int H, int64_t ntiles) {
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
         const f32x4* src = reinterpret_cast<const f32x4*>(packed);
         const int nt1 = HT * NKC_(d), nt23 = HT * HT, nt4 = NJ_(d) * 2 * HT;
         const int ntiles_w = nt1 + 2 * nt23 + nt4;
-        for (int i = threadIdx.x; i < ntiles_w * 256; i += 64 * kBwdWaves) {
+        for (int i = threadIdx.x; i < ntiles_w * 256; i += 64 * NW) {
             const int tl = i >> 8, q = i & 255, rq = q >> 6, ln = q & 63;
             int srco, dsto;
             if (tl < nt1) { srco = L.w1 + tl * 1024; dsto = BL.w1 + tl * kPadTile; }
@@ -279,12 +285,12 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
             else { srco = L.w4 + (tl - nt1 - 2 * nt23) * 1024; dsto = BL.w4 + (tl - nt1 - 2 * nt23) * kPadTile; }
             *reinterpret_cast<f32x4*>(lds + dsto + rq * kPadRQ + ln * 4 + (ln >> 5) * kPadH) = src[(srco >> 2) + q];
         }
-        for (int i = threadIdx.x; i < HT * 32; i += 64 * kBwdWaves) {
+        for (int i = threadIdx.x; i < HT * 32; i += 64 * NW) {
             lds[BL.b1 + i] = packed[L.b1 + i];
             lds[BL.b2 + i] = packed[L.b2 + i];
             lds[BL.b3 + i] = packed[L.b3 + i];
         }
-        for (int i = threadIdx.x; i < NJ_(d) * 64; i += 64 * kBwdWaves) lds[BL.b4 + i] = packed[L.b4 + i];
+        for (int i = threadIdx.x; i < NJ_(d) * 64; i += 64 * NW) lds[BL.b4 + i] = packed[L.b4 + i];
     }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) void made_bwd_kernel(
     };
     const float tsafe = packed[L.tsafe];
 
-    for (int64_t t = (int64_t)blockIdx.x * kBwdWaves + wave; t < ntiles; t += (int64_t)gridDim.x * kBwdWaves) {
+    for (int64_t t = (int64_t)blockIdx.x * NW + wave; t < ntiles; t += (int64_t)gridDim.x * NW) {
         // the per-lane constants are recomputed per tile from threadIdx.x (a few VALU ops) rather
         // than kept live across the loop: at the 256-VGPR budget they would be spilled, and each
         // reload waits behind the tile's factor stores (one in-order vmcnt for loads and stores)
@@ -898,16 +904,27 @@ extern "C" int nfx_made_affine_backward(const float* packed, const float* in, co
         return check_launch("made_bwdw_kernel");
     }
     const MadeLayout L = made_layout(d, HT);
-    const size_t lds = ((size_t)bwd_lds(d, HT).total + (size_t)kBwdWaves * 32 * kTileStride) * sizeof(float);
     (void)L;
     const bool iaf = variant == NFX_IAF_FORWARD;
-    const void* k = HT == 1 ? (iaf ? (const void*)made_bwd_kernel<1, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<1, NFX_MAF_INVERSE>)
-                            : (iaf ? (const void*)made_bwd_kernel<2, NFX_IAF_FORWARD> : (const void*)made_bwd_kernel<2, NFX_MAF_INVERSE>);
+    const int64_t ntiles = (B + 31) / 32;
+    const bool small = ntiles <= (int64_t)kBwdWavesSmall * num_cus();
+    const int nw = small ? kBwdWavesSmall : kBwdWaves;
+    const size_t lds = ((size_t)bwd_lds(d, HT).total + (size_t)nw * 32 * kTileStride) * sizeof(float);
+    const void* k;
+    if (small)
+        k = HT == 1 ? (iaf ? (const void*)made_bwd_kernel<1, NFX_IAF_FORWARD, kBwdWavesSmall>
+                           : (const void*)made_bwd_kernel<1, NFX_MAF_INVERSE, kBwdWavesSmall>)
+                    : (iaf ? (const void*)made_bwd_kernel<2, NFX_IAF_FORWARD, kBwdWavesSmall>
+                           : (const void*)made_bwd_kernel<2, NFX_MAF_INVERSE, kBwdWavesSmall>);
+    else
+        k = HT == 1 ? (iaf ? (const void*)made_bwd_kernel<1, NFX_IAF_FORWARD, kBwdWaves>
+                           : (const void*)made_bwd_kernel<1, NFX_MAF_INVERSE, kBwdWaves>)
+                    : (iaf ? (const void*)made_bwd_kernel<2, NFX_IAF_FORWARD, kBwdWaves>
+                           : (const void*)made_bwd_kernel<2, NFX_MAF_INVERSE, kBwdWaves>);
     int rc = prepare_lds(k, lds);
     if (rc) return rc;
-    const int64_t ntiles = (B + 31) / 32;
-    const int threads = 64 * kBwdWaves;
-    const int grid = resident_grid(k, threads, lds, (ntiles + kBwdWaves - 1) / kBwdWaves);
+    const int threads = 64 * nw;
+    const int grid = resident_grid(k, threads, lds, (ntiles + nw - 1) / nw);
     hipStream_t s = (hipStream_t)stream;
     typedef void (*bwd_t)(const float*, const float*, const float*, const float*, float*, float*, int64_t, int, int,
                           int64_t);
