@@ -232,6 +232,10 @@ int nfx_made_affine(const float* packed, const float* in, float* out, float* log
 #define NFX_MADE_SEQ_AUTO 0
 #define NFX_MADE_SEQ_SEGMENT 1
 #define NFX_MADE_SEQ_WAVE 2
+/* NFX_MADE_SEQ_PUSH: the wave-per-sample PUSH kernel (made_seqp_kernel, d <= 1024): every step's
+ * (mu, alpha) accumulated in registers as units complete, the completing unit's layer-1 sum formed
+ * once; falls back to the wave kernel outside d <= 1024. */
+#define NFX_MADE_SEQ_PUSH 3
 int nfx_made_seq_policy(int policy);
 int nfx_made_affine_logprob(const float* packed, const float* in, float* out, float* log_det,
                             float* logp, double* sums, void* workspace, int64_t B, int d, int H,

@@ -228,6 +228,7 @@ extern "C" size_t nfx_made_packed_floats(int d, int H) {
 }
 
 namespace nfx {
+int made_pack_seqp(int d, int H, float* packed, hipStream_t s);
 // the sequential directions' part of a pack (HT <= 2): the rank-ordered image and the chunk
 // schedule, from the degree tables made_live_kernel wrote
 static int made_pack_seq(int d, int H, float* packed, hipStream_t s) {
@@ -239,7 +240,9 @@ static int made_pack_seq(int d, int H, float* packed, hipStream_t s) {
     if (rc) return rc;
     if (HT == 1) made_seqs_chunk_kernel<1><<<1, 64, 0, s>>>(packed, d, H);
     else made_seqs_chunk_kernel<2><<<1, 64, 0, s>>>(packed, d, H);
-    return check_launch("made_seqs_chunk_kernel");
+    rc = check_launch("made_seqs_chunk_kernel");
+    if (rc) return rc;
+    return made_pack_seqp(d, H, packed, s);
 }
 }  // namespace nfx
 
@@ -285,6 +288,9 @@ namespace nfx {
 int made_seqw_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d, int H,
                      int variant, int accumulate, float* logp, double* partials, double* sums, bool fused,
                      int* grid_out, hipStream_t s);
+int made_seqp_launch(const float* packed, const float* in, float* out, float* log_det, int64_t B, int d, int H,
+                     int variant, int accumulate, float* logp, double* partials, double* sums, bool fused,
+                     hipStream_t s);
 }  // namespace nfx
 
 // Sequential-direction kernel choice (nfx_made_seq_policy): NFX_MADE_SEQ_AUTO (default, or
@@ -385,7 +391,13 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     // short of 2 per SIMD (measured, IAF(784, 64): 74.8 vs 107.9 us at 1,024; 116 vs 138 us at
     // 4,096 for the segment kernel, profiles/r03i_seqw_sweep.jsonl)
     const int seq_pol = made_seq_policy().load(std::memory_order_relaxed);
-    if (seqs && (seq_pol == NFX_MADE_SEQ_WAVE || (seq_pol == NFX_MADE_SEQ_AUTO && B <= 2048 * (int64_t)num_cus() / 256))) {
+    // AUTO: the push kernel while it leads (IAF(784, 64) + log_prob: 31.9 vs 53.5 / 92.7 us at 1,024,
+    // 82.7 vs 137.5 / 94.9 us at 4,096 for the wave / segment kernels; the segment kernel from
+    // 8,192, gpurun_out/r05a/sweep.jsonl)
+    const bool push_auto = seq_pol == NFX_MADE_SEQ_AUTO && B <= 4096 * (int64_t)num_cus() / 256;
+    if (seqs && (seq_pol == NFX_MADE_SEQ_PUSH || push_auto) && L.ps > 0)
+        return made_seqp_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, partials, sums, fused, s);
+    if (seqs && (seq_pol == NFX_MADE_SEQ_PUSH || seq_pol == NFX_MADE_SEQ_WAVE || (seq_pol == NFX_MADE_SEQ_AUTO && B <= 2048 * (int64_t)num_cus() / 256))) {
         int grid = 0;
         return made_seqw_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, partials, sums, fused,
                                 &grid, s);
@@ -414,7 +426,7 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
 
 extern "C" int nfx_made_seq_policy(int policy) {
     if (policy < 0) return made_seq_policy().load();
-    if (policy > NFX_MADE_SEQ_WAVE) return set_error(NFX_EINVAL, "made_seq_policy: unknown policy %d", policy);
+    if (policy > NFX_MADE_SEQ_PUSH) return set_error(NFX_EINVAL, "made_seq_policy: unknown policy %d", policy);
     return made_seq_policy().exchange(policy);
 }
 

@@ -54,6 +54,15 @@ struct MadeLayout {
     int rimg;  // made_seqs_kernel's LDS prologue image (HT <= 2): [w2 | w3 by rank][b1 | b2 | b3 | deg | gend]
     int sw1, sw4, sb4;  // made_seqs_kernel's block-ready step rows (HT <= 2), d + kSeqsPadRows rows each
     int ctab;           // the sequential kernels' chunk schedule (HT <= 2): seqs_max_chunks x 8 words
+    // made_seqp_kernel (HT <= 2, d <= 1024; 0-sized otherwise), units by completion rank g, steps
+    // in 64-step slots s (lane l = step 64 s + l):
+    //   pw4 [Hp][ceil(ps/2)][64][4]  unit g's (mu, alpha) output weights of step 64 s + l, slots
+    //                                 2j and 2j + 1 in one 16-byte piece per lane
+    //   pw1 [Hp][ceil(ps/4)][64][4]  its W1 row, slots 4j .. 4j + 3 per piece
+    //   pb4 [ps][64][2]      (mu, alpha) biases per step
+    //   pw23 [Hp][Hp][2]     row g, lane p = (W2, W3)[rank p][rank g] (unit g's outgoing weights)
+    //   ptb [4][Hp]          b1 | b2 | b3 by rank, degree by rank      ptab: the chunk schedule
+    int ps, pw4, pw1, pb4, pw23, ptb, ptab;
     int total;
 };
 
@@ -67,6 +76,14 @@ constexpr int kSeqsPadRows = 64;
 // Chunks of the sequential schedule: each ends at 16 steps (<= d/16), at a completion (<= Hp) or
 // at a staged block's end (<= d/64 + Hp + 1); + 1 sentinel entry.
 __host__ __device__ constexpr int seqs_max_chunks(int d, int Hp) { return d / 8 + 2 * Hp + 8; }
+// made_seqp_kernel: 64-step slots (0 = not built: HT > 2 or d > 1024); chunks end at a completion
+// (<= Hp; a group of m units of one degree takes 3m chunks), a slot end (<= slots) or the last
+// step; + 1 sentinel entry
+constexpr int kSeqpMaxS = 16;
+__host__ __device__ constexpr int seqp_slots(int d, int HT) {
+    return (HT <= 2 && d <= 64 * kSeqpMaxS) ? (d + 63) / 64 : 0;
+}
+__host__ __device__ constexpr int seqp_max_chunks(int d, int Hp) { return (d + 63) / 64 + 3 * Hp + 4; }
 
 __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     MadeLayout L{};
@@ -111,6 +128,15 @@ __host__ __device__ constexpr MadeLayout made_layout(int d, int HT) {
     L.sw4 = o; o += made_up4(rows * seqs_w4_stride(L.Hp));
     L.sb4 = o; o += made_up4(2 * rows);
     L.ctab = o; o += HT <= 2 ? 8 * seqs_max_chunks(d, L.Hp) : 0;
+    // made_seqp_kernel's images (HT <= 2, d <= 1024; nfx_made_seqp_kernel.h)
+    const int PS = seqp_slots(d, HT);
+    L.ps = PS;
+    L.pw4 = o; o += L.Hp * ((PS + 1) / 2) * 256;
+    L.pw1 = o; o += L.Hp * ((PS + 3) / 4) * 256;
+    L.pb4 = o; o += PS * 128;
+    L.pw23 = o; o += PS ? 2 * L.Hp * L.Hp : 0;
+    L.ptb = o; o += PS ? 4 * L.Hp : 0;
+    L.ptab = o; o += PS ? 16 * seqp_max_chunks(d, L.Hp) : 0;
     L.total = o;
     return L;
 }

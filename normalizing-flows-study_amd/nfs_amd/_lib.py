@@ -28,6 +28,7 @@ NFX_AFFINE_SMALL = 2
 NFX_MADE_SEQ_AUTO = 0
 NFX_MADE_SEQ_SEGMENT = 1
 NFX_MADE_SEQ_WAVE = 2
+NFX_MADE_SEQ_PUSH = 3
 
 # Every symbol include/nfx.h declares (tests check the built library exports all of them).
 EXPORTED_SYMBOLS = (

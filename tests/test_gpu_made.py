@@ -16,13 +16,17 @@ from conftest import golden_json, load_golden, oracle_sd, state_dict_from
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["wave", "segment"])
+_SEQ_POLICIES = {"wave": "NFX_MADE_SEQ_WAVE", "segment": "NFX_MADE_SEQ_SEGMENT", "push": "NFX_MADE_SEQ_PUSH"}
+
+
+@pytest.fixture(params=["wave", "segment", "push"])
 def seq_policy(request, cuda_device):
-    """Run a test on both sequential-direction kernels (nfx_made_seq_policy): the wave-per-sample
-    made_seqw_kernel (default) and the segment-parallel made_seqs_kernel."""
+    """Run a test on every sequential-direction kernel (nfx_made_seq_policy): the wave-per-sample
+    made_seqw_kernel, the segment-parallel made_seqs_kernel and the push-formulation
+    made_seqp_kernel (d <= 1024; the wave kernel beyond)."""
     from nfs_amd import _lib
     L = _lib.lib()
-    old = L.nfx_made_seq_policy(_lib.NFX_MADE_SEQ_WAVE if request.param == "wave" else _lib.NFX_MADE_SEQ_SEGMENT)
+    old = L.nfx_made_seq_policy(getattr(_lib, _SEQ_POLICIES[request.param]))
     yield request.param
     L.nfx_made_seq_policy(old)
 

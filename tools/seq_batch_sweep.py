@@ -1,6 +1,6 @@
 """Sequential IAF(784, 64) inverse (cfg5i shape) + fused Gaussian log_prob: kernel time per
 batch size for each sequential-MADE kernel (nfx_made_seq_policy: wave-per-sample made_seqw_kernel
-vs segment-parallel made_seqs_kernel), HIP events around the log_prob call.
+vs segment-parallel made_seqs_kernel vs push made_seqp_kernel), HIP events around the log_prob call.
 
     python tools/seq_batch_sweep.py [B ...]
 """
@@ -26,7 +26,8 @@ batches = [int(b) for b in sys.argv[1:]] or [256, 512, 1024, 2048, 4096, 8192, 1
 for B in batches:
     x = torch.randn(B, d, device="cuda")
     row = {"B": B}
-    for name, pol in (("wave", _lib.NFX_MADE_SEQ_WAVE), ("segment", _lib.NFX_MADE_SEQ_SEGMENT)):
+    for name, pol in (("wave", _lib.NFX_MADE_SEQ_WAVE), ("segment", _lib.NFX_MADE_SEQ_SEGMENT),
+                      ("push", _lib.NFX_MADE_SEQ_PUSH)):
         L.nfx_made_seq_policy(pol)
         with torch.no_grad():
             for _ in range(2):
