@@ -49,6 +49,12 @@ class GraphedFlow:
         self.mode = mode
         self.strict = strict
         self.static_in = example.detach().clone().contiguous()
+        # the graph's own log_prob workspace (float64 partials + arrival counter): replays of two
+        # graphs, or a replay beside eager calls, never share one
+        self.workspace = None
+        if mode == "log_prob":
+            from .models.normalizing_flow_model import new_gauss_workspace
+            self.workspace = new_gauss_workspace(example.shape[0], example.device)
         fn = self._call
         stream = torch.cuda.Stream(device=example.device)
         stream.wait_stream(torch.cuda.current_stream(example.device))
@@ -71,7 +77,7 @@ class GraphedFlow:
             self.static_in.normal_()
             return self.model.forward(self.static_in)
         if self.mode == "log_prob":
-            return self.model.log_prob(self.static_in, return_sums=True)
+            return self.model.log_prob(self.static_in, return_sums=True, workspace=self.workspace)
         if self.mode == "forward":
             return self.model.forward(self.static_in)
         return self.model.inverse(self.static_in)

@@ -186,23 +186,26 @@ class NormalizingFlowModel(nn.Module):
         return cur, ld
 
     # -- log-density -------------------------------------------------------------------------
-    def log_prob(self, x, return_sums=False):
+    def log_prob(self, x, return_sums=False, workspace=None):
         """log p(x) = log N(z; 0, I) + log|det J_inv| per sample, z = inverse(x).
 
         With return_sums=True also returns a float64 tensor [sum_i log p(x_i), B] on x's device
-        (the partial a data-parallel NLL all-reduces)."""
+        (the partial a data-parallel NLL all-reduces). `workspace`: the fused epilogue's float64
+        partials + arrival counter (uint8 tensor of at least nfx_gauss_workspace_bytes(B) bytes,
+        zero-filled once); by default one cached per (device, current stream), so calls on
+        different streams never share one."""
         if self._hip_chain_ok(x) and len(self.flows) > 0:
             B = x.shape[0]
             logp = torch.empty(B, device=x.device, dtype=torch.float32)
             sums = torch.empty(2, device=x.device, dtype=torch.float64)
-            ws = gauss_workspace(B, x.device)
+            ws = check_gauss_workspace(workspace, B, x.device) if workspace is not None else gauss_workspace(B, x.device)
             z, ld, fused = self._hip_chain(x, -1, logprob=(logp, sums, ws))
             if not fused:
                 gauss_logprob(z, ld, logp, sums, ws)
             return (logp, sums) if return_sums else logp
         z, ld = self.inverse(x)
         if z.device.type == "cuda" and z.dtype == torch.float32 and not self._needs_grad(x):
-            logp, sums = gauss_logprob(z, ld)
+            logp, sums = gauss_logprob(z, ld, ws=workspace)
         else:
             d = z.shape[1]
             logp = -0.5 * (d * math.log(2 * math.pi) + z.pow(2).sum(-1)) + ld
@@ -222,19 +225,36 @@ class NormalizingFlowModel(nn.Module):
 _GAUSS_WS = {}
 
 
-def gauss_workspace(B, device):
+def gauss_workspace(B, device, stream=None):
     """The per-workgroup float64 partial sums + arrival counter of the fused log_prob epilogues
-    (nfx_gauss_workspace_bytes): zero-filled once and cached per device — every launch's last
-    workgroup resets the counter, so the buffer stays valid call after call and inside captured
-    graphs. Launches are stream-ordered; callers running log_prob concurrently on two streams of
-    one device pass their own zero-filled workspace."""
+    (nfx_gauss_workspace_bytes): zero-filled once and cached per (device, stream) — every launch's
+    last workgroup resets the counter, so the buffer stays valid call after call on its stream.
+    Launches on one stream are ordered; two streams never share a workspace (concurrent launches
+    on one would race on its counter and partials). Captured graphs (GraphedFlow) own theirs."""
     dev = torch.device(device)
-    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    if dev.type == "cuda":
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        st = stream if stream is not None else torch.cuda.current_stream(idx)
+        key = (dev.type, idx, int(st.cuda_stream))
+    else:
+        key = (dev.type, dev.index, 0)
     n = _lib.lib().nfx_gauss_workspace_bytes(B)
     ws = _GAUSS_WS.get(key)
     if ws is None or ws.numel() < n:
         ws = torch.zeros(n, device=dev, dtype=torch.uint8)
         _GAUSS_WS[key] = ws
+    return ws
+
+
+def new_gauss_workspace(B, device):
+    """A fresh zero-filled log_prob workspace for B samples (for callers that own one)."""
+    return torch.zeros(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
+
+
+def check_gauss_workspace(ws, B, device):
+    n = _lib.lib().nfx_gauss_workspace_bytes(B)
+    if ws.dtype != torch.uint8 or ws.device != torch.device(device) or ws.numel() < n or not ws.is_contiguous():
+        raise ValueError(f"log_prob workspace: need a contiguous uint8 tensor of >= {n} bytes on {device}")
     return ws
 
 
@@ -247,8 +267,7 @@ def gauss_logprob(z, ld, logp=None, sums=None, ws=None):
     if sums is None:
         sums = torch.empty(2, device=z.device, dtype=torch.float64)
     L = _lib.lib()
-    if ws is None:
-        ws = gauss_workspace(B, z.device)
+    ws = gauss_workspace(B, z.device) if ws is None else check_gauss_workspace(ws, B, z.device)
     _lib.check(L.nfx_gauss_logprob(_lib.ptr(z), _lib.ptr(ld), _lib.ptr(logp), _lib.ptr(sums),
                                    _lib.ptr(ws), B, d, _lib.stream_of(z)), "nfx_gauss_logprob")
     STATS["hip"] += 1

@@ -27,8 +27,8 @@ class RealNVP(nn.Module):
     def inverse(self, x):
         return self.flow.inverse(x)
 
-    def log_prob(self, x, return_sums=False):
-        return self.flow.log_prob(x, return_sums=return_sums)
+    def log_prob(self, x, return_sums=False, workspace=None):
+        return self.flow.log_prob(x, return_sums=return_sums, workspace=workspace)
 
     def nll(self, x):
         return self.flow.nll(x)

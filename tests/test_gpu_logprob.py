@@ -204,3 +204,61 @@ def test_graphed_sampling(cuda_device):
     assert abs(zs.mean().item()) < 0.05 and abs(zs.std().item() - 1) < 0.05
     with pytest.raises(ValueError):
         g(z1)
+
+
+@pytest.mark.parametrize("kind", ["realnvp", "maf63", "iaf150_sequential"])
+def test_concurrent_streams_own_workspaces(cuda_device, kind):
+    """Two log_prob calls issued on two streams at once (different inputs) and two captured
+    graphs replayed on two streams: each uses its own workspace (per-stream cache, the graphs'
+    own), so every NLL partial equals its serial value bit for bit (a shared arrival counter /
+    partials array would let the launches corrupt each other's sums)."""
+    m, d, _ = _model(kind)
+    m = m.to(cuda_device).eval()
+    B1, B2 = (300_001, 200_003) if not kind.startswith("iaf") else (4099, 3001)
+    g = torch.Generator().manual_seed(5)
+    xa = torch.randn(B1, d, generator=g).to(cuda_device)
+    xb = torch.randn(B2, d, generator=g).to(cuda_device)
+    with torch.no_grad():
+        la, sa = m.log_prob(xa, return_sums=True)
+        lb, sb = m.log_prob(xb, return_sums=True)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(4):
+        s1.wait_stream(torch.cuda.current_stream())
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.no_grad():
+            with torch.cuda.stream(s1):
+                la2, sa2 = m.log_prob(xa, return_sums=True)
+            with torch.cuda.stream(s2):
+                lb2, sb2 = m.log_prob(xb, return_sums=True)
+        torch.cuda.synchronize()
+        assert torch.equal(sa2, sa) and torch.equal(sb2, sb)
+        assert torch.equal(la2, la) and torch.equal(lb2, lb)
+    ga = nfs_amd.GraphedFlow(m, xa, mode="log_prob")
+    gb = nfs_amd.GraphedFlow(m, xb, mode="log_prob")
+    assert ga.workspace.data_ptr() != gb.workspace.data_ptr()
+    for _ in range(4):
+        s1.wait_stream(torch.cuda.current_stream())
+        s2.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s1):
+            ra = ga()
+        with torch.cuda.stream(s2):
+            rb = gb()
+        torch.cuda.synchronize()
+        assert torch.equal(ra[1], sa) and torch.equal(rb[1], sb)
+
+
+def test_log_prob_caller_workspace(cuda_device):
+    """log_prob(x, workspace=...) runs on a caller-owned zero-filled workspace (and rejects one
+    that is too small)."""
+    from nfs_amd.models.normalizing_flow_model import new_gauss_workspace
+    m, d, _ = _model("spline_k5")
+    m = m.to(cuda_device).eval()
+    x = torch.randn(5000, d, device=cuda_device)
+    ws = new_gauss_workspace(5000, cuda_device)
+    with torch.no_grad():
+        lp, s = m.log_prob(x, return_sums=True)
+        lp2, s2 = m.log_prob(x, return_sums=True, workspace=ws)
+        with pytest.raises(ValueError):
+            m.log_prob(x, return_sums=True, workspace=ws[:8])
+    assert torch.equal(lp, lp2) and torch.equal(s, s2)
