@@ -182,6 +182,14 @@ int nfx_rqs_unit(const float* in, const float* widths, const float* heights,
                  const float* derivatives, float* out, float* log_det, int64_t N, int K,
                  float min_bin_width, float min_bin_height, float min_derivative, int inverse,
                  void* stream);
+/* Its adjoint (autograd of the same function, torch semantics: clamps pass the gradient on
+ * their closed range, bin selection carries none): grad_out, grad_log_det [N] in; grad_in [N],
+ * grad_widths / grad_heights [N,K], grad_derivatives [N,K-1] out (overwritten). */
+int nfx_rqs_unit_backward(const float* in, const float* widths, const float* heights,
+                          const float* derivatives, const float* grad_out, const float* grad_log_det,
+                          float* grad_in, float* grad_widths, float* grad_heights, float* grad_derivatives,
+                          int64_t N, int K, float min_bin_width, float min_bin_height, float min_derivative,
+                          int inverse, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * ARQS — autoregressive unit-interval RQ spline flow (src/flows/spline/arqs.py:7-114):

@@ -1,5 +1,6 @@
 // Backward of the SEQUENTIAL MADE directions with a WAVE per sample (H <= 64) — the small-batch
-// counterpart of made_seq_bwd_kernel (nfx_made_seqbwd.hip; same math, same outputs):
+// counterpart of made_seq_bwd_kernel (nfx_made_seqbwd.hip; same math, results within tolerance:
+// the recomputed mu/alpha sum by butterfly, not in the forward kernels' order):
 // InverseAutoregressiveFlow.inverse (inverse_autoregressive_flow.py:65-103, the IAF density
 // direction) and MaskedAutoregressiveFlow.forward (masked_autoregressive_flow.py:46-78) under
 // autograd, e.g. the reference's 6x IAF(2, 64) figure model trained full-batch on 2,000 points

@@ -28,7 +28,7 @@ from . import generic as _generic
 from .flow import HipFlow, STATS
 
 MAX_H = 256       # eval kernels (H > 128: nfx_made_big.hip)
-MAX_H_BWD = 128   # fused backward kernels; wider layers differentiate through the composite
+MAX_H_BWD = 128   # fused backward kernels; wider layers: the any-shape path (csrc/nfx_generic.hip)
 MAX_D = 4096
 # Tests: route every call through the any-shape path (csrc/nfx_generic.hip) even where a fused
 # kernel exists, to pin it against the same fixtures.
@@ -406,7 +406,10 @@ class _MadeAffineFlow(HipFlow):
         if variant in (_lib.NFX_MAF_FORWARD, _lib.NFX_IAF_INVERSE) and not getattr(packed, "_nfx_seq", True):
             _lib.check(_lib.lib().nfx_made_pack_sequential(self.dim, self.conditioner.hidden_dim, _lib.ptr(packed),
                                                            _lib.stream_of(packed)), "nfx_made_pack_sequential")
-            packed._nfx_seq = True
+            # under graph capture the build is only recorded: an eager call before the first
+            # replay must build it again
+            if not torch.cuda.is_current_stream_capturing():
+                packed._nfx_seq = True
         return packed
 
     # -- training: fused backward of every direction (§8(f) item 1) --------------------------

@@ -44,6 +44,10 @@ TRAIN_EVENTS = None
 # library accepts (nfx_affine_chain_supported) up to this many samples; 0 disables them (tests
 # compare them with the per-layer kernels).
 CHAIN_MAX_B = int(os.environ.get("NFX_CHAIN_MAX_B", str(1 << 62)))
+# Stacks with H > 64 have no streaming chain: above this many samples they run the per-layer
+# streaming kernels (their MFMA tiling, measured in rounds 2-3) rather than the small-batch chain,
+# whose large-batch rate at H > 64 has not been measured against them.
+CHAIN_MAX_B_WIDE = int(os.environ.get("NFX_CHAIN_MAX_B_WIDE", str(1 << 16)))
 # Tests: route every call through the any-shape path (csrc/nfx_generic.hip) even where a fused
 # kernel exists, to pin it against the same fixtures.
 FORCE_GENERIC = False
@@ -61,6 +65,8 @@ def chain_ok(flows, x):
         return False
     d, H = f0.data_dim, f0._hidden()
     if d not in (2, 4, 8) or H > MAX_H or x.shape[1] != d:
+        return False
+    if H > 64 and x.shape[0] > CHAIN_MAX_B_WIDE:
         return False
     if not _lib.lib().nfx_affine_chain_supported(x.shape[0], d, H):
         return False

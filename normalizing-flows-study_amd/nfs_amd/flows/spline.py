@@ -510,26 +510,51 @@ def rational_quadratic_spline(inputs, widths, heights, derivatives, inverse=Fals
                               epsilon=1e-6):
     """Unit-interval RQ spline (src/flows/spline/rational_quadratic_spline.py:4-104).
 
-    1-D inputs [N] with widths/heights [N,K], derivatives [N,K-1]. fp32 on a ROCm device runs
-    the elementwise gfx950 kernel; anything else (CPU, fp64, autograd) the composite."""
-    needs_grad = torch.is_grad_enabled() and any(
-        t.requires_grad for t in (inputs, widths, heights, derivatives))
-    if (inputs.device.type == "cuda" and inputs.dtype == torch.float32 and inputs.dim() == 1
-            and not needs_grad):
-        return _rqs_unit_hip(inputs, widths, heights, derivatives, inverse, min_bin_width,
-                             min_bin_height, min_derivative)
-    STATS["torch"] += 1
-    return _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,
-                           min_bin_height, min_derivative)
+    Elementwise over inputs of any shape S with widths/heights [*S, K] and derivatives
+    [*S, K - 1]. fp32 on a ROCm device runs the gfx950 kernels — nfx_rqs_unit forward and, under
+    autograd, nfx_rqs_unit_backward (gradients for inputs and all three parameter tensors); CPU
+    tensors run the composite. A GPU call outside the kernels (another dtype, K outside 2..16,
+    shapes that need broadcasting) raises NotImplementedError / ValueError, as every layer does,
+    unless nfs_amd.flows.flow.ALLOW_TORCH_FALLBACK is set."""
+    if inputs.device.type != "cuda":
+        STATS["torch"] += 1
+        return _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,
+                               min_bin_height, min_derivative)
+    from . import flow as _flow
+    K = widths.shape[-1] if widths.dim() else 0
+    S = tuple(inputs.shape)
+    why = None
+    if any(t.dtype != torch.float32 for t in (inputs, widths, heights, derivatives)):
+        why = "fp32 tensors only"
+    elif not 2 <= K <= 16:
+        why = f"K={K} outside 2..16"
+    elif (tuple(widths.shape) != S + (K,) or tuple(heights.shape) != S + (K,)
+          or tuple(derivatives.shape) != S + (K - 1,)):
+        if not _flow.ALLOW_TORCH_FALLBACK:
+            raise ValueError(f"rational_quadratic_spline: inputs {S} need widths/heights {S + (K,)} and "
+                             f"derivatives {S + (K - 1,)} (got {tuple(widths.shape)}, {tuple(heights.shape)}, "
+                             f"{tuple(derivatives.shape)}; broadcasting is not supported on the GPU)")
+        why = "broadcast shapes"
+    if why is not None:
+        if not _flow.ALLOW_TORCH_FALLBACK:
+            raise NotImplementedError(f"rational_quadratic_spline: no gfx950 kernel for this call ({why}); "
+                                      f"set nfs_amd.flows.flow.ALLOW_TORCH_FALLBACK=True to run eager PyTorch")
+        STATS["torch"] += 1
+        return _rqs_unit_torch(inputs, widths, heights, derivatives, inverse, min_bin_width,
+                               min_bin_height, min_derivative)
+    consts = (float(min_bin_width), float(min_bin_height), float(min_derivative), bool(inverse))
+    if torch.is_grad_enabled() and any(t.requires_grad for t in (inputs, widths, heights, derivatives)):
+        return _RqsUnitFn.apply(inputs, widths, heights, derivatives, consts)
+    out, ld = _rqs_unit_hip(inputs.reshape(-1), widths.reshape(-1, K), heights.reshape(-1, K),
+                            derivatives.reshape(-1, K - 1), *consts)
+    return out.view(S), ld.view(S)
 
 
-def _rqs_unit_hip(inputs, widths, heights, derivatives, inverse, min_w, min_h, min_d):
+def _rqs_unit_hip(inputs, widths, heights, derivatives, min_w, min_h, min_d, inverse):
     N = inputs.shape[0]
     K = widths.shape[-1]
-    if widths.shape != (N, K) or heights.shape != (N, K) or derivatives.shape != (N, K - 1):
-        raise ValueError("rational_quadratic_spline: expected widths/heights [N,K] and derivatives [N,K-1]")
     x = inputs.contiguous()
-    uw, uh, ud = widths.contiguous().float(), heights.contiguous().float(), derivatives.contiguous().float()
+    uw, uh, ud = widths.contiguous(), heights.contiguous(), derivatives.contiguous()
     out = torch.empty_like(x)
     ld = torch.empty_like(x)
     _lib.check(_lib.lib().nfx_rqs_unit(
@@ -538,3 +563,36 @@ def _rqs_unit_hip(inputs, widths, heights, derivatives, inverse, min_w, min_h, m
         "nfx_rqs_unit")
     STATS["hip"] += 1
     return out, ld
+
+
+class _RqsUnitFn(torch.autograd.Function):
+    """The unit RQ spline under autograd: nfx_rqs_unit forward, nfx_rqs_unit_backward (the
+    elementwise adjoint of rational_quadratic_spline.py:4-104) backward."""
+
+    @staticmethod
+    def forward(ctx, inputs, widths, heights, derivatives, consts):
+        S, K = tuple(inputs.shape), widths.shape[-1]
+        x = inputs.reshape(-1).contiguous()
+        uw = widths.reshape(-1, K).contiguous()
+        uh = heights.reshape(-1, K).contiguous()
+        ud = derivatives.reshape(-1, K - 1).contiguous()
+        out, ld = _rqs_unit_hip(x, uw, uh, ud, *consts)
+        ctx.save_for_backward(x, uw, uh, ud)
+        ctx.consts, ctx.S = consts, S
+        return out.view(S), ld.view(S)
+
+    @staticmethod
+    def backward(ctx, g_out, g_ld):
+        x, uw, uh, ud = ctx.saved_tensors
+        min_w, min_h, min_d, inverse = ctx.consts
+        N, K = x.shape[0], uw.shape[1]
+        go = torch.zeros_like(x) if g_out is None else g_out.reshape(-1).contiguous().float()
+        gl = torch.zeros_like(x) if g_ld is None else g_ld.reshape(-1).contiguous().float()
+        gx, gw, gh, gd = torch.empty_like(x), torch.empty_like(uw), torch.empty_like(uh), torch.empty_like(ud)
+        p = _lib.ptr
+        _lib.check(_lib.lib().nfx_rqs_unit_backward(
+            p(x), p(uw), p(uh), p(ud), p(go), p(gl), p(gx), p(gw), p(gh), p(gd), N, K, min_w, min_h, min_d,
+            int(inverse), _lib.stream_of(x)), "nfx_rqs_unit_backward")
+        STATS["hip"] += 1
+        S = ctx.S
+        return gx.view(S), gw.view(S + (K,)), gh.view(S + (K,)), gd.view(S + (K - 1,)), None

@@ -39,6 +39,8 @@ no layer is the identity, runs them on seeded inputs, and writes plain arrays:
   g17_options.npz     the remaining constructor options under autograd: train-mode use_batch_norm=True
                       in IAF density (2-layer model step) and MAF sampling, ARQS with BatchNorm in train
                       mode (both directions), SplineCouplingLayer with per-dimension data_min/data_max
+  g18_arqs_bounds.npz ARQS with data_min/data_max (per-dimension tensors and python floats), eval,
+                      both directions under autograd: y, ld, dL/dx, every parameter gradient
   g8_full_nll.json    oracle NLL scalars (float64) at the full BASELINE batch sizes (+ cfg5: IAF(784,64)
                       inverse NLL at B=8192 and forward checksums at B=524288)
 
@@ -705,6 +707,48 @@ def g17(flows, models):
     print("g17 written", flush=True)
 
 
+def g18(flows):
+    """ARQS with data bounds under autograd (arqs.py:28-42 rescale, :44-114 both
+    directions): eval mode, loss L = sum(y wy) + sum(ld wl), each direction from the same state.
+      arqsdm  ARQS(3, 32, num_bins=6, data_min/data_max = per-dimension tensors)
+      arqssc  ARQS(4, 24, num_bins=5, data_min=-2.5, data_max=3.0) (python float bounds)
+    Per case: y, ld, dL/dx and every parameter gradient."""
+    out = {}
+    g = torch.Generator().manual_seed(180)
+
+    def case(name, build, B, scale):
+        torch.manual_seed(1800 + len(name))
+        f = build()
+        perturb(f, 0.1, 1810 + len(name))
+        f.eval()
+        init = {k: v.detach().clone() for k, v in f.state_dict().items()}
+        out.update(sd_arrays(f, name + ".init."))
+        d = f.dim
+        xx = torch.randn(B, d, generator=g) * scale
+        wy = torch.randn(B, d, generator=g)
+        wl = torch.randn(B, generator=g)
+        out.update({f"{name}.x": xx.numpy(), f"{name}.wy": wy.numpy(), f"{name}.wl": wl.numpy()})
+        for dname in ("fwd", "inv"):
+            f.load_state_dict(init)
+            f.zero_grad()
+            xr = xx.clone().requires_grad_(True)
+            y, ldd = (f.forward if dname == "fwd" else f.inverse)(xr)
+            ((y * wy).sum() + (ldd * wl).sum()).backward()
+            out[f"{name}.{dname}.y"] = y.detach().numpy()
+            out[f"{name}.{dname}.ld"] = ldd.detach().numpy()
+            out[f"{name}.{dname}.gx"] = xr.grad.numpy()
+            for k, p in f.named_parameters():
+                out[f"{name}.{dname}.grad.{k}"] = p.grad.numpy()
+
+    dmin, dmax = torch.tensor([-3.0, -2.0, -4.0]), torch.tensor([3.0, 2.5, 1.0])
+    out["arqsdm.data_min"], out["arqsdm.data_max"] = dmin.numpy(), dmax.numpy()
+    case("arqsdm", lambda: flows.ARQS(3, 32, num_bins=6, data_min=dmin, data_max=dmax), 300, 1.2)
+    out["arqssc.data_min"], out["arqssc.data_max"] = np.float64(-2.5), np.float64(3.0)
+    case("arqssc", lambda: flows.ARQS(4, 24, num_bins=5, data_min=-2.5, data_max=3.0), 256, 1.0)
+    np.savez_compressed(os.path.join(HERE, "g18_arqs_bounds.npz"), **out)
+    print("g18 written", flush=True)
+
+
 def g8_cfg5(f6):
     """cfg5 IAF(784,64) (G6 weights): inverse NLL at B=8192 (seed 1237) and forward checksums at
     B=524288 (seed 1238); merged into g8_full_nll.json."""
@@ -805,6 +849,9 @@ def main():
     if a.only == "g17":
         g17(flows, models)
         return
+    if a.only == "g18":
+        g18(flows)
+        return
     if a.only == "g8_cfg5":
         g8_cfg5(g6(flows))
         return
@@ -824,6 +871,7 @@ def main():
     g15(models)
     g16(flows, models)
     g17(flows, models)
+    g18(flows)
     if not a.skip_full:
         g8(m2, m3, m5)
         g8_cfg5(f6)

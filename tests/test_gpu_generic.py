@@ -454,11 +454,9 @@ def test_arqs_backward_vs_float64_autograd(cuda_device, d, H, K, direction):
 @pytest.mark.parametrize("name", ["a1", "a3", "a5", "a4bn", "a10"])
 def test_generic_arqs_vs_reference_g10(cuda_device, name):
     """The any-shape ARQS steps (mode 0, also the backward's recompute) forced onto the
-    reference's ARQS fixtures (G10): outputs and log-dets under the fused kernel's parity test.
-    (Fixtures with data_min/data_max stay on the fused kernel: the any-shape path takes None.)"""
-    from test_gpu_arqs import _case, test_arqs_vs_reference
-    if _case(load_golden("g10_arqs.npz"), name)[4]:
-        pytest.skip("data_min/data_max rescale: fused kernel only")
+    reference's ARQS fixtures (G10): outputs and log-dets under the fused kernel's parity test
+    (a10 carries scalar data_min/data_max: the any-shape path rescales with nfx_arqs_bounds)."""
+    from test_gpu_arqs import test_arqs_vs_reference
     old = _aq.FORCE_GENERIC
     _aq.FORCE_GENERIC = True
     try:
@@ -490,14 +488,12 @@ def _made_bn(cls, d, H, seed):
 def test_generic_made_batchnorm_backward_vs_float64(cuda_device, cls, dname, d, H, mode):
     """MADE(use_batch_norm=True) under autograd. eval: running-statistics BatchNorm, both
     directions (the sequential ones by the triangular adjoint through the BatchNorm'ed MADE);
-    train: batch-statistics BatchNorm with the running update, the parallel directions (MAF
-    inverse, IAF forward). Against float64 autograd of the same module (outputs, dL/dx, every
-    parameter gradient, running statistics after the step)."""
+    train: batch-statistics BatchNorm with the running update, both directions (the sequential
+    ones as the reference's d MADE calls, each with its own batch statistics and running update,
+    differentiated call by call). Against float64 autograd of the same module (outputs, dL/dx,
+    every parameter gradient, running statistics after the step)."""
     from test_gpu_grad_fixtures import _grad_close, _run
     klass = nfs_amd.MaskedAutoregressiveFlow if cls == "maf" else nfs_amd.InverseAutoregressiveFlow
-    parallel = (cls == "maf") == (dname == "inv")
-    if mode == "train" and not parallel:
-        pytest.skip("train-mode BatchNorm in a sequential direction: torch composite (d batch-stat calls)")
     f = _made_bn(klass, d, H, d * 7 + H)
     f = f.train() if mode == "train" else f.eval()
     g = torch.Generator().manual_seed(d + H)

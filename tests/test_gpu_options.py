@@ -183,7 +183,8 @@ def test_arqs_per_dimension_bounds_and_eval_bn_backward(cuda_device, dname, bn):
     them over every dim) and, with bn, an eval-mode BatchNorm MADE, under autograd on the any-shape
     path (nfx_arqs_bounds + the reverse sweep with the running statistics): y, log-det, dL/dx and
     every parameter gradient vs float64 autograd of the same module, side by side with the fp32
-    composite on the CPU (parity unpinned by a reference fixture: G10 holds scalar bounds only)."""
+    composite on the CPU (the eval-BN combination; the bounds themselves are pinned to the
+    reference's own outputs and gradients by test_arqs_bounds_vs_reference_g18)."""
     from nfs_amd.flows.arqs import ARQS
     torch.manual_seed(41)
     f = ARQS(3, 24, num_bins=4, data_min=torch.tensor([-2.0, -1.0, -3.0]), data_max=torch.tensor([2.0, 3.0, 1.5]),
@@ -219,3 +220,44 @@ def test_arqs_per_dimension_bounds_and_eval_bn_backward(cuda_device, dname, bn):
         _gclose(a, b, what, r, frac=2e-5)
     for a, b, r in zip(rg[3], r64[3], r32[3]):
         _gclose(a, b, "param grad", r)
+
+
+@pytest.mark.parametrize("dname", ["fwd", "inv"])
+@pytest.mark.parametrize("case", ["arqsdm", "arqssc"])
+def test_arqs_bounds_vs_reference_g18(cuda_device, case, dname):
+    """G18 (tests/golden/make_golden.py:g18): ARQS with data_min / data_max — per-dimension tensors
+    (arqsdm: ARQS(3, 32, K = 6)) and python floats (arqssc: ARQS(4, 24, K = 5)) — eval mode, both
+    directions under L = sum(y wy) + sum(ld wl) (arqs.py:28-42 rescale, :44-114 the sequential
+    steps): y, log-det, dL/dx and every parameter gradient against the reference's own values, with
+    float64 autograd of the same module as the yardstick; every call HIP."""
+    from nfs_amd.flows.arqs import ARQS
+    g = load_golden("g18_arqs_bounds.npz")
+    if case == "arqsdm":
+        dmin, dmax = torch.from_numpy(g["arqsdm.data_min"]), torch.from_numpy(g["arqsdm.data_max"])
+        f = ARQS(3, 32, num_bins=6, data_min=dmin, data_max=dmax)
+    else:
+        f = ARQS(4, 24, num_bins=5, data_min=float(g["arqssc.data_min"]), data_max=float(g["arqssc.data_max"]))
+    f = _load(f, g, case + ".init.").eval()
+    f64 = copy.deepcopy(f).double()
+    if case == "arqsdm":
+        f64.data_min, f64.data_max = f.data_min.double(), f.data_max.double()
+    x = torch.from_numpy(g[case + ".x"])
+    wy, wl = torch.from_numpy(g[case + ".wy"]), torch.from_numpy(g[case + ".wl"])
+    gpu = f.to(cuda_device)
+    if case == "arqsdm":
+        gpu.data_min, gpu.data_max = f.data_min.to(cuda_device), f.data_max.to(cuda_device)
+    nfs_amd.reset_stats()
+    xr = x.to(cuda_device).requires_grad_(True)
+    y, ld = (gpu.forward if dname == "fwd" else gpu.inverse)(xr)
+    ((y * wy.to(cuda_device)).sum() + (ld * wl.to(cuda_device)).sum()).backward()
+    assert nfs_amd.STATS["torch"] == 0 and nfs_amd.STATS["hip"] >= 1, nfs_amd.STATS
+    x64 = x.double().requires_grad_(True)
+    y64, ld64 = (f64.forward if dname == "fwd" else f64.inverse)(x64)
+    ((y64 * wy.double()).sum() + (ld64 * wl.double()).sum()).backward()
+    pre = f"{case}.{dname}."
+    _gclose(y, g[pre + "y"], "y", y64, frac=2e-5)
+    _gclose(ld, g[pre + "ld"], "ld", ld64, frac=2e-5)
+    _gclose(xr.grad, g[pre + "gx"], "dL/dx", x64.grad)
+    sc = _gscale(f64)
+    for (k, p), (_, p64) in zip(gpu.named_parameters(), f64.named_parameters()):
+        _gclose(p.grad, g[pre + "grad." + k], what=k, ref32=p64.grad, scale=sc)

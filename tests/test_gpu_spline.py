@@ -217,3 +217,76 @@ def test_spline_extreme_logits_vs_oracle(cuda_device, K):
         sy, sl = fp32_jitter(lambda s, v: oracle.spline_coupling(s, "", v, direction, K=K), x, sd=sd)
         assert_fp32_parity(yg.cpu(), yr, y64, what=f"y dir={direction}", sens=sy)
         assert_fp32_parity(lg.cpu(), lr, l64, what=f"ld dir={direction}", sens=sl)
+
+
+def _rqs_grads(fn, args, wy, wl, inverse):
+    xs = [a.clone().requires_grad_(True) for a in args]
+    y, ld = fn(*xs, inverse=inverse)
+    ((y * wy).sum() + (ld * wl).sum()).backward()
+    return y.detach(), ld.detach(), [t.grad for t in xs]
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_rqs_unit_backward_vs_float64(cuda_device, inverse):
+    """The stand-alone rational_quadratic_spline under autograd on the GPU (nfx_rqs_unit +
+    nfx_rqs_unit_backward): dL/d(inputs, widths, heights, derivatives) for L = sum(y wy) +
+    sum(ld wl) on the reference's G4 inputs, against float64 autograd of the composite
+    (rational_quadratic_spline.py:4-104), within 4x the fp32 composite's own distance from it
+    (+ 2e-5 relative); every call HIP."""
+    from nfs_amd.flows.spline import _rqs_unit_torch
+    g = load_golden("g4_rqs_unit.npz")
+    a32 = [torch.from_numpy(g[k]) for k in ("x", "uw", "uh", "ud")]
+    gen = torch.Generator().manual_seed(44)
+    wy, wl = torch.randn(a32[0].shape, generator=gen), torch.randn(a32[0].shape, generator=gen)
+
+    def comp(*v, inverse):
+        return _rqs_unit_torch(*v, inverse, 1e-3, 1e-3, 1e-3)
+
+    _, _, g64 = _rqs_grads(comp, [a.double() for a in a32], wy.double(), wl.double(), inverse)
+    _, _, g32 = _rqs_grads(comp, a32, wy, wl, inverse)
+    nfs_amd.reset_stats()
+    y, ld, gg = _rqs_grads(nfs_amd.rational_quadratic_spline, [a.to(cuda_device) for a in a32], wy.to(cuda_device),
+                           wl.to(cuda_device), inverse)
+    assert nfs_amd.STATS["hip"] == 2 and nfs_amd.STATS["torch"] == 0, nfs_amd.STATS
+    yk, lk = ("inv_y", "inv_ld") if inverse else ("fwd_y", "fwd_ld")
+    np.testing.assert_array_equal(y.cpu().numpy(), nfs_amd.rational_quadratic_spline(
+        *[a.to(cuda_device) for a in a32], inverse=inverse)[0].cpu().numpy())
+    assert np.allclose(y.cpu().numpy(), g[yk], rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert np.allclose(ld.cpu().numpy(), g[lk], rtol=1e-4, atol=1e-4, equal_nan=True)
+    for name, a, b32, b64 in zip(("dL/dx", "dL/dwidths", "dL/dheights", "dL/dderivatives"), gg, g32, g64):
+        a, b32, b64 = a.double().cpu(), b32.double(), b64.double()
+        fin = torch.isfinite(b64)
+        assert torch.equal(torch.isfinite(a), fin), f"{name}: non-finite pattern differs"
+        bound = 2e-5 * (1 + b64[fin].abs().max().item()) + 4 * (b32 - b64)[fin].abs().max().item()
+        err = (a - b64)[fin].abs().max().item()
+        assert err <= bound, f"{name}: max err {err:.3g} > {bound:.3g}"
+
+
+def test_rqs_unit_nd_and_unsupported(cuda_device):
+    """N-d inputs run the same kernels elementwise (equal to the flattened call bit for bit, both
+    passes); GPU calls outside the kernels raise instead of running eager PyTorch."""
+    gen = torch.Generator().manual_seed(45)
+    B, d, K = 300, 3, 7
+    x = torch.rand(B, d, generator=gen)
+    uw, uh, ud = (torch.randn(B, d, K, generator=gen), torch.randn(B, d, K, generator=gen),
+                  torch.randn(B, d, K - 1, generator=gen))
+    dev = [t.to(cuda_device) for t in (x, uw, uh, ud)]
+    flat = [dev[0].reshape(-1), dev[1].reshape(-1, K), dev[2].reshape(-1, K), dev[3].reshape(-1, K - 1)]
+    nfs_amd.reset_stats()
+    for inverse in (False, True):
+        y, ld = nfs_amd.rational_quadratic_spline(*dev, inverse=inverse)
+        yf, lf = nfs_amd.rational_quadratic_spline(*flat, inverse=inverse)
+        assert y.shape == (B, d) and ld.shape == (B, d)
+        assert torch.equal(y.reshape(-1), yf) and torch.equal(ld.reshape(-1), lf)
+        wy = torch.randn(B, d, generator=gen).to(cuda_device)
+        _, _, gn = _rqs_grads(nfs_amd.rational_quadratic_spline, dev, wy, wy, inverse)
+        _, _, gfl = _rqs_grads(nfs_amd.rational_quadratic_spline, flat, wy.reshape(-1), wy.reshape(-1), inverse)
+        for a, b in zip(gn, gfl):
+            assert torch.equal(a.reshape(b.shape), b)
+    assert nfs_amd.STATS["torch"] == 0
+    with pytest.raises(NotImplementedError):
+        nfs_amd.rational_quadratic_spline(*[t.double() for t in dev])
+    with pytest.raises(NotImplementedError):
+        nfs_amd.rational_quadratic_spline(dev[0], *(torch.randn(B, d, k).to(cuda_device) for k in (17, 17, 16)))
+    with pytest.raises(ValueError):
+        nfs_amd.rational_quadratic_spline(dev[0], dev[1][:1], dev[2], dev[3])
