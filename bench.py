@@ -568,12 +568,14 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
     t_max = float(t_all.item())
 
-    # dominant kernel: the per-layer fused kernel (every launch of the timed steps)
+    # dominant kernel: the per-layer fused kernel (every launch of the timed steps), named by the
+    # library as dispatched (nfx_last_kernel)
     durs = [e0.elapsed_time(e1) for _, e0, e1 in events]
     kname = events[0][0] if events else "?"
     mean_ms = sum(durs) / max(1, len(durs))
     # one-launch coupling chains (nfx_affine_chain / nfx_spline_chain): one event covers every layer
-    layers_per_launch = len(flow.flows) if kname in ("affine_chain_kernel", "spline_chain_kernel") else 1
+    layers_per_launch = len(flow.flows) if kname in ("affine_chain_kernel", "affine_schain_kernel",
+                                                     "spline_chain_kernel", "spline_schain_kernel") else 1
     f_launch = f_layer * layers_per_launch
     achieved = f_launch * B / (mean_ms * 1e-3) / 1e12
 
@@ -613,9 +615,18 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     # event-timed numbers, with both step checks (same-run, and against this run's step).
     rp_name = config if B == DEFAULT_BATCH.get(config) else f"{config}_{B}"
     tp = os.path.join(ROOT, "profiles", f"rocprof_{rp_name}.json")
+    lib_sha = lib_digest()
+    rj = None
     if os.path.exists(tp):
         with open(tp) as fh:
             rj = json.load(fh)
+    if rj is not None and rj.get("lib_sha256") != lib_sha:
+        # profiled with another build of libnfx.so: its kernels may no longer exist as profiled
+        rocprof = {"stale": True, "profiled_lib_sha256": rj.get("lib_sha256"), "source": os.path.relpath(tp, ROOT),
+                   "round": rj.get("round"),
+                   "note": "profile taken with a different libnfx.so build; figures withheld "
+                           "(re-run tools/profile_bench.sh + tools/reconcile_profile.py)"}
+    elif rj is not None:
         spl = rj["bench_roofline"]["samples_per_launch"]
         if rj.get("hbm_bytes_per_launch") and spl:
             traffic = rj["hbm_bytes_per_launch"] / spl * B
@@ -661,7 +672,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                      "rocprof": rocprof},
         "cpu_baseline": None,
     }
-    if rocprof is not None:
+    result["lib_sha256"] = lib_sha
+    if rocprof is not None and not rocprof.get("stale"):
         # rocprof kernel time per step vs THIS run's step (a different process; the profiled run's
         # own check is fits_profiled_step) and the rocprof frac vs this run's event frac
         rocprof["fits_this_step"] = rocprof["kernel_ms_per_step"] <= result["ms_per_step"]
@@ -748,6 +760,18 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
             cb["nll_abs_diff_vs_gpu"] = abs(cpu_nll - gpu_nll)
         result["cpu_baseline"] = cb
     return result
+
+
+def lib_digest():
+    """sha256 (first 16 hex digits) of the libnfx.so this process loaded: ties a reconciled
+    rocprof profile to the build it measured."""
+    import hashlib
+    from nfs_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
 
 
 def main():

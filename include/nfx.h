@@ -74,6 +74,9 @@ typedef struct NfxMlpRaw {
 
 int nfx_abi_version(void);
 const char* nfx_last_error(void);
+/* The name of the last kernel this thread launched (e.g. "made_seqp_kernel"); "" before any.
+ * Profiling aid: which kernel of a family an entry point dispatched to. */
+const char* nfx_last_kernel(void);
 /* Test hook: overwrite the LDS of every CU with the 32-bit pattern `bits` (tests poison LDS
  * before a kernel to show it never reads LDS it did not write). */
 int nfx_debug_fill_lds(uint32_t bits, void* stream);

@@ -7,6 +7,7 @@
 namespace nfx {
 
 static thread_local char g_err[512] = "";
+static thread_local const char* g_last_kernel = "";  // (string literals of the launch sites)
 
 int set_error(int code, const char* fmt, ...) {
     va_list ap;
@@ -17,6 +18,7 @@ int set_error(int code, const char* fmt, ...) {
 }
 
 int check_launch(const char* what) {
+    g_last_kernel = what;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(NFX_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
     return NFX_OK;
@@ -40,6 +42,7 @@ int num_cus() {
 
 extern "C" int nfx_abi_version(void) { return NFX_ABI_VERSION; }
 extern "C" const char* nfx_last_error(void) { return nfx::g_err; }
+extern "C" const char* nfx_last_kernel(void) { return nfx::g_last_kernel; }
 
 // Test hook: fill the whole LDS of every CU with the 32-bit pattern `bits` (one 160 KiB workgroup
 // per CU, several rounds), so a kernel that read LDS it never wrote would see that pattern

@@ -370,6 +370,105 @@ __device__ __forceinline__ void spline_unit_apply(const float* P, const SplineLa
     }
 }
 
+// spline_unit_apply with the two 32-sample tiles run one after the other through layers 1-3 (the
+// same MFMAs on the same operands in the same order per tile, so bit-identical results): only one
+// tile's hidden activations are live at a time (h1 + h2 of one tile, 64 VGPRs at H = 64, instead of
+// both tiles' 128), which is what lets the 12-wave streaming chain (168 VGPRs per lane) hold its
+// unit body without scratch spills. The layer weights are read from LDS once per tile.
+template <int HT, int K, int DIR, int DMAX, int TILES>
+__device__ __forceinline__ void spline_unit_apply_tseq(const float* P, const SplineLayout& L,
+                                                       const SplineConsts& C, int KS1, int NT,
+                                                       const float (&xb)[2][4], const float (&xr)[DMAX],
+                                                       float (&y)[DMAX], float& ld) {
+#pragma clang fp contract(off)
+    const int lane = lane_id(), h = lane >> 5;
+    f32x16 p3[2][DMAX];  // layer-3 outputs per tile and transformed-dim tile t < NT
+#pragma unroll
+    for (int tile = 0; tile < 2; ++tile) {
+        if (tile == 1 && TILES == 1) {
+            // (as spline_unit_apply: the absent tile's accumulators hold the bias)
+#pragma unroll
+            for (int t = 0; t < DMAX; ++t) p3[1][t] = load_bias16(P + L.b3 + t * 32 + opaque_zero(), h);
+            break;
+        }
+        f32x16 h1[HT];
+#pragma unroll
+        for (int ht = 0; ht < HT; ++ht) {
+            f32x16 a = load_bias16(P + L.b1 + ht * 32 + opaque_zero(), h);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                if (ks < KS1) a = mfma32(P[L.w1 + (ht * 4 + ks) * 64 + lane], xb[tile][ks], a);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+            h1[ht] = a;
+        }
+        f32x16 h2[HT];
+#pragma unroll
+        for (int hto = 0; hto < HT; ++hto) {
+            f32x16 a = load_bias16(P + L.b2 + hto * 32 + opaque_zero(), h);
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+                for (int rq = 0; rq < 4; ++rq) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(
+                        P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h1[kt][4 * rq + rr], a);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
+            h2[hto] = a;
+        }
+#pragma unroll
+        for (int t = 0; t < DMAX; ++t) {
+            if (t < NT) {
+                f32x16 a = load_bias16(P + L.b3 + t * 32 + opaque_zero(), h);
+#pragma unroll
+                for (int kt = 0; kt < HT; ++kt) {
+#pragma unroll
+                    for (int rq = 0; rq < 4; ++rq) {
+                        const f32x4 w = *reinterpret_cast<const f32x4*>(
+                            P + L.w3 + (((t * HT + kt) * 4 + rq) * 64 + lane) * 4);
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h2[kt][4 * rq + rr], a);
+                    }
+                }
+                p3[tile][t] = a;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < DMAX; ++j) y[j] = xr[j];
+    ld = 0.f;
+#pragma unroll
+    for (int t = 0; t < DMAX; ++t) {
+        if (t < NT) {
+            // Half-wave exchange: afterwards every lane holds rows 0..31 of its own sample.
+            float prm[32];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(p3[0][t][r]), __float_as_uint(p3[1][t][r]),
+                                                           false, false);
+                prm[crow(r, 0)] = __uint_as_float(sw[0]);
+                prm[crow(r, 1)] = __uint_as_float(sw[1]);
+            }
+            const int dt = (int)P[L.tdim + t];
+            float v = 0.f;
+#pragma unroll
+            for (int j = 0; j < DMAX; ++j) v = (j == dt) ? xr[j] : v;
+            if (C.rescale) v = C.rs_to_scale * (v - C.rs_lo) - C.bound;
+            float o, l;
+            rq_spline_elem<K, (DIR < 0)>(v, prm, C, o, l);
+            if (C.rescale) o = (o + C.bound) * C.rs_from_scale + C.rs_lo;
+#pragma unroll
+            for (int j = 0; j < DMAX; ++j) y[j] = (j == dt) ? o : y[j];
+            ld = (t == 0) ? l : ld + l;
+        }
+    }
+}
+
 // spline_unit_apply's body in three parts (the same operations in the same order), for the stage
 // clocks of the streaming chain's timing build (NFX_SCHAIN_TIMING): layers 1 and 2 (h2), layer 3's
 // tile t with the half-wave exchange (the lane's 32 spline parameters), and dim t's spline. The

@@ -129,7 +129,10 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
                     NFX_CMARK(2);  // spline
                 }
 #else
-                spline_unit_apply<HT, K, DIR, D, TILES>(W + opaque_zero(), L, C, 1, NT, xb, xr, y, ld);
+                if constexpr (NW > 8 && HT > 1)  // (the 168-VGPR budget: one tile's activations at a time)
+                    spline_unit_apply_tseq<HT, K, DIR, D, TILES>(W + opaque_zero(), L, C, 1, NT, xb, xr, y, ld);
+                else
+                    spline_unit_apply<HT, K, DIR, D, TILES>(W + opaque_zero(), L, C, 1, NT, xb, xr, y, ld);
 #endif
                 if (act) {
                     float yo[D];

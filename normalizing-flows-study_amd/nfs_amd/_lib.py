@@ -32,7 +32,7 @@ NFX_MADE_SEQ_PUSH = 3
 
 # Every symbol include/nfx.h declares (tests check the built library exports all of them).
 EXPORTED_SYMBOLS = (
-    "nfx_abi_version", "nfx_last_error", "nfx_debug_fill_lds",
+    "nfx_abi_version", "nfx_last_error", "nfx_last_kernel", "nfx_debug_fill_lds",
     "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
     "nfx_affine_kernel_policy", "nfx_affine_chain", "nfx_affine_chain_logprob", "nfx_affine_chain_supported",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
@@ -94,6 +94,7 @@ _sz = ctypes.c_size_t
 _SIGNATURES = {
     "nfx_abi_version": (_int, []),
     "nfx_last_error": (ctypes.c_char_p, []),
+    "nfx_last_kernel": (ctypes.c_char_p, []),
     "nfx_debug_fill_lds": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p]),
     "nfx_affine_packed_floats": (_sz, [_int, _int]),
     "nfx_affine_pack": (_int, [ctypes.POINTER(NfxMlpRaw), ctypes.POINTER(NfxMlpRaw), _vp, _int, _int, _vp, _vp]),
@@ -292,3 +293,8 @@ def mlp_raw(linears, batchnorms=(), masks=None):
         eps = bn.eps
     raw.bn_eps = eps
     return raw, keep
+
+
+def last_kernel():
+    """Name of the last kernel this thread launched through libnfx (profiling aid)."""
+    return lib().nfx_last_kernel().decode()

@@ -144,7 +144,7 @@ class NormalizingFlowModel(nn.Module):
             chain.chain_launch(list(self.flows), x, out, ld, direction, False, logprob)
             if ev is not None:
                 e1.record()
-                ev.append(("affine_chain_kernel" if chain is _coupling else "spline_chain_kernel", e0, e1))
+                ev.append((_lib.last_kernel(), e0, e1))
             return (out, ld, True) if logprob is not None else (out, ld)
         bufs = [torch.empty_like(x), torch.empty_like(x)]
         order = range(n) if direction > 0 else reversed(range(n))
@@ -171,7 +171,7 @@ class NormalizingFlowModel(nn.Module):
                 self.flows[i]._hip_launch_counted(cur, out, ld, direction, accumulate=not first)
             if ev is not None:
                 e1.record()
-                ev.append((type(self.flows[i]).__name__, e0, e1))
+                ev.append((_lib.last_kernel(), e0, e1))
             first = False
             cur, k = out, k ^ 1
             if direction > 0 and self.batch_norm_between_layers and i < n - 1:

@@ -32,11 +32,11 @@ HOT = {
     "cfg2": ("affine_coupling_kernel", "affine_schain_kernel", "affine_chain_kernel"),
     "cfg3": ("spline_coupling_kernel", "spline_schain_kernel"),
     "cfg4": ("made_tile_kernel",),
-    "cfg5i": ("made_seqs_kernel", "made_seqw_kernel"),
+    "cfg5i": ("made_seqs_kernel", "made_seqw_kernel", "made_seqp_kernel"),
     "cfg5f": ("made_wide_kernel",),
     "sample4k": ("affine_chain_kernel", "affine_small_kernel", "affine_coupling_kernel"),
     "sample4k_spline": ("spline_coupling_kernel", "spline_schain_kernel"),
-    "sample4k_maf": ("made_seqs_kernel", "made_seqw_kernel", "made_seq_kernel"),
+    "sample4k_maf": ("made_seqs_kernel", "made_seqw_kernel", "made_seqp_kernel", "made_seq_kernel"),
     "sample4k_iaf": ("made_tile_kernel",),
     "trainfig_iaf": ("made_seq_bwd_kernel", "made_seqw_bwd_kernel"),
     "trainfig_maf": ("made_bwd_kernel",),
@@ -120,7 +120,7 @@ def reconcile(cdir, rtag):
     spl = rf["samples_per_launch"]
     ach = f_launch * spl / (mean_us * 1e-6) / 1e12
     res = {
-        "config": name, "round": rtag,
+        "config": name, "round": rtag, "lib_sha256": bench.get("lib_sha256"),
         "bench": {k: bench.get(k) for k in ("value", "ms_per_step", "steps", "warmup", "n_gpus")},
         "bench_roofline": {k: rf.get(k) for k in ("kernel", "mean_launch_ms", "launches", "frac",
                                                     "frac_executed", "flop_per_sample_per_launch",
