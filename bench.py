@@ -438,7 +438,9 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     graphed = None
     if graph and not training:
         graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
-    opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=graph) if training else None
+    # Adam (the reference's optimizer, plots/_common.py:194-211) in torch's fused form: one
+    # multi-tensor kernel per step instead of a few dozen per-parameter elementwise launches
+    opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=graph, fused=True) if training else None
     graphed_train = None
     if graph and training:
         if world > 1:

@@ -38,6 +38,7 @@ struct WgArgs {
 };
 
 constexpr int kWgWaves = 4;
+constexpr int kWgTs = 36;  // LDS transpose tile row stride (floats)
 
 __device__ __forceinline__ int wg_layer_of(const WgArgs& a, int t) {
     int k = 0;
@@ -50,6 +51,7 @@ __device__ __forceinline__ int wg_layer_of(const WgArgs& a, int t) {
 template <bool VEC4>
 __global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int64_t B, int64_t P, int64_t chunk,
                                                                    int64_t ntasks, int blocks_per_xcd, float* part) {
+    __shared__ float wg_lds[kWgWaves * 32 * kWgTs];
     // undo the hardware's round robin of consecutive workgroups over the 8 XCDs
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: descriptors stay scalar
@@ -69,7 +71,6 @@ __global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int
 #undef WGF
     const int lt = t - Ltile0, tmi = lt / Ltn, tni = lt % Ltn;
     const int lane = lane_id(), i = lane & 31, kh = lane >> 5;
-    const int64_t s0 = c * chunk, s1 = (s0 + chunk < B) ? s0 + chunk : B;
     // descriptors based at the tile's first row: rows past M / N read as 0 (range check)
     const int rowsD = LM - 32 * tmi < 32 ? LM - 32 * tmi : 32;
     const int rowsA = LN - 32 * tni < 32 ? LN - 32 * tni : 32;
@@ -77,76 +78,93 @@ __global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int
                                                       (int)(rowsD * P * 4), 0x00020000);
     const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Lam) + (int64_t)32 * tni * P, 0,
                                                       (int)(rowsA * P * 4), 0x00020000);
-    const int vo = (int)((i * P + 16 * kh) * 4);
     const bool bias = tni == 0 && has_b;
     f32x16 acc{};
     float bsum = 0.f;
-    int64_t s = s0;
-    // full 32-sample steps, two per iteration with the next pair's loads in flight
-#define load16(r, st, v)                                                                                   \
-    if constexpr (VEC4) {                                                                                  \
-        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                                    \
-            const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, vo, (int)((st) * 4) + 16 * q, 0);      \
-            v[q] = f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),             \
-                         __uint_as_float(u[3])};                                                           \
-        }                                                                                                  \
-    } else {                                                                                               \
-        _Pragma("unroll") for (int q = 0; q < 4; ++q) _Pragma("unroll") for (int e = 0; e < 4; ++e)        \
-            v[q][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, (int)((st) * 4) + 16 * q + 4 * e, 0)); \
-    }
-    const int64_t full_end = s0 + ((s1 - s0) / 32) * 32;
-    if (s < full_end) {
-        // software pipeline over two register sets: the next step's rows are in flight while this
-        // step's 16 MFMAs run; the sched barriers keep the loads ahead of the MFMAs (the last
-        // step's prefetch re-reads itself instead of branching around the loads)
-        f32x4 dA[4], aA[4], dB[4], aB[4];
-        load16(rd, s, dA);
-        load16(ra, s, aA);
-        for (;;) {
-            int64_t sn = s + 32 < full_end ? s + 32 : s;
-            load16(rd, sn, dB);
-            load16(ra, sn, aB);
-            __builtin_amdgcn_sched_barrier(0);
+    // Rows arrive COALESCED — lane l reads samples 4 (l & 7) .. + 3 of row 8q + (l >> 3), so one
+    // load instruction covers eight whole 128-byte row segments (16 cache accesses instead of the
+    // 64 of a lane-per-row read: the texture-address stage was 82 % busy with those) — and are
+    // turned into MFMA operand order (lane (i, kh): row i, samples 16 kh + 4q .. + 3) through a
+    // wave-private LDS tile. Same MFMA operands in the same order as a lane-per-row read.
+    float* tl = wg_lds + wave * (32 * kWgTs);  // [32 rows][kWgTs], δ then a (LDS keeps a wave's order)
+    const int cr = lane >> 3, cc = 4 * (lane & 7);
+    const int gvo = (int)((cr * P + cc) * 4);
+    auto stage = [&](const __amdgpu_buffer_rsrc_t& r, int64_t st, f32x4 (&g)[4]) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q) {
+            const int so = (int)((st + (int64_t)8 * q * P) * 4);
+            if constexpr (VEC4) {
+                const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, gvo, so, 0);
+                g[q] = f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3])};
+            } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    acc = mfma32(dA[q][e], aA[q][e], acc);
-                    if (bias) bsum += dA[q][e];
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            s += 32;
-            if (s >= full_end) break;
-            sn = s + 32 < full_end ? s + 32 : s;
-            load16(rd, sn, dA);
-            load16(ra, sn, aA);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    acc = mfma32(dB[q][e], aB[q][e], acc);
-                    if (bias) bsum += dB[q][e];
-                }
-            __builtin_amdgcn_sched_barrier(0);
-            s += 32;
-            if (s >= full_end) break;
+                for (int e = 0; e < 4; ++e) g[q][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, gvo, so + 4 * e, 0));
+            }
         }
-    }
-    if (s < s1) {  // ragged tail of the batch: samples >= B hold pitch padding -> select 0
-        f32x4 dv[4], av[4];
-        load16(rd, s, dv);
-        load16(ra, s, av);
-        const int64_t nval = s1 - s - 16 * kh;
+    };
+    auto xpose = [&](const f32x4 (&gd)[4], const f32x4 (&ga)[4], f32x4 (&dv)[4], f32x4 (&av)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(tl + (8 * q + cr) * kWgTs + cc) = gd[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dv[q] = *reinterpret_cast<const f32x4*>(tl + i * kWgTs + 16 * kh + 4 * q);
+        asm volatile("" ::: "memory");  // (the tile is rewritten with a only after δ's reads, in LDS order)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<f32x4*>(tl + (8 * q + cr) * kWgTs + cc) = ga[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) av[q] = *reinterpret_cast<const f32x4*>(tl + i * kWgTs + 16 * kh + 4 * q);
+    };
+    auto step_mfma = [&](const f32x4 (&dv)[4], const f32x4 (&av)[4]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const bool ok = 4 * q + e < nval;
-                const float dvv = ok ? dv[q][e] : 0.f, avv = ok ? av[q][e] : 0.f;
-                acc = mfma32(dvv, avv, acc);
-                if (bias) bsum += dvv;
+                acc = mfma32(dv[q][e], av[q][e], acc);
+                if (bias) bsum += dv[q][e];
             }
+    };
+    // Chunk c takes the 32-sample steps c, c + nch, c + 2 nch, ... (steps dealt round-robin over
+    // the chunks, so at any moment the chunks read one window of nch consecutive steps).
+    const int64_t nch = (B + chunk - 1) / chunk;
+    const int64_t nfs = B / 32;  // full steps of the batch
+    const int64_t nfull = nfs > c ? (nfs - c + nch - 1) / nch : 0;  // this chunk's full steps
+    auto step_at = [&](int64_t k) { return 32 * (c + nch * k); };
+    if (nfull > 0) {
+        // two register sets of global rows: the next step's rows are in flight while this step
+        // goes through the LDS tile and its 16 MFMAs (past the last step the prefetch re-reads it)
+        f32x4 gdA[4], gaA[4], gdB[4], gaB[4], dv[4], av[4];
+        int64_t k = 0;
+        stage(rd, step_at(0), gdA);
+        stage(ra, step_at(0), gaA);
+        for (;;) {
+            int64_t sn = step_at(k + 1 < nfull ? k + 1 : k);
+            stage(rd, sn, gdB);
+            stage(ra, sn, gaB);
+            xpose(gdA, gaA, dv, av);
+            step_mfma(dv, av);
+            if (++k >= nfull) break;
+            sn = step_at(k + 1 < nfull ? k + 1 : k);
+            stage(rd, sn, gdA);
+            stage(ra, sn, gaA);
+            xpose(gdB, gaB, dv, av);
+            step_mfma(dv, av);
+            if (++k >= nfull) break;
+        }
+    }
+    if (B % 32 != 0 && nfs % nch == c) {  // the batch's ragged last step: samples >= B hold pitch padding -> 0
+        const int64_t st = 32 * nfs;
+        f32x4 gd[4], ga[4], dv[4], av[4];
+        stage(rd, st, gd);
+        stage(ra, st, ga);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool ok = st + cc + e < B;
+                gd[q][e] = ok ? gd[q][e] : 0.f;
+                ga[q][e] = ok ? ga[q][e] : 0.f;
+            }
+        xpose(gd, ga, dv, av);
+        step_mfma(dv, av);
     }
     const int64_t len = (int64_t)T * 1024 + (int64_t)a.NBT * 32;
     float* out = part + c * len + (int64_t)t * 1024 + lane * 16;
@@ -157,7 +175,6 @@ __global__ __launch_bounds__(64 * kWgWaves) void made_wgrad_kernel(WgArgs a, int
         const float other = __shfl_xor(bsum, 32, 64);
         if (kh == 0) part[c * len + (int64_t)T * 1024 + (int64_t)(Lbt0 + tmi) * 32 + i] = bsum + other;
     }
-#undef load16
 }
 
 // sums[T*1024 + NBT*32] (float64, accumulator order) -> parameter gradients, masks applied.
@@ -186,8 +203,9 @@ __global__ void made_wgrad_assemble_kernel(WgArgs a, const double* sums) {
 }
 
 static int64_t wg_chunk(int64_t B, int T) {
-    // about 4096 tasks (4 waves per SIMD in one round), chunks of >= 1024 samples, 32-aligned
-    int64_t c = (B * T + 4095) / 4096;
+    // about 6144 tasks (6 waves per SIMD in one round: 84 VGPRs, 4.6 KB of LDS each), chunks of
+    // >= 1024 samples, 32-aligned
+    int64_t c = (B * T + 6143) / 6144;
     if (c < 1024) c = 1024;
     return (c + 31) & ~(int64_t)31;
 }
