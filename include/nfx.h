@@ -397,6 +397,10 @@ int nfx_affine_eval_stats(float* const* running_mean, float* const* running_var,
 size_t nfx_gauss_workspace_bytes(int64_t B);
 int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
                       void* workspace, int64_t B, int d, void* stream);
+/* Its adjoint (training: loss = -mean log p): grad_z[i, j] = -z[i, j] * grad_logp[i],
+ * grad_log_det[i] = grad_logp[i] (autograd of the expression above). */
+int nfx_gauss_logprob_backward(const float* z, const float* grad_logp, float* grad_z, float* grad_log_det,
+                               int64_t B, int d, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Between-layer BatchNorm of NormalizingFlowModel(batch_norm_between_layers=True)

@@ -96,9 +96,39 @@ int gauss_finish(const double* partials, int n, double* sums, int64_t B, hipStre
     return check_launch("gauss_finish_kernel");
 }
 
+// Its adjoint under autograd: grad_z[i, j] = -z[i, j] * g[i] (torch's pow backward, 2 z times
+// the sum's -0.5 g: both exact scalings, one rounding), grad_log_det[i] = g[i].
+template <bool WIDE>
+__global__ __launch_bounds__(256) void gauss_logprob_bwd_kernel(const float* __restrict__ z, const float* __restrict__ g,
+                                                                float* __restrict__ gz, float* __restrict__ gld,
+                                                                int64_t B, int d) {
+    const int64_t n = B * d, stride = (int64_t)gridDim.x * 256;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+        const int64_t i = WIDE ? e / d : (int64_t)((uint32_t)e / (uint32_t)d);
+        gz[e] = -(z[e] * g[i]);
+    }
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B; i += stride) gld[i] = g[i];
+}
+
 }  // namespace nfx
 
 using namespace nfx;
+
+extern "C" int nfx_gauss_logprob_backward(const float* z, const float* grad_logp, float* grad_z, float* grad_log_det,
+                                          int64_t B, int d, void* stream) {
+    if (B < 0 || d <= 0) return set_error(NFX_EINVAL, "gauss_logprob_backward: bad shape B=%lld d=%d", (long long)B, d);
+    if (B == 0) return NFX_OK;
+    if (!z || !grad_logp || !grad_z || !grad_log_det) return set_error(NFX_EINVAL, "gauss_logprob_backward: null pointer");
+    const int64_t n = B * d;
+    int64_t blocks = (n + 255) / 256;
+    const int64_t cap = (int64_t)num_cus() * 8;
+    if (blocks > cap) blocks = cap;
+    if (n < ((int64_t)1 << 31))
+        gauss_logprob_bwd_kernel<false><<<(int)blocks, 256, 0, (hipStream_t)stream>>>(z, grad_logp, grad_z, grad_log_det, B, d);
+    else
+        gauss_logprob_bwd_kernel<true><<<(int)blocks, 256, 0, (hipStream_t)stream>>>(z, grad_logp, grad_z, grad_log_det, B, d);
+    return check_launch("gauss_logprob_bwd_kernel");
+}
 
 extern "C" size_t nfx_gauss_workspace_bytes(int64_t B) {
     (void)B;

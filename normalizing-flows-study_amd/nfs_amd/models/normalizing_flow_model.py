@@ -204,8 +204,11 @@ class NormalizingFlowModel(nn.Module):
                 gauss_logprob(z, ld, logp, sums, ws)
             return (logp, sums) if return_sums else logp
         z, ld = self.inverse(x)
-        if z.device.type == "cuda" and z.dtype == torch.float32 and not self._needs_grad(x):
+        if z.device.type == "cuda" and z.dtype == torch.float32 and z.dim() == 2 and not self._needs_grad(x):
             logp, sums = gauss_logprob(z, ld, ws=workspace)
+        elif z.device.type == "cuda" and z.dtype == torch.float32 and z.dim() == 2:
+            # training: the same HIP epilogue under autograd, its adjoint in one HIP kernel
+            logp, sums = _GaussLogProbFn.apply(z, ld, workspace)
         else:
             d = z.shape[1]
             logp = -0.5 * (d * math.log(2 * math.pi) + z.pow(2).sum(-1)) + ld
@@ -272,6 +275,30 @@ def gauss_logprob(z, ld, logp=None, sums=None, ws=None):
                                    _lib.ptr(ws), B, d, _lib.stream_of(z)), "nfx_gauss_logprob")
     STATS["hip"] += 1
     return logp, sums
+
+
+class _GaussLogProbFn(torch.autograd.Function):
+    """log N(z; 0, I) + ld under autograd: nfx_gauss_logprob forward (the eval epilogue, the
+    reference's rounding order), nfx_gauss_logprob_backward (dL/dz = -z g, dL/dld = g)."""
+
+    @staticmethod
+    def forward(ctx, z, ld, workspace):
+        z = z.contiguous()
+        logp, sums = gauss_logprob(z, ld.contiguous(), ws=workspace)
+        ctx.save_for_backward(z)
+        ctx.mark_non_differentiable(sums)
+        return logp, sums
+
+    @staticmethod
+    def backward(ctx, g, _gs):
+        (z,) = ctx.saved_tensors
+        B, d = z.shape
+        g = g.contiguous().float()
+        gz, gld = torch.empty_like(z), torch.empty_like(g)
+        _lib.check(_lib.lib().nfx_gauss_logprob_backward(_lib.ptr(z), _lib.ptr(g), _lib.ptr(gz), _lib.ptr(gld), B, d,
+                                                         _lib.stream_of(z)), "nfx_gauss_logprob_backward")
+        STATS["hip"] += 1
+        return gz, gld, None
 
 
 # ---------------------------------------------------------------------------------------------
