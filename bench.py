@@ -13,8 +13,11 @@ Scaling (default STRONG, north_star's ">= 6x strong scaling at 8 GPUs"): the BAS
 whole batch instead. The weights are the reference's own (tests/golden/*.npz, produced by
 importing the reference) and the input is the G8 seeded batch, so the line also carries the
 global NLL against the reference's full-scale NLL ("test-NLL match", BASELINE.json metric).
-Eval passes replay a captured HIP graph by default (`--eager` for per-layer launches): at
-125k samples per GPU the ~20 us per-layer host issue cost would otherwise rival the kernels.
+Eval steps of the cfg* workloads launch eagerly (one chain / layer launch per step; `--graph`
+replays a captured HIP graph instead): with the host issuing ahead of the device, a plain launch
+leaves less idle between steps than a graph replay (measured, `profiles/r05_graph_vs_eager.jsonl`:
+cfg2 125k 164.7 vs 167.0 us, cfg3 125k 131.9 vs 136.0 us, cfg5i 1Ki 32.1 vs 36.3 us, cfg2 1M
+equal). The sample4k* steps (several small launches each) keep the graph (`--eager` opts out).
 
 At the default config (cfg2, RealNVP d=2) the line nests the second half of the metric, MAF
 d=63 (cfg4, 5x MAF(63,64), 4M samples split over the ranks), with its own roofline and CPU
@@ -789,9 +792,10 @@ def main():
                     help="global batch (default: the BASELINE batch, 1M; 4M cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--graph", action="store_true",
-                    help="training configs: replay the captured HIP graph of the step (nfs_amd.GraphedTrainStep)")
+                    help="replay a captured HIP graph of the step (training: nfs_amd.GraphedTrainStep; "
+                         "cfg* eval: nfs_amd.GraphedFlow)")
     ap.add_argument("--eager", action="store_true",
-                    help="eval configs: eager per-layer launches instead of the captured HIP graph (GraphedFlow)")
+                    help="sample4k* configs: eager launches instead of the captured HIP graph (GraphedFlow)")
     ap.add_argument("--weak", action="store_true", help="weak scaling: every rank processes the whole batch")
     ap.add_argument("--strong", action="store_true", help="(default) strong scaling: split the batch over the ranks")
     ap.add_argument("--no-secondary", action="store_true", help="cfg2: skip the nested MAF d=63 (cfg4) line")
@@ -814,7 +818,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     training = a.config in TRAIN_CONFIGS
-    graph = a.graph if training else not a.eager
+    graph = a.graph if training else ((not a.eager) if a.config.startswith("sample4k") else (a.graph and not a.eager))
     strong = not a.weak
     result = run_config(a.config, a, world, rank, dev, strong, graph, not a.no_cpu)
     if a.config == "cfg2" and not a.no_secondary:
