@@ -682,6 +682,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         # rocprof kernel time per step vs THIS run's step (a different process; the profiled run's
         # own check is fits_profiled_step) and the rocprof frac vs this run's event frac
         rocprof["fits_this_step"] = rocprof["kernel_ms_per_step"] <= result["ms_per_step"]
+        # (kernels run a little slower under rocprofv3 than unprofiled: the ratio says how much)
+        rocprof["kernel_ms_over_this_step"] = rocprof["kernel_ms_per_step"] / result["ms_per_step"]
         rocprof["frac_rel_diff_vs_events"] = abs(rocprof["frac"] - result["roofline"]["frac"]) / result["roofline"]["frac"]
     if config == "cfg4":
         fe = made_executed_flop_per_sample(63, 64)
