@@ -303,3 +303,19 @@ def test_log_prob_autograd_gauss_adjoint(cuda_device, kind):
     close(gxg, gx32, gx64, "dL/dx")
     for (n, _), a, b, c in zip(model.named_parameters(), gpg, gp32, gp64):
         close(a, b, c, n)
+
+
+def test_last_kernel_names_dispatch(cuda_device):
+    """nfx_last_kernel names the kernel an entry point dispatched (bench.py labels its roofline
+    with it): a RealNVP log_prob at 100k rows runs the streaming chain, at 4k the small-batch
+    chain; an IAF(784, 64) log_prob at 1Ki the push kernel."""
+    from nfs_amd import _lib
+    model = nfs_amd.RealNVP(2, 4, 64).to(cuda_device).eval()
+    with torch.no_grad():
+        model.log_prob(torch.randn(100_000, 2, device=cuda_device))
+        assert _lib.last_kernel() == "affine_schain_kernel"
+        model.log_prob(torch.randn(4_000, 2, device=cuda_device))
+        assert _lib.last_kernel() == "affine_chain_kernel"
+        iaf = nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)]).to(cuda_device).eval()
+        iaf.log_prob(torch.randn(1024, 784, device=cuda_device))
+        assert _lib.last_kernel() == "made_seqp_kernel"
