@@ -403,7 +403,13 @@ __device__ __forceinline__ void spline_unit_apply_tseq(const float* P, const Spl
             for (int r = 0; r < 16; ++r) a[r] = trelu(a[r]);
             h1[ht] = a;
         }
+        // (with one tile in flight a weight group feeds only 4 MFMAs, less than an LDS read's
+        // latency: each group is read one group ahead)
         f32x16 h2[HT];
+        auto w2at = [&](int q) {  // group q = (hto * HT + kt) * 4 + rq
+            return *reinterpret_cast<const f32x4*>(P + L.w2 + (q * 64 + lane) * 4);
+        };
+        f32x4 wn = w2at(0);
 #pragma unroll
         for (int hto = 0; hto < HT; ++hto) {
             f32x16 a = load_bias16(P + L.b2 + hto * 32 + opaque_zero(), h);
@@ -411,8 +417,9 @@ __device__ __forceinline__ void spline_unit_apply_tseq(const float* P, const Spl
             for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
                 for (int rq = 0; rq < 4; ++rq) {
-                    const f32x4 w = *reinterpret_cast<const f32x4*>(
-                        P + L.w2 + (((hto * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                    const int q = (hto * HT + kt) * 4 + rq;
+                    const f32x4 w = wn;
+                    if (q + 1 < HT * HT * 4) wn = w2at(q + 1);
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h1[kt][4 * rq + rr], a);
                 }
@@ -425,12 +432,17 @@ __device__ __forceinline__ void spline_unit_apply_tseq(const float* P, const Spl
         for (int t = 0; t < DMAX; ++t) {
             if (t < NT) {
                 f32x16 a = load_bias16(P + L.b3 + t * 32 + opaque_zero(), h);
+                auto w3at = [&](int q) {  // group q = kt * 4 + rq of tile t
+                    return *reinterpret_cast<const f32x4*>(P + L.w3 + ((t * HT * 4 + q) * 64 + lane) * 4);
+                };
+                f32x4 wn3 = w3at(0);
 #pragma unroll
                 for (int kt = 0; kt < HT; ++kt) {
 #pragma unroll
                     for (int rq = 0; rq < 4; ++rq) {
-                        const f32x4 w = *reinterpret_cast<const f32x4*>(
-                            P + L.w3 + (((t * HT + kt) * 4 + rq) * 64 + lane) * 4);
+                        const int q = kt * 4 + rq;
+                        const f32x4 w = wn3;
+                        if (q + 1 < HT * 4) wn3 = w3at(q + 1);
 #pragma unroll
                         for (int rr = 0; rr < 4; ++rr) a = mfma32(w[rr], h2[kt][4 * rq + rr], a);
                     }
