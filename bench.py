@@ -172,10 +172,14 @@ def build(config):
         m = nfs_amd.RealNVP(2, 8, 64)
         perturb(m, 0.03, 1)
         H = 64
-        # dominant kernel = BWD2 of the train-mode backward: per net layer-2 forward recompute,
-        # (diag(r2) W2)^T e2 and dW2 = sum e2 a1^T (3 x 2H^2) + layer 1 (2H) + output layer and
-        # W3^T delta3 (2 x 2H), n_c = n_t = 1
-        f = 2 * (3 * 2 * H * H + 2 * H + 2 * 2 * H)
+        # dominant kernel = BWD2 of the train-mode backward, per net: (diag(r2) W2)^T e2 and
+        # dW2 = sum e2 a1^T (2 x 2H^2) + layer 1 (2H) + W3^T delta3 (2H), the layer-2
+        # pre-activations read from the copy the statistics pass kept (NFX_TRAIN_KEEP=0: the
+        # round-4 kernel also recomputes layer 2 and the output layer, 3 x 2H^2 + 2H + 2 x 2H)
+        if os.environ.get("NFX_TRAIN_KEEP", "1") != "0":
+            f = 2 * (2 * 2 * H * H + 2 * H + 2 * H)
+        else:
+            f = 2 * (3 * 2 * H * H + 2 * H + 2 * 2 * H)
         import oracle
         what = ("cfg2t RealNVP(2,8,64) training step (train-mode BatchNorm: batch statistics + "
                 "running-stat update, -log_prob mean, fused backward, Adam)") if config == "cfg2t" else \
@@ -714,8 +718,9 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                               "(tests/golden/g15_fig_train.npz, written by importing the reference)")
         result["nll_f64"] = None
         result["roofline"]["note"] = ("dominant kernel = BWD2 of the train-mode coupling backward "
-                                      "(layer-2 recompute, W2^T e2 and the sample-contraction dW2 on "
-                                      "MFMA); a layer runs STATS1, STATS2, the fused forward, BWD1-3")
+                                      "(W2^T e2 and the sample-contraction dW2 on MFMA, one net per "
+                                      "workgroup); a layer runs STATS1, STATS2 (keeps the layer-2 "
+                                      "pre-activations, 512 B/sample), OUT, BWD1-3")
         if world > 1:
             result["config"]["parallelism"] = (f"dp{world} (sample shards, SyncBN: 4 all-gathers/all-reduces "
                                                f"of <= 3 KB per layer + 1 bucketed gradient all-reduce)")

@@ -373,6 +373,22 @@ int nfx_affine_train_backward(const float* tpack, const float* in, const float* 
                               void* workspace, void* stream);
 int nfx_affine_train_assemble(const double* G, const double* stats1, const double* stats2, int d,
                               int H, float eps, float* grads, void* stream);
+/* Kept activations (H <= 64): nfx_affine_train_stats_keep(layer 2, keep) also writes the raw
+ * layer-2 pre-activations h2 = W2 a1 + b2 of both nets into `keep` (nfx_affine_train_keep_floats
+ * floats, 512 B per sample at H = 64), and nfx_affine_train_backward_keep(stage 1 or 2, keep)
+ * reads them instead of recomputing layers 1-2 (keep = NULL: the plain entry points). */
+size_t nfx_affine_train_keep_floats(int64_t B, int d, int H);
+int nfx_affine_train_stats_keep(const float* tpack, const float* in, int64_t B, int d, int H,
+                                int layer, double* stats, void* workspace, float* keep,
+                                void* stream);
+int nfx_affine_train_backward_keep(const float* tpack, const float* in, const float* grad_out,
+                                   const float* grad_log_det, float* grad_in, int64_t B, int d,
+                                   int H, int direction, int stage, const double* stats2,
+                                   double* G, void* workspace, const float* keep, void* stream);
+/* The layer's (y, log_det) from the kept pre-activations, tpack folded with both statistics:
+ * replaces nfx_affine_coupling(epack, ...) in a forward that kept them. */
+int nfx_affine_train_output(const float* tpack, const float* in, const float* keep, float* out,
+                            float* log_det, int64_t B, int d, int H, int direction, void* stream);
 /* Eval-mode CouplingLayer under autograd (coupling_layer.py:40-96 with model.eval(): BatchNorm
  * normalises with its RUNNING statistics, which are buffers, so nothing couples the samples).
  * Same kernels: nfx_affine_eval_stats writes triples (-1, running_mean, -running_var) for the 4

@@ -113,10 +113,17 @@ __global__ void affine_train_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const
                 const int ot = (t >> 10) % HT, kt = (t >> 10) / HT;
                 const int row = 32 * ot + crow(4 * rq + rr, lane >> 5), c = 32 * kt + (lane & 31);
                 if (row < H && c < H) v = (float)(bn_fold(stats2, Hp, net, row, eps).r * (double)raw_w(P, 1, H, row, c));
-            } else {  // w1c [D][HT][32]: (diag(r1) W1)[row][j]
+            } else if (o < L.m2) {  // w1c [D][HT][32]: (diag(r1) W1)[row][j]
                 const int t = o - L.w1c, j = t / (HT * 32), a = t % (HT * 32);
                 const int row = 32 * (a >> 5) + crow(a & 15, (a >> 4) & 1);
                 if (j < d && row < H) v = (float)(bn_fold(stats1, Hp, net, row, eps).r * (double)raw_w(P, 0, d, row, j));
+            } else {  // m2, r2 [HT][32]: BN2 mean and 1/sqrt(var + eps), accumulator order
+                const int which = (o - L.m2) / (HT * 32), t = (o - L.m2) % (HT * 32);
+                const int row = 32 * (t >> 5) + crow(t & 15, (t >> 4) & 1);
+                if (row < H) {
+                    const BnFold f = bn_fold(stats2, Hp, net, row, eps);
+                    v = (float)(which == 0 ? f.mean : f.r);
+                }
             }
         }
         tpack[i] = v;
@@ -173,35 +180,33 @@ __global__ void affine_train_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const
     }
 }
 
-// stats[net][row][3] = Chan merge of the per-workgroup triples: 16 threads per feature merge
-// workgroups g, g+16, ... and the 16 results are merged in order (deterministic).
+// stats[net][row][3] = Chan merge of the per-workgroup triples: one wave per feature, lane l
+// merges workgroups l, l + 64, ... in order, then a fixed pairwise tree over the 64 lanes
+// (deterministic; the 16-thread serial version took 17 us at 512 workgroups).
 __global__ __launch_bounds__(256) void affine_train_stats_finish(const double* part, int nw, int Hp, double* stats) {
-    __shared__ double red[16][16][3];
-    const int e = threadIdx.x & 15, g = threadIdx.x >> 4;
-    const int i = blockIdx.x * 16 + e;  // net * Hp + row
+    const int l = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // net * Hp + row
+    if (i >= 2 * Hp) return;                             // whole waves
     double n = 0.0, mean = 0.0, m2 = 0.0;
-    if (i < 2 * Hp) {
-        for (int w = g; w < nw; w += 16) {
-            const double* q = part + ((size_t)w * 2 * Hp + i) * 3;
+    for (int w = l; w < nw; w += 64) {
+        const double* q = part + ((size_t)w * 2 * Hp + i) * 3;
+        if (n == 0.0) {
+            n = q[0]; mean = q[1]; m2 = q[2];
+        } else {
+            chan_merge(n, mean, m2, q[0], q[1], q[2]);
+        }
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        const double nb = __shfl_down(n, off, 64), mb = __shfl_down(mean, off, 64), qb = __shfl_down(m2, off, 64);
+        if ((l & (2 * off - 1)) == 0) {
             if (n == 0.0) {
-                n = q[0]; mean = q[1]; m2 = q[2];
+                n = nb; mean = mb; m2 = qb;
             } else {
-                chan_merge(n, mean, m2, q[0], q[1], q[2]);
+                chan_merge(n, mean, m2, nb, mb, qb);
             }
         }
     }
-    red[g][e][0] = n;
-    red[g][e][1] = mean;
-    red[g][e][2] = m2;
-    __syncthreads();
-    if (g == 0 && i < 2 * Hp) {
-        for (int k = 1; k < 16; ++k) {
-            if (n == 0.0) {
-                n = red[k][e][0]; mean = red[k][e][1]; m2 = red[k][e][2];
-            } else {
-                chan_merge(n, mean, m2, red[k][e][0], red[k][e][1], red[k][e][2]);
-            }
-        }
+    if (l == 0) {
         stats[i * 3 + 0] = n;
         stats[i * 3 + 1] = mean;
         stats[i * 3 + 2] = m2;
@@ -327,6 +332,7 @@ __global__ __launch_bounds__(256) void affine_trainw_finish(const float* part, i
 }
 
 static int pad_d(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : (d <= 8 ? 8 : 0)); }
+static size_t train_dl_bytes(int64_t B, int D) { return ((size_t)B * 2 * D * sizeof(float) + 255) & ~(size_t)255; }
 
 static affine_trainw_kernel_t pick_trainw(int HT, int D, int stage) {
     switch (HT) {
@@ -483,7 +489,8 @@ extern "C" size_t nfx_affine_train_workspace_bytes(int64_t B, int d, int H) {
     if ((size_t)GL.len3 * sizeof(float) > per_wave) per_wave = (size_t)GL.len3 * sizeof(float);
     if (st > per_wave) per_wave = st;
     const size_t partials = ((size_t)nw * per_wave + 255) & ~(size_t)255;
-    return partials + (size_t)ntiles * 2 * HT * 1024 * sizeof(float);
+    // + the delta3 rows BWD1K hands to BWD2K ([B][2][D]), then the g_y1 tiles (BWD2 -> BWD3)
+    return partials + train_dl_bytes(B, D) + (size_t)ntiles * 2 * HT * 1024 * sizeof(float);
 }
 
 extern "C" int nfx_affine_train_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, const float* mask,
@@ -506,14 +513,30 @@ extern "C" int nfx_affine_train_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_
     return check_launch("affine_train_pack_kernel");
 }
 
+// Floats of the kept layer-2 pre-activations (nfx_affine_train_stats_keep /
+// nfx_affine_train_backward_keep): 2 nets x Hp per sample in 32-sample tiles; 0 where the pass
+// family does not keep them (HT > 2: the wide path recomputes).
+extern "C" size_t nfx_affine_train_keep_floats(int64_t B, int d, int H) {
+    if (!pad_d(d) || H <= 0 || H > 64 || B < 1) return 0;
+    const int HT = (H + 31) / 32;
+    return (size_t)((B + 31) / 32) * 2 * HT * 1024;
+}
+
 extern "C" int nfx_affine_train_stats(const float* tpack, const float* x, int64_t B, int d, int H, int layer,
                                       double* stats, void* workspace, void* stream) {
+    return nfx_affine_train_stats_keep(tpack, x, B, d, H, layer, stats, workspace, nullptr, stream);
+}
+
+extern "C" int nfx_affine_train_stats_keep(const float* tpack, const float* x, int64_t B, int d, int H, int layer,
+                                           double* stats, void* workspace, float* keep, void* stream) {
     int rc = train_check(d, H, "affine_train_stats");
     if (rc) return rc;
     if (layer != 1 && layer != 2) return set_error(NFX_EINVAL, "affine_train_stats: layer must be 1 or 2");
     if (B < 1) return set_error(NFX_EINVAL, "affine_train_stats: batch statistics need B >= 1 (B=%lld)", (long long)B);
     if (!tpack || !x || !stats || !workspace) return set_error(NFX_EINVAL, "affine_train_stats: null pointer");
     const int D = pad_d(d), HT = (H + 31) / 32, Hp = 32 * HT;
+    if (keep && (layer != 2 || HT > 2))
+        return set_error(NFX_EINVAL, "affine_train_stats: keep needs layer 2 and H <= 64 (H=%d)", H);
     if (HT > 2) {  // wide path: one net per workgroup (blockIdx.y)
         const int st = layer == 1 ? TW_STATS1 : TW_STATS2;
         affine_trainw_kernel_t kw = pick_trainw(HT, D, st);
@@ -525,21 +548,43 @@ extern "C" int nfx_affine_train_stats(const float* tpack, const float* x, int64_
                                                                           nullptr, nullptr, nullptr, workspace, B, d, 1,
                                                                           ntiles);
         if ((rc = check_launch("affine_trainw_kernel(stats)"))) return rc;
-        affine_train_stats_finish<<<(2 * Hp + 15) / 16, 256, 0, s>>>(reinterpret_cast<const double*>(workspace),
+        affine_train_stats_finish<<<(2 * Hp + 3) / 4, 256, 0, s>>>(reinterpret_cast<const double*>(workspace),
                                                                      (int)(2 * gx), Hp, stats);
         return check_launch("affine_train_stats_finish");
     }
-    affine_train_kernel_t k = pick_train(HT, D, layer == 1 ? TS_STATS1 : TS_STATS2);
-    const size_t lds = affine_train_lds(D, HT);
+    const int ts = layer == 1 ? TS_STATS1 : TS_STATS2;
+    affine_train_kernel_t k = pick_train(HT, D, ts);
+    const size_t lds = affine_train_lds(D, HT, ts);
     if ((rc = prepare_lds((const void*)k, lds))) return rc;
     const TrainGrid g = train_grid(k, lds, B);
     hipStream_t s = (hipStream_t)stream;
-    k<<<g.grid, 256, lds, s>>>(tpack, x, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, workspace, B, d, 1,
-                               g.ntiles);
+    k<<<g.grid, 256, lds, s>>>(tpack, x, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, workspace, keep,
+                               nullptr, B, d, 1, g.ntiles);
     if ((rc = check_launch("affine_train_kernel(stats)"))) return rc;
-    affine_train_stats_finish<<<(2 * Hp + 15) / 16, 256, 0, s>>>(reinterpret_cast<const double*>(workspace),
+    affine_train_stats_finish<<<(2 * Hp + 3) / 4, 256, 0, s>>>(reinterpret_cast<const double*>(workspace),
                                                                  g.grid, Hp, stats);
     return check_launch("affine_train_stats_finish");
+}
+
+// The train-mode layer's output (y, log_det) from the kept layer-2 pre-activations and the pack
+// folded with both statistics: replaces nfx_affine_coupling(epack) in a forward that keeps them.
+extern "C" int nfx_affine_train_output(const float* tpack, const float* x, const float* keep, float* y,
+                                       float* log_det, int64_t B, int d, int H, int direction, void* stream) {
+    int rc = train_check(d, H, "affine_train_output");
+    if (rc) return rc;
+    if (direction != NFX_FORWARD && direction != NFX_INVERSE)
+        return set_error(NFX_EINVAL, "affine_train_output: direction must be +1 or -1");
+    if (B < 1) return set_error(NFX_EINVAL, "affine_train_output: B >= 1 required");
+    if (!tpack || !x || !keep || !y || !log_det) return set_error(NFX_EINVAL, "affine_train_output: null pointer");
+    const int D = pad_d(d), HT = (H + 31) / 32;
+    if (HT > 2) return set_error(NFX_EINVAL, "affine_train_output: kept activations need H <= 64 (H=%d)", H);
+    affine_train_kernel_t k = pick_train(HT, D, TS_OUTK);
+    const size_t lds = affine_train_lds(D, HT, TS_OUTK);
+    if ((rc = prepare_lds((const void*)k, lds))) return rc;
+    const TrainGrid g = train_grid(k, lds, B);
+    k<<<g.grid, 256, lds, (hipStream_t)stream>>>(tpack, x, nullptr, nullptr, y, nullptr, nullptr, nullptr, nullptr,
+                                                 const_cast<float*>(keep), log_det, B, d, direction, g.ntiles);
+    return check_launch("affine_train_kernel(output)");
 }
 
 extern "C" int nfx_affine_train_update_running(const double* stats1, const double* stats2, float* const* running_mean,
@@ -574,6 +619,14 @@ extern "C" int nfx_affine_eval_stats(float* const* running_mean, float* const* r
 extern "C" int nfx_affine_train_backward(const float* tpack, const float* x, const float* gy, const float* gld,
                                          float* gx, int64_t B, int d, int H, int direction, int stage,
                                          const double* stats2, double* G, void* workspace, void* stream) {
+    return nfx_affine_train_backward_keep(tpack, x, gy, gld, gx, B, d, H, direction, stage, stats2, G, workspace,
+                                          nullptr, stream);
+}
+
+extern "C" int nfx_affine_train_backward_keep(const float* tpack, const float* x, const float* gy, const float* gld,
+                                              float* gx, int64_t B, int d, int H, int direction, int stage,
+                                              const double* stats2, double* G, void* workspace, const float* keep,
+                                              void* stream) {
     int rc = train_check(d, H, "affine_train_backward");
     if (rc) return rc;
     if (stage < 1 || stage > 3) return set_error(NFX_EINVAL, "affine_train_backward: stage must be 1, 2 or 3");
@@ -584,25 +637,31 @@ extern "C" int nfx_affine_train_backward(const float* tpack, const float* x, con
         return set_error(NFX_EINVAL, "affine_train_backward: null pointer");
     const int D = pad_d(d), HT = (H + 31) / 32;
     const TrainGrad GL = train_grad_layout(D, HT);
+    if (keep && HT > 2) return set_error(NFX_EINVAL, "affine_train_backward: keep needs H <= 64 (H=%d)", H);
     if (HT > 2) return trainw_backward(tpack, x, gy, gld, gx, B, d, D, HT, direction, stage, stats2, G, workspace,
                                        (hipStream_t)stream);
-    const int ts = stage == 1 ? TS_BWD1 : (stage == 2 ? TS_BWD2 : TS_BWD3);
+    const int ts = stage == 1 ? (keep ? TS_BWD1K : TS_BWD1) : (stage == 2 ? (keep ? TS_BWD2K : TS_BWD2) : TS_BWD3);
     affine_train_kernel_t k = pick_train(HT, D, ts);
-    const size_t lds = affine_train_lds(D, HT);
+    const size_t lds = affine_train_lds(D, HT, ts);
     if ((rc = prepare_lds((const void*)k, lds))) return rc;
     const TrainGrid g = train_grid(k, lds, B);
-    // partials first, then the g_y1 tiles (same offsets as nfx_affine_train_workspace_bytes)
+    // partials first, then the delta3 rows and the g_y1 tiles (offsets as in
+    // nfx_affine_train_workspace_bytes)
     const size_t full = nfx_affine_train_workspace_bytes(B, d, H);
     const size_t gbytes = (size_t)g.ntiles * 2 * HT * 1024 * sizeof(float);
     char* ws = reinterpret_cast<char*>(workspace);
     float* gbuf = reinterpret_cast<float*>(ws + (full - gbytes));
+    float* dlb = reinterpret_cast<float*>(ws + (full - gbytes - train_dl_bytes(B, D)));
     hipStream_t s = (hipStream_t)stream;
-    k<<<g.grid, 256, lds, s>>>(tpack, x, gy, gld, gx, gbuf, G, stats2, workspace, B, d, direction, g.ntiles);
+    // BWD2K: one net per workgroup (blockIdx.y), the resident workgroups split between the nets
+    const int ny = train_stage_nets(ts) == 1 ? 2 : 1, gxn = ny == 2 ? (g.grid + 1) / 2 : g.grid;
+    k<<<dim3(gxn, ny), 256, lds, s>>>(tpack, x, gy, gld, gx, gbuf, G, stats2, workspace, const_cast<float*>(keep),
+                                      dlb, B, d, direction, g.ntiles);
     if ((rc = check_launch("affine_train_kernel(backward)"))) return rc;
     const int off = stage == 1 ? GL.g1s : (stage == 2 ? GL.g2s : GL.g3w);
     const int len = stage == 1 ? GL.len1 : (stage == 2 ? GL.len2 : GL.len3);
-    affine_train_sum_finish<<<(len + 15) / 16, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), g.grid, len,
-                                                            G + off);
+    affine_train_sum_finish<<<(len + 15) / 16, 256, 0, s>>>(reinterpret_cast<const float*>(workspace), gxn * ny,
+                                                            len, G + off);
     return check_launch("affine_train_sum_finish");
 }
 

@@ -12,6 +12,9 @@ static affine_train_kernel_t pick_1(int stage) {
         case TS_BWD1: return affine_train_kernel<1, D, TS_BWD1>;
         case TS_BWD2: return affine_train_kernel<1, D, TS_BWD2>;
         case TS_BWD3: return affine_train_kernel<1, D, TS_BWD3>;
+        case TS_BWD1K: return affine_train_kernel<1, D, TS_BWD1K>;
+        case TS_BWD2K: return affine_train_kernel<1, D, TS_BWD2K>;
+        case TS_OUTK: return affine_train_kernel<1, D, TS_OUTK>;
         default: return nullptr;
     }
 }

@@ -15,7 +15,12 @@
 
 namespace nfx {
 
-enum TrainStage { TS_STATS1 = 0, TS_STATS2 = 1, TS_BWD1 = 2, TS_BWD2 = 3, TS_BWD3 = 4 };
+// TS_BWD1K / TS_BWD2K: BWD1 / BWD2 reading the layer-2 pre-activations STATS2 kept in HBM
+// (`keep`, 512 B per sample at H = 64) instead of recomputing layers 1-2 of both nets.
+// TS_OUTK: the layer's forward output (y, log-det) from the kept pre-activations.
+enum TrainStage {
+    TS_STATS1 = 0, TS_STATS2 = 1, TS_BWD1 = 2, TS_BWD2 = 3, TS_BWD3 = 4, TS_BWD1K = 5, TS_BWD2K = 6, TS_OUTK = 7
+};
 
 constexpr int kTS = 36;  // row stride (floats) of a per-wave 32 x 32 transpose buffer
 
@@ -31,10 +36,11 @@ constexpr int kTS = 36;  // row stride (floats) of a per-wave 32 x 32 transpose 
 //   b3  [D]
 //   w2t [HT][HT][4][64][4]  A operand of (diag(r2) W2)^T         [in tile][out tile][..]
 //   w1c [D][HT][32]         (diag(r1) W1)[row][j]              accumulator order
+//   m2, r2 [HT][32]         mu2, r2 of BN2 (float)              accumulator order  (K stages)
 // then mask [D] (padding columns j >= d: mask 1, zero weights).
 struct TrainLayout {
     int D, HT, KS1;
-    int w1, c1, g1, e1, w2, c2, g2, e2, w3, b3, w2t, w1c, net, mask, total;
+    int w1, c1, g1, e1, w2, c2, g2, e2, w3, b3, w2t, w1c, m2, r2, net, mask, total;
 };
 
 __host__ __device__ constexpr TrainLayout train_layout(int D, int HT) {
@@ -55,9 +61,33 @@ __host__ __device__ constexpr TrainLayout train_layout(int D, int HT) {
     L.b3 = o; o += (D + 3) & ~3;
     L.w2t = o; o += HT * HT * 1024;
     L.w1c = o; o += D * HT * 32;
+    L.m2 = o; o += HT * 32;
+    L.r2 = o; o += HT * 32;
     L.net = o;
     L.mask = 2 * o;
     L.total = 2 * o + ((D + 3) & ~3);
+    return L;
+}
+
+// The pack's LDS image in a pass: the layer-2 transpose w2t only where BWD2 reads it, so every
+// other pass fits two workgroups per CU (H = 64, d = 2: 94 -> 62 KB of LDS per workgroup);
+// BWD2K (one net per workgroup) holds only its net's image.
+__host__ __device__ constexpr bool train_stage_w2t(int stage) { return stage == TS_BWD2 || stage == TS_BWD2K; }
+#ifndef NFX_TRAIN_NET1
+#define NFX_TRAIN_NET1 1
+#endif
+__host__ __device__ constexpr int train_stage_nets(int stage) { return (stage == TS_BWD2K && NFX_TRAIN_NET1) ? 1 : 2; }
+
+__host__ __device__ constexpr TrainLayout train_lds_layout(int D, int HT, bool w2t, int nets) {
+    TrainLayout L = train_layout(D, HT);
+    const int cut = w2t ? 0 : HT * HT * 1024;
+    if (!w2t) L.w2t = -1;
+    L.w1c -= cut;
+    L.m2 -= cut;
+    L.r2 -= cut;
+    L.net -= cut;
+    L.mask = nets * L.net;
+    L.total = nets * L.net + ((D + 3) & ~3);
     return L;
 }
 
@@ -123,25 +153,49 @@ struct TrainRow {
     float v[D];
 };
 
-template <int HT, int D, int STAGE>
-__global__ __launch_bounds__(256) void affine_train_kernel(
+// keep: the raw layer-2 pre-activations h2 = W2 a1 + b2 of both nets, [tile][net][HT][16][64]
+// (accumulator layout, lane-contiguous): written by STATS2 when non-null, read by the K stages.
+// Passes whose register use is held to 256 (2 waves per SIMD; the LDS image admits 2
+// workgroups per CU) at the cost of a few scratch spills.
+#ifndef NFX_TRAIN_W2_MASK
+#define NFX_TRAIN_W2_MASK ((1 << TS_BWD1K) | (1 << TS_BWD2K))
+#endif
+__host__ __device__ constexpr int train_waves_per_eu(int stage) { return ((NFX_TRAIN_W2_MASK) >> stage) & 1 ? 2 : 1; }
+
+template <int HT, int D, int TSTAGE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves_per_eu(TSTAGE)))) void affine_train_kernel(
     const float* __restrict__ pack, const float* __restrict__ x, const float* __restrict__ gy,
     const float* __restrict__ gld, float* __restrict__ gx, float* __restrict__ gbuf,
     const double* __restrict__ G, const double* __restrict__ stats2, void* __restrict__ part,
-    int64_t B, int d, int dir, int64_t ntiles) {
-    constexpr TrainLayout L = train_layout(D, HT);
+    float* __restrict__ keep, float* __restrict__ dlb, int64_t B, int d, int dir, int64_t ntiles) {
+    constexpr bool KEEP = TSTAGE == TS_BWD1K || TSTAGE == TS_BWD2K || TSTAGE == TS_OUTK;
+    constexpr bool NET1 = train_stage_nets(TSTAGE) == 1;  // one net per workgroup: net = blockIdx.y
+    constexpr int STAGE = TSTAGE == TS_BWD1K ? TS_BWD1 : (TSTAGE == TS_BWD2K ? TS_BWD2 : TSTAGE);
+    constexpr TrainLayout PL = train_layout(D, HT);                          // the pack in HBM
+    constexpr TrainLayout L = train_lds_layout(D, HT, train_stage_w2t(TSTAGE), train_stage_nets(TSTAGE));  // LDS image
+    const int net = NET1 ? (int)blockIdx.y : 0;
     constexpr TrainGrad GL = train_grad_layout(D, HT);
     constexpr int KS1 = L.KS1;
     constexpr int Hp = 32 * HT;
     constexpr int PACKF = (L.total + 3) & ~3;
+    static_assert(L.net % 4 == 0 && L.w1c % 4 == 0 && PL.w1c % 4 == 0 && PL.net % 4 == 0, "16-byte pack pieces");
     extern __shared__ f32x4 lds4[];
     float* sm = reinterpret_cast<float*>(lds4);
     float* tbuf_all = sm + PACKF;                        // 4 x 32 x kTS
     float* sbuf_all = tbuf_all + 4 * 32 * kTS;           // 4 x 32 x (2D)  per-sample scratch
     float* kc = sbuf_all + 4 * 32 * 2 * D;               // [2 nets][2][Hp] BN-backward constants
     {
-        const f32x4* src = reinterpret_cast<const f32x4*>(pack);
-        for (int i = threadIdx.x; i < PACKF / 4; i += 256) lds4[i] = src[i];
+        for (int i = threadIdx.x; i < PACKF / 4; i += 256) {
+            const int f = 4 * i;  // LDS float index -> pack float index (w2t skipped unless kept)
+            int src;
+            if (f >= L.mask) {
+                src = PL.mask + (f - L.mask);
+            } else {
+                const int n = NET1 ? 0 : (f >= L.net), o = f - n * L.net;
+                src = (NET1 ? net : n) * PL.net + (o < L.w1c ? o : o + (PL.w1c - L.w1c));
+            }
+            lds4[i] = *reinterpret_cast<const f32x4*>(pack + src);
+        }
     }
     if constexpr (STAGE == TS_BWD2 || STAGE == TS_BWD3) {
         // k1 = sum g / N, k2 = sum g x^ / N in accumulator order, N = the batch the statistics
@@ -202,13 +256,17 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
     // Software pipeline: the next tile's per-sample inputs (x row, upstream gradients, and in
     // BWD3 the g_y1 tiles) are loaded while the current tile computes. Out-of-range lanes load
     // a clamped valid address and zero the value.
-    constexpr bool GRADS = STAGE == TS_BWD1 || STAGE == TS_BWD2;
-    constexpr int NGQ = STAGE == TS_BWD3 ? 2 * HT * 16 : 1;
+    constexpr bool GRADS = STAGE == TS_BWD1 || (STAGE == TS_BWD2 && !NET1);
+    // NET1 loads its kept tile at the top of the iteration (a register double buffer pushed it
+    // to 1 wave per SIMD and measured ~2x slower); BWD3 with or without the prefetch measured equal
+    constexpr bool QPRE = !NET1 && (KEEP || STAGE == TS_BWD3);
+    constexpr int NGQ = QPRE ? 2 * HT * 16 : 1;
     struct Fetch {
         float xr[D];
         float gyr[D];
         float gl;
         float gq[NGQ];
+        float dl[D];  // NET1: the net's delta3 row from BWD1K
     };
     auto fetch = [&](int64_t tile, Fetch& f) {
         const int64_t s = tile * 32 + col;
@@ -228,11 +286,18 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
             const float v = gld[sc];
             f.gl = ok ? v : 0.f;
         }
-        if constexpr (STAGE == TS_BWD3) {
+        if constexpr (QPRE) {  // g_y1 tiles (BWD3) / kept h2 tiles
             const int64_t tc = tile < ntiles ? tile : 0;
-            const float* gq = gbuf + (tc * 2 * HT * 16) * 64 + lane;
+            const float* gq = (KEEP ? keep : gbuf) + ((tc * 2 + net) * HT * 16) * 64 + lane;
 #pragma unroll
             for (int q = 0; q < NGQ; ++q) f.gq[q] = gq[q * 64];
+        }
+        if constexpr (NET1) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const float v = dlb[(sc * 2 + net) * D + j];
+                f.dl[j] = ok ? v : 0.f;
+            }
         }
     };
 
@@ -313,6 +378,65 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
             st_s2[n][ht] += (double)s2;
         };
 
+        // BWD2 after e2 of net n: a1 of the net again (layer 1 is K = d: cheap) and its
+        // pre-activation for the ReLU, db2 / dW2 sums into accumulator slot sl, g_a1 = (diag(r2)
+        // W2)^T e2 -> relu backward -> the g_y1 tiles to HBM, BN1 sums.
+        auto bwd2_tail = [&](const float* P, int n, int sl, const f32x16 (&e2t)[HT]) {
+            f32x16 xh1[HT], a1[HT];
+            layer1(P, xh1);
+            bn_relu(P + L.g1, P + L.e1, xh1, a1);
+            float Te[HT][16];
+#pragma unroll
+            for (int o = 0; o < HT; ++o) {
+                transpose_tile(tbuf, e2t[o], Te[o]);
+                float sb = 0.f;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) sb += Te[o][t];
+                ac_db[sl][o] += sb;
+            }
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt) {
+                float Ta[16];
+                transpose_tile(tbuf, a1[kt], Ta);
+#pragma unroll
+                for (int o = 0; o < HT; ++o)
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) ac_dw[sl][o][kt] = mfma32(Te[o][t], Ta[t], ac_dw[sl][o][kt]);
+            }
+            // g_a1 = (diag(r2) W2)^T e2, relu backward, BN1 sums, g_y1 to HBM
+            const f32x4* wt = reinterpret_cast<const f32x4*>(P + L.w2t) + lane;
+#pragma unroll
+            for (int kt = 0; kt < HT; ++kt) {
+                f32x16 ga;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ga[r] = 0.f;
+#pragma unroll
+                for (int o = 0; o < HT; ++o)
+#pragma unroll
+                    for (int rq = 0; rq < 4; ++rq) {
+                        const f32x4 w = wt[((kt * HT + o) * 4 + rq) * 64];
+#pragma unroll
+                        for (int rr = 0; rr < 4; ++rr) ga = mfma32(w[rr], e2t[o][4 * rq + rr], ga);
+                    }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) ga[r] = a1[kt][r] > 0.f ? ga[r] : 0.f;
+                float* gp = gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64 + lane;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) gp[r * 64] = ga[r];
+                float Tg[16], Tx[16];
+                transpose_tile(tbuf, ga, Tg);
+                transpose_tile(tbuf, xh1[kt], Tx);
+                float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    s1 += Tg[t];
+                    s2 = fmaf(Tg[t], Tx[t], s2);
+                }
+                ac_s1[sl][kt] += s1;
+                ac_s2[sl][kt] += s2;
+            }
+        };
+
         if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
 #pragma unroll
             for (int n = 0; n < 2; ++n) {
@@ -326,11 +450,109 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                     f32x16 a1[HT], h2[HT];
                     bn_relu(P + L.g1, P + L.e1, xh1, a1);
                     layer2(P, a1, h2);
+                    if (keep) {  // (the pack folds no layer-2 statistics here: h2 is raw)
+#pragma unroll
+                        for (int ht = 0; ht < HT; ++ht) {
+                            float* kp = keep + (((tile * 2 + n) * HT + ht) * 16) * 64 + lane;
+#pragma unroll
+                            for (int r = 0; r < 16; ++r) kp[r * 64] = h2[ht][r];
+                        }
+                    }
 #pragma unroll
                     for (int ht = 0; ht < HT; ++ht) stats_tile(n, ht, h2[ht]);
                 }
             }
             st_n += (double)nvh;
+        } else if constexpr (TSTAGE == TS_OUTK) {
+            // ---- forward output from the kept h2 (OUTK: gx = y, dlb = log-det), with the
+            // epilogue of the streaming eval kernel (nfx_affine_kernel.h) ----------------------
+            float outv[2][D];
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const float* P = smi + n * L.net;
+                float pj[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) pj[j] = 0.f;
+#pragma unroll
+                for (int o = 0; o < HT; ++o) {
+                    const f32x16 m = load_bias16(P + L.m2 + o * 32, h), rs = load_bias16(P + L.r2 + o * 32, h);
+                    const f32x16 g = load_bias16(P + L.g2 + o * 32, h), e = load_bias16(P + L.e2 + o * 32, h);
+                    f32x16 a2;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        a2[r] = trelu(fmaf(g[r], (cur.gq[(n * HT + o) * 16 + r] - m[r]) * rs[r], e[r]));
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + o) * 32, h);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) pj[j] = fmaf(w3[r], a2[r], pj[j]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j) outv[n][j] = halves_sum(pj[j], pj[j]) + P[L.b3 + j];
+            }
+            if (h == 0 && valid) {
+#pragma clang fp contract(off)  // separate mul/add roundings, as the reference's torch ops
+                float ld = 0.f, yv[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const float sv = tclamp(outv[0][j], -10.f, 10.f), bv = tclamp(outv[1][j], -10.f, 10.f);
+                    const float m = mk[j], om = 1.f - m;
+                    const float xa = xr[j] * m;
+                    float t;
+                    if (dir < 0) {
+                        t = (xr[j] - bv) * exp_fast(-sv);
+                        ld = ld + om * (-sv);
+                    } else {
+                        t = xr[j] * exp_fast(sv) + bv;
+                        ld = ld + om * sv;
+                    }
+                    const float v = xa + om * t;
+                    yv[j] = nonfinite(v) ? 0.f : v;
+                }
+                if (nonfinite(ld)) ld = 0.f;
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    if (j < d) gx[s * d + j] = yv[j];
+                dlb[s] = ld;
+            }
+        } else if constexpr (NET1) {
+            // ---- BWD2, net `net` only: x^2 from the kept h2, delta3 from BWD1K -------------
+            const float* P = smi;
+            float kq[HT * 16];  // the net's kept h2 tile (loaded here: no register double buffer)
+            {
+                const float* q = keep + ((tile * 2 + net) * HT * 16) * 64 + lane;
+#pragma unroll
+                for (int i = 0; i < HT * 16; ++i) kq[i] = q[i * 64];
+            }
+            f32x16 e2t[HT];
+#pragma unroll
+            for (int o = 0; o < HT; ++o) {
+                const f32x16 m = load_bias16(P + L.m2 + o * 32, h), rs = load_bias16(P + L.r2 + o * 32, h);
+                const f32x16 g = load_bias16(P + L.g2 + o * 32, h), e = load_bias16(P + L.e2 + o * 32, h);
+                f32x16 xh2, gy2, a2;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    xh2[r] = (kq[o * 16 + r] - m[r]) * rs[r];
+                    a2[r] = trelu(fmaf(g[r], xh2[r], e[r]));
+                    gy2[r] = 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const f32x16 w3 = load_bias16(P + L.w3 + (j * HT + o) * 32, h);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) gy2[r] = fmaf(w3[r], cur.dl[j], gy2[r]);
+                }
+                const f32x16 k1 = load_bias16(kci + (net * 2 + 0) * Hp + o * 32, h);
+                const f32x16 k2 = load_bias16(kci + (net * 2 + 1) * Hp + o * 32, h);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float gr = a2[r] > 0.f ? gy2[r] : 0.f;  // relu backward
+                    const float v = g[r] * ((gr - k1[r]) - xh2[r] * k2[r]);
+                    e2t[o][r] = valid ? v : 0.f;
+                }
+            }
+            bwd2_tail(P, net, 0, e2t);
         } else if constexpr (STAGE == TS_BWD1 || STAGE == TS_BWD2) {
             // ---- recompute the forward of both nets (layer-2 x^2 kept for both) ----------
             f32x16 xh2[2][HT];
@@ -338,10 +560,20 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
 #pragma unroll
             for (int n = 0; n < 2; ++n) {
                 const float* P = smi + n * L.net;
-                f32x16 xh1[HT], a1[HT];
-                layer1(P, xh1);
-                bn_relu(P + L.g1, P + L.e1, xh1, a1);
-                layer2(P, a1, xh2[n]);
+                if constexpr (KEEP) {
+                    // x^2 = (h2 - mu2) r2 from the kept pre-activations
+#pragma unroll
+                    for (int o = 0; o < HT; ++o) {
+                        const f32x16 m = load_bias16(P + L.m2 + o * 32, h), rs = load_bias16(P + L.r2 + o * 32, h);
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) xh2[n][o][r] = (cur.gq[(n * HT + o) * 16 + r] - m[r]) * rs[r];
+                    }
+                } else {
+                    f32x16 xh1[HT], a1[HT];
+                    layer1(P, xh1);
+                    bn_relu(P + L.g1, P + L.e1, xh1, a1);
+                    layer2(P, a1, xh2[n]);
+                }
                 float pj[D];
 #pragma unroll
                 for (int j = 0; j < D; ++j) pj[j] = 0.f;
@@ -413,6 +645,12 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
 #pragma unroll
                     for (int j = 0; j < D; ++j)
                         if (j < d) gx[s * d + j] = gxd[j];
+                    if constexpr (KEEP) {  // delta3 of both nets for BWD2K
+#pragma unroll
+                        for (int n = 0; n < 2; ++n)
+#pragma unroll
+                            for (int j = 0; j < D; ++j) dlb[(s * 2 + n) * D + j] = dl[n][j];
+                    }
                 }
                 // per-sample delta3 of both nets for the transposed dW3 sums
                 if (h == 0) {
@@ -479,62 +717,7 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                         }
                     }
                 }
-                if constexpr (STAGE == TS_BWD2) {
-                    // a1 of net n again (layer 1 is K = d: cheap), its pre-activation y1 for the ReLU
-                    f32x16 xh1[HT], a1[HT];
-                    layer1(P, xh1);
-                    bn_relu(P + L.g1, P + L.e1, xh1, a1);
-                    float Te[HT][16];
-#pragma unroll
-                    for (int o = 0; o < HT; ++o) {
-                        transpose_tile(tbuf, e2t[o], Te[o]);
-                        float sb = 0.f;
-#pragma unroll
-                        for (int t = 0; t < 16; ++t) sb += Te[o][t];
-                        ac_db[n][o] += sb;
-                    }
-#pragma unroll
-                    for (int kt = 0; kt < HT; ++kt) {
-                        float Ta[16];
-                        transpose_tile(tbuf, a1[kt], Ta);
-#pragma unroll
-                        for (int o = 0; o < HT; ++o)
-#pragma unroll
-                            for (int t = 0; t < 16; ++t) ac_dw[n][o][kt] = mfma32(Te[o][t], Ta[t], ac_dw[n][o][kt]);
-                    }
-                    // g_a1 = (diag(r2) W2)^T e2, relu backward, BN1 sums, g_y1 to HBM
-                    const f32x4* wt = reinterpret_cast<const f32x4*>(P + L.w2t) + lane;
-#pragma unroll
-                    for (int kt = 0; kt < HT; ++kt) {
-                        f32x16 ga;
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) ga[r] = 0.f;
-#pragma unroll
-                        for (int o = 0; o < HT; ++o)
-#pragma unroll
-                            for (int rq = 0; rq < 4; ++rq) {
-                                const f32x4 w = wt[((kt * HT + o) * 4 + rq) * 64];
-#pragma unroll
-                                for (int rr = 0; rr < 4; ++rr) ga = mfma32(w[rr], e2t[o][4 * rq + rr], ga);
-                            }
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) ga[r] = a1[kt][r] > 0.f ? ga[r] : 0.f;
-                        float* gp = gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64 + lane;
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) gp[r * 64] = ga[r];
-                        float Tg[16], Tx[16];
-                        transpose_tile(tbuf, ga, Tg);
-                        transpose_tile(tbuf, xh1[kt], Tx);
-                        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-                        for (int t = 0; t < 16; ++t) {
-                            s1 += Tg[t];
-                            s2 = fmaf(Tg[t], Tx[t], s2);
-                        }
-                        ac_s1[n][kt] += s1;
-                        ac_s2[n][kt] += s2;
-                    }
-                }
+                if constexpr (STAGE == TS_BWD2) bwd2_tail(P, n, n, e2t);
             }
         } else {  // TS_BWD3: layer 1 only
             if (h == 0) {
@@ -599,9 +782,13 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
     float* red = sm;
     double* redd = reinterpret_cast<double*>(sm);
     constexpr int LEN = STAGE == TS_BWD1 ? GL.len1 : (STAGE == TS_BWD2 ? GL.len2 : (STAGE == TS_BWD3 ? GL.len3 : 0));
+    if constexpr (NET1) {  // the other net's entries of this workgroup's partial stay zero
+        for (int i = threadIdx.x; i < LEN; i += 256) red[i] = 0.f;
+        __syncthreads();
+    }
     for (int rnd = 0; rnd < 4; ++rnd) {
         if (wave == rnd) {
-            auto put = [&](int idx, float v) { red[idx] = rnd ? red[idx] + v : v; };
+            auto put = [&](int idx, float v) { red[idx] = (rnd || NET1) ? red[idx] + v : v; };
             if constexpr (STAGE == TS_STATS1 || STAGE == TS_STATS2) {
                 // per lane (n, mean, M2) of its half's samples; merge the halves (same features)
 #pragma unroll
@@ -660,19 +847,20 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                     }
             } else if constexpr (STAGE == TS_BWD2) {
 #pragma unroll
-                for (int n = 0; n < 2; ++n) {
+                for (int n = 0; n < (NET1 ? 1 : 2); ++n) {
+                    const int nd = NET1 ? net : n;  // the net whose G block slot n holds
 #pragma unroll
                     for (int ht = 0; ht < HT; ++ht) {
                         const float a = halves_sum(ac_s1[n][ht], ac_s1[n][ht]);
                         const float b = halves_sum(ac_s2[n][ht], ac_s2[n][ht]);
                         const float c = halves_sum(ac_db[n][ht], ac_db[n][ht]);
                         if (h == 0) {
-                            put((n * 2 + 0) * Hp + 32 * ht + col, a);
-                            put((n * 2 + 1) * Hp + 32 * ht + col, b);
-                            put(4 * Hp + n * (Hp * Hp + Hp) + Hp * Hp + 32 * ht + col, c);
+                            put((nd * 2 + 0) * Hp + 32 * ht + col, a);
+                            put((nd * 2 + 1) * Hp + 32 * ht + col, b);
+                            put(4 * Hp + nd * (Hp * Hp + Hp) + Hp * Hp + 32 * ht + col, c);
                         }
                     }
-                    const int pdw = 4 * Hp + n * (Hp * Hp + Hp);
+                    const int pdw = 4 * Hp + nd * (Hp * Hp + Hp);
 #pragma unroll
                     for (int o = 0; o < HT; ++o)
 #pragma unroll
@@ -681,7 +869,7 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
                             for (int r = 0; r < 16; ++r)
                                 put(pdw + (32 * o + crow(r, h)) * Hp + 32 * kt + col, ac_dw[n][o][kt][r]);
                 }
-            } else {
+            } else if constexpr (STAGE == TS_BWD3) {
 #pragma unroll
                 for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -702,20 +890,23 @@ __global__ __launch_bounds__(256) void affine_train_kernel(
         double* pw = reinterpret_cast<double*>(part) + (int64_t)blockIdx.x * (2 * Hp * 3);
         for (int i = threadIdx.x; i < 2 * Hp * 3; i += 256) pw[i] = redd[i];
     } else {
-        float* pw = reinterpret_cast<float*>(part) + (int64_t)blockIdx.x * LEN;
+        float* pw = reinterpret_cast<float*>(part) + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * LEN;
         for (int i = threadIdx.x; i < LEN; i += 256) pw[i] = red[i];
     }
 }
 
 typedef void (*affine_train_kernel_t)(const float*, const float*, const float*, const float*, float*, float*,
-                                      const double*, const double*, void*, int64_t, int, int, int64_t);
+                                      const double*, const double*, void*, float*, float*, int64_t, int, int,
+                                      int64_t);
 
 template <int HT>
 affine_train_kernel_t affine_train_pick_ht(int D, int stage);
 
-// LDS bytes of affine_train_kernel<HT, D, *>
-__host__ __device__ constexpr size_t affine_train_lds(int D, int HT) {
-    return (size_t)(((train_layout(D, HT).total + 3) & ~3) + 4 * 32 * kTS + 4 * 32 * 2 * D + 4 * 32 * HT) *
+// LDS bytes of affine_train_kernel<HT, D, stage>
+__host__ __device__ constexpr size_t affine_train_lds(int D, int HT, int stage) {
+    return (size_t)(((train_lds_layout(D, HT, train_stage_w2t(stage), train_stage_nets(stage)).total + 3) & ~3) +
+                    4 * 32 * kTS +
+                    4 * 32 * 2 * D + 4 * 32 * HT) *
            sizeof(float);
 }
 

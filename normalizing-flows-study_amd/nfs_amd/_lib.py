@@ -46,7 +46,8 @@ EXPORTED_SYMBOLS = (
     "nfx_affine_train_pack_floats", "nfx_affine_train_stats_doubles", "nfx_affine_train_grad_doubles",
     "nfx_affine_train_param_floats", "nfx_affine_train_workspace_bytes", "nfx_affine_train_pack",
     "nfx_affine_train_stats", "nfx_affine_train_update_running", "nfx_affine_train_backward",
-    "nfx_affine_train_assemble", "nfx_affine_eval_stats",
+    "nfx_affine_train_assemble", "nfx_affine_eval_stats", "nfx_affine_train_keep_floats",
+    "nfx_affine_train_stats_keep", "nfx_affine_train_backward_keep", "nfx_affine_train_output",
     "nfx_spline_backward_packed_floats", "nfx_spline_backward_param_floats",
     "nfx_spline_backward_workspace_bytes", "nfx_spline_pack_backward", "nfx_spline_coupling_backward",
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob", "nfx_gauss_logprob_backward",
@@ -183,6 +184,11 @@ _SIGNATURES = {
     "nfx_affine_train_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp, _vp, _vp,
                                          _vp]),
     "nfx_affine_train_assemble": (_int, [_vp, _vp, _vp, _int, _int, _f, _vp, _vp]),
+    "nfx_affine_train_keep_floats": (_sz, [_i64, _int, _int]),
+    "nfx_affine_train_stats_keep": (_int, [_vp, _vp, _i64, _int, _int, _int, _vp, _vp, _vp, _vp]),
+    "nfx_affine_train_backward_keep": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp, _vp,
+                                              _vp, _vp, _vp]),
+    "nfx_affine_train_output": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _vp]),
     "nfx_affine_eval_stats": (_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int, _vp, _vp, _vp]),
     "nfx_spline_backward_packed_floats": (_sz, [_int, _int, _int]),
     "nfx_spline_backward_param_floats": (_sz, [_int, _int, _int]),

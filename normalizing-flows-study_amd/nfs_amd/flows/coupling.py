@@ -104,7 +104,7 @@ class _CouplingTrainFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, layer, direction, x, *params):
-        y, ld, tpack, stats = layer._train_forward(x, direction)
+        y, ld, tpack, stats = layer._train_forward(x, direction, keep=True)
         ctx.layer = layer
         ctx.direction = direction
         ctx.tpack = tpack
@@ -352,9 +352,12 @@ class CouplingLayer(HipFlow):
         b_raw, k2 = _lib.mlp_raw([self.b_net[0], self.b_net[3], self.b_net[6]], [self.b_net[1], self.b_net[4]])
         return s_raw, b_raw, (k1, k2)
 
-    def _train_forward(self, x, direction):
+    def _train_forward(self, x, direction, keep=False):
         """Batch statistics (2 passes, SyncBN merge between them), the fused layer with the
-        statistics folded in, running-statistics update. Returns (y, ld, tpack, stats)."""
+        statistics folded in, running-statistics update. Returns (y, ld, tpack, stats). keep=True
+        (a forward the backward will follow): the layer-2 statistics pass also keeps the raw
+        layer-2 pre-activations in HBM (tpack._nfx_h2, 512 B per sample at H = 64) for the
+        backward's first two passes, which then skip recomputing layers 1-2."""
         if not self._fused_train():
             return self._generic_train_forward(x, direction)
         L = _lib.lib()
@@ -363,13 +366,16 @@ class CouplingLayer(HipFlow):
         H = self._hidden()
         dev = x.device
         st = _lib.stream_of(x)
-        s_raw, b_raw, keep = self._raw_nets()
+        s_raw, b_raw, keep_src = self._raw_nets()
         mask = self.mask.detach().to(device=dev, dtype=torch.float32).contiguous()
         nst = L.nfx_affine_train_stats_doubles(H)
         stats = torch.empty(2, nst, device=dev, dtype=torch.float64)
         tpack = torch.empty(L.nfx_affine_train_pack_floats(d, H), device=dev, dtype=torch.float32)
         epack = torch.empty(L.nfx_affine_packed_floats(d, H), device=dev, dtype=torch.float32)
         ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
+        keep = keep and os.environ.get("NFX_TRAIN_KEEP", "1") != "0"  # 0: the backward recomputes
+        nkeep = L.nfx_affine_train_keep_floats(B, d, H) if keep else 0
+        h2 = torch.empty(nkeep, device=dev, dtype=torch.float32) if nkeep else None
         ev = TRAIN_EVENTS
         p = _lib.ptr
         _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), None, None, d, H, p(tpack), None, st),
@@ -378,7 +384,8 @@ class CouplingLayer(HipFlow):
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            _lib.check(L.nfx_affine_train_stats(p(tpack), p(x), B, d, H, layer, p(stats[layer - 1]), p(ws), st),
+            _lib.check(L.nfx_affine_train_stats_keep(p(tpack), p(x), B, d, H, layer, p(stats[layer - 1]), p(ws),
+                                                     p(h2) if (h2 is not None and layer == 2) else None, st),
                        "nfx_affine_train_stats")
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
@@ -394,12 +401,16 @@ class CouplingLayer(HipFlow):
         if ev is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        _lib.check(L.nfx_affine_coupling(p(epack), p(x), p(y), p(ld), B, d, H, int(direction), 0, st),
-                   "nfx_affine_coupling")
+        if h2 is not None:  # from the kept pre-activations (no layer 1-2 recompute)
+            _lib.check(L.nfx_affine_train_output(p(tpack), p(x), p(h2), p(y), p(ld), B, d, H, int(direction), st),
+                       "nfx_affine_train_output")
+        else:
+            _lib.check(L.nfx_affine_coupling(p(epack), p(x), p(y), p(ld), B, d, H, int(direction), 0, st),
+                       "nfx_affine_coupling")
         if ev is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            ev.append(("affine_coupling_kernel", e0, e1))
+            ev.append(("affine_train_kernel<OUTK>" if h2 is not None else "affine_coupling_kernel", e0, e1))
         bns = [self.s_net[1], self.s_net[4], self.b_net[1], self.b_net[4]]
         rm = (ctypes_vp * 4)(*[bn.running_mean.data_ptr() for bn in bns])
         rv = (ctypes_vp * 4)(*[bn.running_var.data_ptr() for bn in bns])
@@ -409,7 +420,8 @@ class CouplingLayer(HipFlow):
             torch.autograd.graph.increment_version(bn.running_mean)
             torch.autograd.graph.increment_version(bn.running_var)
         torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
-        tpack._nfx_keep = (keep, mask, epack, ws)  # sources alive while the kernels are queued
+        tpack._nfx_keep = (keep_src, mask, epack, ws)  # sources alive while the kernels are queued
+        tpack._nfx_h2 = h2
         return y, ld, tpack, stats
 
     # -- eval mode under autograd (running-statistics BatchNorm) -----------------------------
@@ -469,14 +481,18 @@ class CouplingLayer(HipFlow):
         ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
         Hp, D = 32 * ((H + 31) // 32), _pad_d(d)
         s_blocks = {1: G[0:4 * Hp], 2: G[4 * Hp + 2 * (D * Hp + D):][:4 * Hp]}
+        h2 = getattr(tpack, "_nfx_h2", None)  # kept by a train-mode forward (else: recompute)
         p = _lib.ptr
         ev = TRAIN_EVENTS
         for stage in (1, 2, 3):
             if ev is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            _lib.check(L.nfx_affine_train_backward(p(tpack), p(x), p(gy), p(gld), p(gx), B, d, H, int(direction),
-                                                   stage, p(stats[1]), p(G), p(ws), st), "nfx_affine_train_backward")
+            kept = h2 if stage < 3 else None
+            _lib.check(L.nfx_affine_train_backward_keep(p(tpack), p(x), p(gy), p(gld), p(gx), B, d, H,
+                                                        int(direction), stage, p(stats[1]), p(G), p(ws),
+                                                        p(kept) if kept is not None else None, st),
+                       "nfx_affine_train_backward")
             if ev is not None:
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record()

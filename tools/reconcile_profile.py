@@ -42,7 +42,7 @@ HOT = {
     "trainfig_maf": ("made_bwd_kernel",),
     "trainfig_spline": ("spline_bwd_kernel",),
     "cfg4t": ("made_bwd_kernel",),
-    "cfg2t": ("affine_train_kernel<2, 2, 3>",),  # BWD2, the bench's event-timed pass
+    "cfg2t": ("affine_train_kernel<2, 2, 3>", "affine_train_kernel<2, 2, 6>"),  # BWD2 / BWD2K (event-timed)
     "cfg3t": ("spline_bwd_kernel",),
 }
 PER_PASS = ("gauss_finish_kernel",)  # once per log_prob pass besides the layer kernels
