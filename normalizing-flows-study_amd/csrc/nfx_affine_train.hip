@@ -581,7 +581,10 @@ extern "C" int nfx_affine_train_output(const float* tpack, const float* x, const
     affine_train_kernel_t k = pick_train(HT, D, TS_OUTK);
     const size_t lds = affine_train_lds(D, HT, TS_OUTK);
     if ((rc = prepare_lds((const void*)k, lds))) return rc;
-    const TrainGrid g = train_grid(k, lds, B);
+    // no per-workgroup partials: the grid is every resident workgroup (not capped at 2 per CU)
+    TrainGrid g;
+    g.ntiles = (B + 31) / 32;
+    g.grid = resident_grid((const void*)k, 256, lds, (g.ntiles + 3) / 4);
     k<<<g.grid, 256, lds, (hipStream_t)stream>>>(tpack, x, nullptr, nullptr, y, nullptr, nullptr, nullptr, nullptr,
                                                  const_cast<float*>(keep), log_det, B, d, direction, g.ntiles);
     return check_launch("affine_train_kernel(output)");

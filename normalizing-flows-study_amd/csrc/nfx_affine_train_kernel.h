@@ -78,6 +78,25 @@ __host__ __device__ constexpr bool train_stage_w2t(int stage) { return stage == 
 #endif
 __host__ __device__ constexpr int train_stage_nets(int stage) { return (stage == TS_BWD2K && NFX_TRAIN_NET1) ? 1 : 2; }
 
+// OUTK reads only the layer-2 BatchNorm / output-layer block [c2, w2t) and m2, r2 of each net
+// (3.6 KB at H = 64, d = 2): occupancy is then set by the registers alone.
+__host__ __device__ constexpr TrainLayout train_lds_layout_out(int D, int HT) {
+    TrainLayout L = train_layout(D, HT);
+    const int cut = L.c2, piece = L.w2t - L.c2;
+    L.w1 = L.c1 = L.g1 = L.e1 = L.w2 = L.w2t = L.w1c = -1;
+    L.c2 -= cut;
+    L.g2 -= cut;
+    L.e2 -= cut;
+    L.w3 -= cut;
+    L.b3 -= cut;
+    L.m2 = piece;
+    L.r2 = piece + HT * 32;
+    L.net = piece + 2 * HT * 32;
+    L.mask = 2 * L.net;
+    L.total = 2 * L.net + ((D + 3) & ~3);
+    return L;
+}
+
 __host__ __device__ constexpr TrainLayout train_lds_layout(int D, int HT, bool w2t, int nets) {
     TrainLayout L = train_layout(D, HT);
     const int cut = w2t ? 0 : HT * HT * 1024;
@@ -153,17 +172,23 @@ struct TrainRow {
     float v[D];
 };
 
-// keep: the raw layer-2 pre-activations h2 = W2 a1 + b2 of both nets, [tile][net][HT][16][64]
-// (accumulator layout, lane-contiguous): written by STATS2 when non-null, read by the K stages.
+// keep: the raw layer-2 pre-activations h2 = W2 a1 + b2 of both nets, [tile][net][HT][4][64 lanes]
+// of 16-byte vectors (accumulator registers 4q..4q+3 of a lane together): written by STATS2 when
+// non-null, read by the K stages. The g_y1 tiles BWD2 hands to BWD3 (gbuf) use the same layout.
+// (Lane-contiguous single floats measured 2.4 % slower on the train step: 4x the memory
+// instructions; a register-major [q][tile][lane] order measured slower still.)
 // Passes whose register use is held to 256 (2 waves per SIMD; the LDS image admits 2
 // workgroups per CU) at the cost of a few scratch spills.
 #ifndef NFX_TRAIN_W2_MASK
 #define NFX_TRAIN_W2_MASK ((1 << TS_BWD1K) | (1 << TS_BWD2K))
 #endif
-__host__ __device__ constexpr int train_waves_per_eu(int stage) { return ((NFX_TRAIN_W2_MASK) >> stage) & 1 ? 2 : 1; }
+__host__ __device__ constexpr int train_waves_per_eu(int stage, int D) {
+    // OUTK at d <= 2: 128 registers without spills (4 waves per SIMD)
+    return stage == TS_OUTK ? (D <= 2 ? 4 : 2) : (((NFX_TRAIN_W2_MASK) >> stage) & 1 ? 2 : 1);
+}
 
 template <int HT, int D, int TSTAGE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves_per_eu(TSTAGE)))) void affine_train_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves_per_eu(TSTAGE, D)))) void affine_train_kernel(
     const float* __restrict__ pack, const float* __restrict__ x, const float* __restrict__ gy,
     const float* __restrict__ gld, float* __restrict__ gx, float* __restrict__ gbuf,
     const double* __restrict__ G, const double* __restrict__ stats2, void* __restrict__ part,
@@ -172,13 +197,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
     constexpr bool NET1 = train_stage_nets(TSTAGE) == 1;  // one net per workgroup: net = blockIdx.y
     constexpr int STAGE = TSTAGE == TS_BWD1K ? TS_BWD1 : (TSTAGE == TS_BWD2K ? TS_BWD2 : TSTAGE);
     constexpr TrainLayout PL = train_layout(D, HT);                          // the pack in HBM
-    constexpr TrainLayout L = train_lds_layout(D, HT, train_stage_w2t(TSTAGE), train_stage_nets(TSTAGE));  // LDS image
+    constexpr TrainLayout L = TSTAGE == TS_OUTK ? train_lds_layout_out(D, HT)  // LDS image
+                                                : train_lds_layout(D, HT, train_stage_w2t(TSTAGE), train_stage_nets(TSTAGE));
     const int net = NET1 ? (int)blockIdx.y : 0;
     constexpr TrainGrad GL = train_grad_layout(D, HT);
     constexpr int KS1 = L.KS1;
     constexpr int Hp = 32 * HT;
     constexpr int PACKF = (L.total + 3) & ~3;
-    static_assert(L.net % 4 == 0 && L.w1c % 4 == 0 && PL.w1c % 4 == 0 && PL.net % 4 == 0, "16-byte pack pieces");
+    static_assert(L.net % 4 == 0 && L.m2 % 4 == 0 && (L.w1c % 4 == 0 || TSTAGE == TS_OUTK) && PL.w1c % 4 == 0 &&
+                      PL.net % 4 == 0 && PL.c2 % 4 == 0 && PL.m2 % 4 == 0,
+                  "16-byte pack pieces");
     extern __shared__ f32x4 lds4[];
     float* sm = reinterpret_cast<float*>(lds4);
     float* tbuf_all = sm + PACKF;                        // 4 x 32 x kTS
@@ -192,7 +220,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
                 src = PL.mask + (f - L.mask);
             } else {
                 const int n = NET1 ? 0 : (f >= L.net), o = f - n * L.net;
-                src = (NET1 ? net : n) * PL.net + (o < L.w1c ? o : o + (PL.w1c - L.w1c));
+                if constexpr (TSTAGE == TS_OUTK)
+                    src = n * PL.net + (o < L.m2 ? PL.c2 + o : PL.m2 + (o - L.m2));
+                else
+                    src = (NET1 ? net : n) * PL.net + (o < L.w1c ? o : o + (PL.w1c - L.w1c));
             }
             lds4[i] = *reinterpret_cast<const f32x4*>(pack + src);
         }
@@ -288,9 +319,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
         }
         if constexpr (QPRE) {  // g_y1 tiles (BWD3) / kept h2 tiles
             const int64_t tc = tile < ntiles ? tile : 0;
-            const float* gq = (KEEP ? keep : gbuf) + ((tc * 2 + net) * HT * 16) * 64 + lane;
+            const f32x4* gq = reinterpret_cast<const f32x4*>((KEEP ? keep : gbuf) + ((tc * 2 + net) * HT * 16) * 64) + lane;
 #pragma unroll
-            for (int q = 0; q < NGQ; ++q) f.gq[q] = gq[q * 64];
+            for (int q4 = 0; q4 < NGQ / 4; ++q4) {
+                const f32x4 v = gq[q4 * 64];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) f.gq[4 * q4 + c] = v[c];
+            }
         }
         if constexpr (NET1) {
 #pragma unroll
@@ -420,9 +455,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
                     }
 #pragma unroll
                 for (int r = 0; r < 16; ++r) ga[r] = a1[kt][r] > 0.f ? ga[r] : 0.f;
-                float* gp = gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64 + lane;
+                f32x4* gp = reinterpret_cast<f32x4*>(gbuf + (((tile * 2 + n) * HT + kt) * 16) * 64) + lane;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) gp[r * 64] = ga[r];
+                for (int rq = 0; rq < 4; ++rq)
+                    gp[rq * 64] = f32x4{ga[4 * rq], ga[4 * rq + 1], ga[4 * rq + 2], ga[4 * rq + 3]};
                 float Tg[16], Tx[16];
                 transpose_tile(tbuf, ga, Tg);
                 transpose_tile(tbuf, xh1[kt], Tx);
@@ -453,9 +489,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
                     if (keep) {  // (the pack folds no layer-2 statistics here: h2 is raw)
 #pragma unroll
                         for (int ht = 0; ht < HT; ++ht) {
-                            float* kp = keep + (((tile * 2 + n) * HT + ht) * 16) * 64 + lane;
+                            f32x4* kp = reinterpret_cast<f32x4*>(keep + (((tile * 2 + n) * HT + ht) * 16) * 64) + lane;
 #pragma unroll
-                            for (int r = 0; r < 16; ++r) kp[r * 64] = h2[ht][r];
+                            for (int rq = 0; rq < 4; ++rq)
+                                kp[rq * 64] = f32x4{h2[ht][4 * rq], h2[ht][4 * rq + 1], h2[ht][4 * rq + 2], h2[ht][4 * rq + 3]};
                         }
                     }
 #pragma unroll
@@ -521,9 +558,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
             const float* P = smi;
             float kq[HT * 16];  // the net's kept h2 tile (loaded here: no register double buffer)
             {
-                const float* q = keep + ((tile * 2 + net) * HT * 16) * 64 + lane;
+                const f32x4* q = reinterpret_cast<const f32x4*>(keep + ((tile * 2 + net) * HT * 16) * 64) + lane;
 #pragma unroll
-                for (int i = 0; i < HT * 16; ++i) kq[i] = q[i * 64];
+                for (int i4 = 0; i4 < HT * 4; ++i4) {
+                    const f32x4 v = q[i4 * 64];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) kq[4 * i4 + c] = v[c];
+                }
             }
             f32x16 e2t[HT];
 #pragma unroll
@@ -776,7 +817,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(train_waves
 
     // ---- workgroup combine: the 4 waves add (merge) their partials into LDS in wave order,
     // then the workgroup writes one partial; the finish kernels reduce workgroups in order ----
-    static_assert(GL.len1 <= PACKF && GL.len2 <= PACKF && GL.len3 <= PACKF && 12 * Hp <= PACKF,
+    static_assert(TSTAGE == TS_OUTK || (GL.len1 <= PACKF && GL.len2 <= PACKF && GL.len3 <= PACKF && 12 * Hp <= PACKF),
                   "reduction buffer must fit the pack region");
     __syncthreads();  // every wave is done with the weight pack: reuse its LDS
     float* red = sm;
@@ -904,6 +945,8 @@ affine_train_kernel_t affine_train_pick_ht(int D, int stage);
 
 // LDS bytes of affine_train_kernel<HT, D, stage>
 __host__ __device__ constexpr size_t affine_train_lds(int D, int HT, int stage) {
+    if (stage == TS_OUTK) return (size_t)(((train_lds_layout_out(D, HT).total + 3) & ~3) + 4 * 32 * kTS +
+                                          4 * 32 * 2 * D + 4 * 32 * HT) * sizeof(float);
     return (size_t)(((train_lds_layout(D, HT, train_stage_w2t(stage), train_stage_nets(stage)).total + 3) & ~3) +
                     4 * 32 * kTS +
                     4 * 32 * 2 * D + 4 * 32 * HT) *
