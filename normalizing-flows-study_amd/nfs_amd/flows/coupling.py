@@ -98,6 +98,18 @@ def _pad_d(d):
     return 2 if d <= 2 else (4 if d <= 4 else 8)
 
 
+_KEEP_BUDGET = {}
+
+
+def _keep_budget(dev):
+    """Bytes one train-mode layer may keep for its backward: 1/32 of the device's memory (the
+    activations of every layer of a model stay alive until its backward)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _KEEP_BUDGET:
+        _KEEP_BUDGET[i] = torch.cuda.get_device_properties(i).total_memory // 32
+    return _KEEP_BUDGET[i]
+
+
 class _CouplingTrainFunction(torch.autograd.Function):
     """Train-mode CouplingLayer on the gfx950 kernels: forward (y, log_det) with batch-statistics
     BatchNorm and running-statistics update; backward = the fused three-pass kernel."""
@@ -375,6 +387,8 @@ class CouplingLayer(HipFlow):
         ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
         keep = keep and os.environ.get("NFX_TRAIN_KEEP", "1") != "0"  # 0: the backward recomputes
         nkeep = L.nfx_affine_train_keep_floats(B, d, H) if keep else 0
+        if nkeep and 4 * nkeep > _keep_budget(dev):
+            nkeep = 0  # a layer's kept copy is capped at 1/32 of HBM (9 GB, 17.6M samples at H = 64)
         h2 = torch.empty(nkeep, device=dev, dtype=torch.float32) if nkeep else None
         ev = TRAIN_EVENTS
         p = _lib.ptr

@@ -237,6 +237,18 @@ def test_recompute_path_vs_float64_autograd(cuda_device, monkeypatch, d, H, B, d
     test_layer_vs_float64_autograd(cuda_device, d, H, B, direction)
 
 
+def test_keep_budget_falls_back_to_recompute(cuda_device, monkeypatch):
+    """A layer keeps its layer-2 pre-activations only within 1/32 of HBM (coupling._keep_budget);
+    past it the forward keeps nothing and the backward recomputes (same float64 bar)."""
+    from nfs_amd.flows import coupling as cp
+    layer = _perturbed_layer(2, 64, 5).to(cuda_device).train()
+    x = torch.randn(1000, 2, device=cuda_device)
+    assert layer._train_forward(x, -1, keep=True)[2]._nfx_h2 is not None
+    monkeypatch.setattr(cp, "_keep_budget", lambda dev: 0)
+    assert layer._train_forward(x, -1, keep=True)[2]._nfx_h2 is None
+    test_layer_vs_float64_autograd(cuda_device, 2, 64, 1000, 1)
+
+
 def test_no_grad_train_forward_updates_running_stats(cuda_device):
     """Under no_grad in train mode BatchNorm still uses (and records) batch statistics."""
     layer = _perturbed_layer(2, 64, 7)
