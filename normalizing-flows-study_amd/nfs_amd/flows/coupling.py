@@ -409,7 +409,8 @@ class CouplingLayer(HipFlow):
             _dist.merge_bn_stats(stats[layer - 1].view(2, -1, 3))
             _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), p(stats[0]),
                                                p(stats[1]) if layer == 2 else None, d, H, p(tpack),
-                                               p(epack) if layer == 2 else None, st), "nfx_affine_train_pack")
+                                               p(epack) if (layer == 2 and h2 is None) else None, st),
+                       "nfx_affine_train_pack")  # (kept pre-activations: OUTK needs no eval image)
         y = torch.empty_like(x)
         ld = torch.empty(B, device=dev, dtype=torch.float32)
         if ev is not None:
