@@ -367,6 +367,11 @@ int nfx_affine_train_stats(const float* tpack, const float* in, int64_t B, int d
 int nfx_affine_train_update_running(const double* stats1, const double* stats2,
                                     float* const* running_mean, float* const* running_var, int H,
                                     double momentum, void* stream);
+/* The same, also adding 1 to the 4 BatchNorms' num_batches_tracked (int64 counters). */
+int nfx_affine_train_update_running_counted(const double* stats1, const double* stats2,
+                                            float* const* running_mean, float* const* running_var,
+                                            int64_t* const* num_batches_tracked, int H,
+                                            double momentum, void* stream);
 int nfx_affine_train_backward(const float* tpack, const float* in, const float* grad_out,
                               const float* grad_log_det, float* grad_in, int64_t B, int d, int H,
                               int direction, int stage, const double* stats2, double* G,

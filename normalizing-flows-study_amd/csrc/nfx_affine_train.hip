@@ -278,11 +278,13 @@ __global__ void affine_train_assemble_kernel(const double* G, const double* stat
 struct NfxBnPtrs {
     float* rm[4];
     float* rv[4];
+    int64_t* nbt[4];  // num_batches_tracked (null: not counted here)
 };
 __global__ void affine_train_running_kernel(const double* stats1, const double* stats2, NfxBnPtrs p, int H,
                                             int Hp, double momentum) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (net * 2 + layer) * H + row
     if (i >= 4 * H) return;
+    if (i < 4 && p.nbt[i]) p.nbt[i][0] += 1;  // the 4 BatchNorms' num_batches_tracked
     const int k = i / H, row = i % H, net = k >> 1, layer = k & 1;
     const double* q = (layer ? stats2 : stats1) + ((size_t)net * Hp + row) * 3;
     const double n = q[0];
@@ -592,12 +594,23 @@ extern "C" int nfx_affine_train_output(const float* tpack, const float* x, const
 
 extern "C" int nfx_affine_train_update_running(const double* stats1, const double* stats2, float* const* running_mean,
                                                float* const* running_var, int H, double momentum, void* stream) {
+    return nfx_affine_train_update_running_counted(stats1, stats2, running_mean, running_var, nullptr, H, momentum,
+                                                   stream);
+}
+
+// + num_batches_tracked += 1 of the 4 BatchNorms in the same launch (BatchNorm1d.forward in train
+// mode; one torch launch per layer otherwise)
+extern "C" int nfx_affine_train_update_running_counted(const double* stats1, const double* stats2,
+                                                       float* const* running_mean, float* const* running_var,
+                                                       int64_t* const* num_batches_tracked, int H, double momentum,
+                                                       void* stream) {
     if (!stats1 || !stats2 || !running_mean || !running_var || H <= 0)
         return set_error(NFX_EINVAL, "affine_train_update_running: bad arguments");
-    NfxBnPtrs p;
+    NfxBnPtrs p{};
     for (int k = 0; k < 4; ++k) {
         p.rm[k] = running_mean[k];
         p.rv[k] = running_var[k];
+        p.nbt[k] = num_batches_tracked ? num_batches_tracked[k] : nullptr;
     }
     const int Hp = 32 * ((H + 31) / 32);
     affine_train_running_kernel<<<(4 * H + 255) / 256, 256, 0, (hipStream_t)stream>>>(stats1, stats2, p, H, Hp, momentum);
@@ -608,7 +621,7 @@ extern "C" int nfx_affine_eval_stats(float* const* running_mean, float* const* r
                                      double* stats2, void* stream) {
     if (!stats1 || !stats2 || !running_mean || !running_var || H <= 0)
         return set_error(NFX_EINVAL, "affine_eval_stats: bad arguments");
-    NfxBnPtrs p;
+    NfxBnPtrs p{};
     for (int k = 0; k < 4; ++k) {
         if (!running_mean[k] || !running_var[k]) return set_error(NFX_EINVAL, "affine_eval_stats: null running stats");
         p.rm[k] = running_mean[k];

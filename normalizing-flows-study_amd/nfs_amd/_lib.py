@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "nfx_affine_train_param_floats", "nfx_affine_train_workspace_bytes", "nfx_affine_train_pack",
     "nfx_affine_train_stats", "nfx_affine_train_update_running", "nfx_affine_train_backward",
     "nfx_affine_train_assemble", "nfx_affine_eval_stats", "nfx_affine_train_keep_floats",
-    "nfx_affine_train_stats_keep", "nfx_affine_train_backward_keep", "nfx_affine_train_output",
+    "nfx_affine_train_stats_keep", "nfx_affine_train_backward_keep", "nfx_affine_train_output", "nfx_affine_train_update_running_counted",
     "nfx_spline_backward_packed_floats", "nfx_spline_backward_param_floats",
     "nfx_spline_backward_workspace_bytes", "nfx_spline_pack_backward", "nfx_spline_coupling_backward",
     "nfx_gauss_workspace_bytes", "nfx_gauss_logprob", "nfx_gauss_logprob_backward",
@@ -181,6 +181,8 @@ _SIGNATURES = {
     "nfx_affine_train_stats": (_int, [_vp, _vp, _i64, _int, _int, _int, _vp, _vp, _vp]),
     "nfx_affine_train_update_running": (_int, [_vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int,
                                                ctypes.c_double, _vp]),
+    "nfx_affine_train_update_running_counted": (_int, [_vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                                       ctypes.POINTER(_vp), _int, ctypes.c_double, _vp]),
     "nfx_affine_train_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp, _vp, _vp,
                                          _vp]),
     "nfx_affine_train_assemble": (_int, [_vp, _vp, _vp, _int, _int, _f, _vp, _vp]),

@@ -429,12 +429,19 @@ class CouplingLayer(HipFlow):
         bns = [self.s_net[1], self.s_net[4], self.b_net[1], self.b_net[4]]
         rm = (ctypes_vp * 4)(*[bn.running_mean.data_ptr() for bn in bns])
         rv = (ctypes_vp * 4)(*[bn.running_var.data_ptr() for bn in bns])
-        _lib.check(L.nfx_affine_train_update_running(p(stats[0]), p(stats[1]), rm, rv, H,
-                                                     float(bns[0].momentum), st), "nfx_affine_train_update_running")
+        counted = all(bn.num_batches_tracked is not None and bn.num_batches_tracked.dtype == torch.int64
+                      and bn.num_batches_tracked.device == dev for bn in bns)
+        nb = (ctypes_vp * 4)(*[bn.num_batches_tracked.data_ptr() for bn in bns]) if counted else None
+        _lib.check(L.nfx_affine_train_update_running_counted(p(stats[0]), p(stats[1]), rm, rv, nb, H,
+                                                             float(bns[0].momentum), st),
+                   "nfx_affine_train_update_running")
         for bn in bns:
             torch.autograd.graph.increment_version(bn.running_mean)
             torch.autograd.graph.increment_version(bn.running_var)
-        torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
+            if counted:
+                torch.autograd.graph.increment_version(bn.num_batches_tracked)
+        if not counted:
+            torch._foreach_add_([bn.num_batches_tracked for bn in bns], 1)
         tpack._nfx_keep = (keep_src, mask, epack, ws)  # sources alive while the kernels are queued
         tpack._nfx_h2 = h2
         return y, ld, tpack, stats
