@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5f|cfg5i|...]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+`--gpus N` with no launcher around it (WORLD_SIZE unset) starts the N ranks itself as child
+processes (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* on 127.0.0.1) and relays rank
+0's line; under a launcher WORLD_SIZE must equal --gpus. The line records the world size and
+every rank's device.
+
 One step = one log_prob pass over the batch: every flow layer's fused kernel (conditioner MLP
 on fp32 MFMA + transform + log-det accumulate), the fused Gaussian base term with the float64
 NLL partial sum, and (N > 1) ONE RCCL all-reduce of the 16-byte partial [sum log p, count] —
@@ -648,6 +653,13 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                    "fits_profiled_step": rj["fits_bench_step"],
                    "profiled_run_event_frac": rj["event_frac"],
                    "source": os.path.relpath(tp, ROOT), "round": rj.get("round")}
+        if rj.get("mfma_busy_frac") is not None:
+            # the MFMA-busy PMC pass (tools/reconcile_profile.py mfma_busy): share of the SIMD-cycles
+            # the matrix pipe ran, the clock, and VALU instructions per MFMA of the hot kernel;
+            # frac = busy x clock / 2.4 GHz x (algorithmic / issued MFMA flop)
+            rocprof.update({"mfma_busy_frac": rj["mfma_busy_frac"], "mfma_issue_frac": rj.get("mfma_issue_frac"),
+                            "clock_ghz": rj.get("clock_ghz"), "valu_insts_per_mfma": rj.get("valu_insts_per_mfma"),
+                            "busy_cycles_per_mfma": rj["pmc_mfma"].get("busy_cycles_per_mfma")})
     result = {
         "metric": METRIC,
         "value": B_global * a.steps / t_max,
@@ -786,7 +798,100 @@ def lib_digest():
     return h.hexdigest()[:16]
 
 
-def main():
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher around it: start N child ranks of this script (one
+    process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set as torch.distributed.run sets
+    them, rendezvous on 127.0.0.1), relay rank 0's JSON line, and return non-zero when any rank
+    fails (the others are then terminated). This process never touches the GPU: the ranks are
+    children started with fork + exec before anything here initialised HIP."""
+    import signal
+    import subprocess
+    import tempfile
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs, outs = [], []
+    libc = None
+    try:
+        import ctypes
+        libc = ctypes.CDLL("libc.so.6", use_errno=True)
+    except OSError:
+        pass
+
+    def die_with_parent():  # runs in the child between fork and exec: no GPU state exists there
+        if libc is not None:
+            libc.prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old_term = signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, NFX_BENCH_LAUNCHER="bench.py")
+            out = tempfile.TemporaryFile(mode="w+") if r == 0 else None
+            outs.append(out)
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                          stdout=out if r == 0 else sys.stderr, preexec_fn=die_with_parent))
+        rc = 0
+        live = list(range(n))
+        while live:
+            for r in list(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.remove(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py launcher: rank {r} exited with {c}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    stop_all()
+            time.sleep(0.05)
+        outs[0].seek(0)
+        text = outs[0].read()
+    finally:
+        stop_all()
+        signal.signal(signal.SIGTERM, old_term)
+    lines = [ln for ln in text.splitlines() if ln.strip()]
+    for ln in lines[:-1]:
+        print(ln, file=sys.stderr)
+    if lines:
+        try:
+            res = json.loads(lines[-1])
+            res["launcher"] = f"bench.py --gpus {n}: {n} child ranks (RANK/LOCAL_RANK/WORLD_SIZE, 127.0.0.1:{port})"
+            print(json.dumps(res), flush=True)
+        except json.JSONDecodeError:
+            print(lines[-1], flush=True)
+    elif rc == 0:
+        print("bench.py launcher: rank 0 printed nothing", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def launch_check(world, rank, local):
+    """NFX_BENCH_LAUNCH_CHECK=1: the ranks join a gloo group and report who they are, with no GPU
+    call — the CPU test of the `--gpus N` launcher (tests/test_bench_cpu.py). NFX_BENCH_FAIL_RANK=r
+    makes rank r exit 3 before joining (the launcher must then fail and stop the others)."""
+    if os.environ.get("NFX_BENCH_FAIL_RANK") == str(rank):
+        raise SystemExit(3)
+    dist.init_process_group("gloo")
+    me = {"rank": dist.get_rank(), "local_rank": local, "pid": os.getpid(), "env_rank": rank}
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, me)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world_size": dist.get_world_size(), "ranks": allr}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -806,24 +911,44 @@ def main():
     ap.add_argument("--weak", action="store_true", help="weak scaling: every rank processes the whole batch")
     ap.add_argument("--strong", action="store_true", help="(default) strong scaling: split the batch over the ranks")
     ap.add_argument("--no-secondary", action="store_true", help="cfg2: skip the nested MAF d=63 (cfg4) line")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {a.gpus})")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:
+            # no launcher around us: start the N ranks ourselves (one process per GPU)
+            raise SystemExit(launch_ranks(a.gpus, sys.argv[1:] if argv is None else list(argv)))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != a.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {a.gpus}; "
+                             f"they must agree (one rank per GPU)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("NFX_BENCH_LAUNCH_CHECK") == "1":
+        return launch_check(world, rank, local)
     # NFX_BENCH_REHEARSE=1: every rank on cuda:0 with gloo collectives — exercises the N > 1 code
     # path (sharding, barriers, max-over-ranks timing, reductions) on a one-GPU box; its numbers
     # are not a scaling measurement (the ranks share one GPU)
     rehearse = os.environ.get("NFX_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
+    elif world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: --gpus {world} but only {torch.cuda.device_count()} GPU(s) visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rank_devices = None
     if world > 1:
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        props = torch.cuda.get_device_properties(dev)
+        mine = f"rank {rank}: cuda:{local} {props.name} pci {getattr(props, 'pci_bus_id', '?')}"
+        rank_devices = [None] * dist.get_world_size()
+        dist.all_gather_object(rank_devices, mine)
     training = a.config in TRAIN_CONFIGS
     graph = a.graph if training else ((not a.eager) if a.config.startswith("sample4k") else (a.graph and not a.eager))
     strong = not a.weak
@@ -835,6 +960,9 @@ def main():
     if rank == 0:
         if rehearse:
             result["rehearsal"] = "NFX_BENCH_REHEARSE=1: all ranks shared cuda:0 over gloo (not a scaling result)"
+        result["world_size"] = dist.get_world_size() if world > 1 else 1
+        result["rank_devices"] = rank_devices or [f"rank 0: cuda:{local} {torch.cuda.get_device_name(dev)}"]
+        result["backend"] = (dist.get_backend() if world > 1 else None)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

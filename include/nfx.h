@@ -33,11 +33,12 @@
 extern "C" {
 #endif
 
-/* ABI 2: the log_prob workspace (nfx_gauss_workspace_bytes) must be zero-filled before its first
- * use (the fused epilogues' last workgroup finishes the float64 sums in the same launch and resets
- * a counter in it); nfx_made_affine_backward / nfx_made_seq_backward / nfx_made_backward_weights
+/* ABI 3: the log_prob workspace (nfx_gauss_workspace_bytes) may hold anything on entry — the
+ * fused epilogues' last workgroup finishes the float64 sums in the same launch, and its arrival
+ * word is tagged per launch, so garbage or a count left by an aborted launch is discarded (ABI 2
+ * required a zero-filled workspace); nfx_made_affine_backward / nfx_made_seq_backward / nfx_made_backward_weights
  * return NFX_EUNSUPPORTED above nfx_made_backward_max_batch(d, H) (callers split the batch). */
-#define NFX_ABI_VERSION 2
+#define NFX_ABI_VERSION 3
 
 #define NFX_OK 0
 #define NFX_EINVAL (-1)

@@ -147,10 +147,9 @@ __device__ __forceinline__ float gauss_lp(float m, float c, float ld) {
 
 // Capacity (doubles) of the partial-sum workspace shared by nfx_gauss_logprob and the fused
 // *_logprob layer epilogues; every launch that writes partials uses at most this many blocks.
-// The workspace holds kMaxPartials doubles of partials, then the arrival counter of
-// logp_commit (zero between launches: the caller zero-fills the workspace once, every launch's
-// last workgroup resets it).
-constexpr int kMaxPartials = 4096;
+// The workspace holds kMaxPartials doubles of partials, then the 64-bit arrival word of
+// logp_commit (any content on entry, below).
+constexpr int kMaxPartials = 4096;  // < 2^16: the arrival word's count field
 
 // End of a fused log_prob epilogue: each workgroup's float64 sum of its log-densities goes to
 // partials[blockIdx.x]; the LAST workgroup to arrive (agent-scope counter after the workspace's
@@ -158,18 +157,36 @@ constexpr int kMaxPartials = 4096;
 // launch. The reduction replays gauss_finish_kernel's order exactly (256 strided accumulators, a
 // shuffle-down tree per 64, the four wave sums in order), so fused and unfused results agree bit
 // for bit whatever the workgroup size NT (a multiple of 64).
+//
+// The arrival word is 64-bit: [63:16] a launch tag, [15:0] the count. The tag is this dispatch's
+// AQL packet address (a ring slot: distinct for every launch in flight on a queue, and never the
+// pattern of a fill), so a workgroup finding another tag in the word — a workspace that was never
+// zeroed, or one left mid-count by an aborted launch — starts the count afresh (CAS) instead of
+// adding to it. The caller's workspace therefore needs no zero-fill and no reset launch (round 6;
+// ABI version 3). The last workgroup still stores 0, so a stale tag can only ever be the one of a
+// launch that did not finish.
+__device__ __forceinline__ uint64_t logp_launch_tag() {
+    const uint64_t p = reinterpret_cast<uint64_t>(__builtin_amdgcn_dispatch_ptr());
+    return ((p >> 6) & 0xFFFFFFFFFFFFull) << 16;
+}
+
 template <int NT>
 __device__ __forceinline__ void logp_commit(double v, double* partials, double* sums, int64_t B) {
     static_assert(NT % 64 == 0, "whole waves");
     const double t = block_sum_f64<NT>(v);
     __shared__ int last;
     __shared__ double red4[4];
-    unsigned* cnt = reinterpret_cast<unsigned*>(partials + kMaxPartials);
+    uint64_t* cnt = reinterpret_cast<uint64_t*>(partials + kMaxPartials);
     if (threadIdx.x == 0) {
         partials[blockIdx.x] = t;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = prev == gridDim.x - 1;
+        const uint64_t tag = logp_launch_tag();
+        uint64_t old = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nw;
+        do {
+            nw = ((old & ~0xFFFFull) == tag) ? old + 1 : (tag | 1u);
+        } while (!__hip_atomic_compare_exchange_weak(cnt, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT));
+        last = (unsigned)(nw & 0xFFFFu) == gridDim.x;
     }
     __syncthreads();
     if (!last) return;
@@ -188,7 +205,7 @@ __device__ __forceinline__ void logp_commit(double v, double* partials, double* 
         for (int w = 0; w < 4; ++w) s += red4[w];
         sums[0] = s;
         sums[1] = (double)B;
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

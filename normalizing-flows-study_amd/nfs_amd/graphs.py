@@ -49,7 +49,7 @@ class GraphedFlow:
         self.mode = mode
         self.strict = strict
         self.static_in = example.detach().clone().contiguous()
-        # the graph's own log_prob workspace (float64 partials + arrival counter): replays of two
+        # the graph's own log_prob workspace (float64 partials + arrival word): replays of two
         # graphs, or a replay beside eager calls, never share one
         self.workspace = None
         if mode == "log_prob":
@@ -110,7 +110,12 @@ class GraphedTrainStep:
             raise ValueError("GraphedTrainStep needs a ROCm device tensor")
         self.model = model
         self.optimizer = optimizer
-        self.loss_fn = loss_fn or (lambda m, x: -m.log_prob(x).mean())
+        # the step's own log_prob workspace (float64 partials + arrival word), as GraphedFlow:
+        # two captured steps, or a replay beside eager calls, never share one
+        from .models.normalizing_flow_model import new_gauss_workspace
+        self.workspace = new_gauss_workspace(example.shape[0], example.device)
+        ws = self.workspace
+        self.loss_fn = loss_fn or (lambda m, x: -m.log_prob(x, workspace=ws).mean())
         self.clip = clip_grad_norm
         self.static_in = example.detach().clone().contiguous()
         params = [p for g in optimizer.param_groups for p in g["params"]]

@@ -11,6 +11,7 @@ intermediate log-det tensors and no Python-side adds.
 (csrc/nfx_gauss.hip): the log_prob glue the reference's callers write inline
 (README.md:113-114, src/utils.py:39-55, plots/_common.py:201-202).
 """
+import collections
 import math
 
 import torch
@@ -191,9 +192,9 @@ class NormalizingFlowModel(nn.Module):
 
         With return_sums=True also returns a float64 tensor [sum_i log p(x_i), B] on x's device
         (the partial a data-parallel NLL all-reduces). `workspace`: the fused epilogue's float64
-        partials + arrival counter (uint8 tensor of at least nfx_gauss_workspace_bytes(B) bytes,
-        zero-filled once); by default one cached per (device, current stream), so calls on
-        different streams never share one."""
+        partials + arrival word (uint8 tensor of at least nfx_gauss_workspace_bytes(B) bytes, any
+        content: ABI 3 tags the arrival word per launch); by default one cached per (device,
+        current stream), so calls on different streams never share one."""
         if self._hip_chain_ok(x) and len(self.flows) > 0:
             B = x.shape[0]
             logp = torch.empty(B, device=x.device, dtype=torch.float32)
@@ -225,15 +226,19 @@ class NormalizingFlowModel(nn.Module):
         return -(s[0] / s[1]).item()
 
 
-_GAUSS_WS = {}
+_GAUSS_WS = collections.OrderedDict()
+_GAUSS_WS_MAX = 8  # (device, stream) entries kept; least recently used dropped beyond
 
 
 def gauss_workspace(B, device, stream=None):
-    """The per-workgroup float64 partial sums + arrival counter of the fused log_prob epilogues
-    (nfx_gauss_workspace_bytes): zero-filled once and cached per (device, stream) — every launch's
-    last workgroup resets the counter, so the buffer stays valid call after call on its stream.
-    Launches on one stream are ordered; two streams never share a workspace (concurrent launches
-    on one would race on its counter and partials). Captured graphs (GraphedFlow) own theirs."""
+    """The per-workgroup float64 partial sums + arrival word of the fused log_prob epilogues
+    (nfx_gauss_workspace_bytes), cached per (device, stream). Any content is valid (ABI 3: the
+    kernels tag the arrival word per launch). Launches on one stream are ordered; two streams
+    never share a workspace (concurrent launches on one would race on its partials). The cache
+    holds the _GAUSS_WS_MAX most recently used streams: a transient stream's entry is dropped
+    once eight others were used after it (the caching allocator reuses a dropped buffer only on
+    the stream it was allocated on, after that stream's queued work). Captured graphs
+    (GraphedFlow, GraphedTrainStep) own theirs."""
     dev = torch.device(device)
     if dev.type == "cuda":
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -244,14 +249,17 @@ def gauss_workspace(B, device, stream=None):
     n = _lib.lib().nfx_gauss_workspace_bytes(B)
     ws = _GAUSS_WS.get(key)
     if ws is None or ws.numel() < n:
-        ws = torch.zeros(n, device=dev, dtype=torch.uint8)
+        ws = torch.empty(n, device=dev, dtype=torch.uint8)
         _GAUSS_WS[key] = ws
+    _GAUSS_WS.move_to_end(key)
+    while len(_GAUSS_WS) > _GAUSS_WS_MAX:
+        _GAUSS_WS.popitem(last=False)
     return ws
 
 
 def new_gauss_workspace(B, device):
-    """A fresh zero-filled log_prob workspace for B samples (for callers that own one)."""
-    return torch.zeros(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
+    """A fresh log_prob workspace for B samples (for callers that own one; no fill needed)."""
+    return torch.empty(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
 
 
 def check_gauss_workspace(ws, B, device):

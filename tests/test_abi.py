@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_sizes():
     L = _lib.lib()
-    assert L.nfx_abi_version() == 2
+    assert L.nfx_abi_version() == 3
     assert L.nfx_affine_packed_floats(2, 64) > 0
     assert L.nfx_affine_packed_floats(2, 64) % 4 == 0
     assert L.nfx_spline_packed_floats(2, 64, 8) % 4 == 0

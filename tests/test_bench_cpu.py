@@ -28,3 +28,38 @@ def test_lib_digest_is_stable():
 def test_reconcile_knows_config(cfg):
     import reconcile_profile
     assert cfg in reconcile_profile.HOT
+
+
+def _bench(env_extra, *args, timeout=180):
+    import subprocess
+    env = dict(os.environ, **env_extra)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        if k not in env_extra:
+            env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts 2 ranks itself and they join one
+    process group (NFX_BENCH_LAUNCH_CHECK: gloo, no GPU call); rank 0's line is relayed."""
+    import json
+    r = _bench({"NFX_BENCH_LAUNCH_CHECK": "1"}, "--gpus", "2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["launch_check"] and line["world_size"] == 2
+    assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
+    assert [x["local_rank"] for x in sorted(line["ranks"], key=lambda x: x["rank"])] == [0, 1]
+    assert len({x["pid"] for x in line["ranks"]}) == 2
+    assert "2 child ranks" in line["launcher"]
+
+
+def test_gpus_flag_rank_failure_fails_the_run():
+    r = _bench({"NFX_BENCH_LAUNCH_CHECK": "1", "NFX_BENCH_FAIL_RANK": "1"}, "--gpus", "2")
+    assert r.returncode != 0
+    assert "rank 1 exited" in r.stderr
+
+
+def test_world_size_must_match_gpus():
+    r = _bench({"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"}, "--gpus", "2")
+    assert r.returncode != 0 and "must agree" in r.stderr

@@ -133,7 +133,7 @@ def test_fused_path_taken(cuda_device, kind):
     x = torch.randn(1000, d, device=cuda_device)
     with torch.no_grad():
         logp, sums = torch.empty(1000, device=cuda_device), torch.empty(2, device=cuda_device, dtype=torch.float64)
-        ws = torch.zeros(1 << 16, device=cuda_device, dtype=torch.uint8)  # (zero-filled: logp_commit's counter)
+        ws = torch.empty(1 << 16, device=cuda_device, dtype=torch.uint8)  # (any content, ABI 3)
         chain = getattr(m, "flow", m)  # RealNVP wraps a NormalizingFlowModel
         _, _, fused = chain._hip_chain(x, -1, logprob=(logp, sums, ws))
     assert fused == fused_expected
@@ -249,8 +249,8 @@ def test_concurrent_streams_own_workspaces(cuda_device, kind):
 
 
 def test_log_prob_caller_workspace(cuda_device):
-    """log_prob(x, workspace=...) runs on a caller-owned zero-filled workspace (and rejects one
-    that is too small)."""
+    """log_prob(x, workspace=...) runs on a caller-owned workspace (and rejects one that is too
+    small)."""
     from nfs_amd.models.normalizing_flow_model import new_gauss_workspace
     m, d, _ = _model("spline_k5")
     m = m.to(cuda_device).eval()
@@ -319,3 +319,39 @@ def test_last_kernel_names_dispatch(cuda_device):
         iaf = nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)]).to(cuda_device).eval()
         iaf.log_prob(torch.randn(1024, 784, device=cuda_device))
         assert _lib.last_kernel() == "made_seqp_kernel"
+
+
+@pytest.mark.parametrize("kind", KINDS + ["iaf784_push", "iaf784_seqs"])
+def test_garbage_workspace_gives_serial_sums(cuda_device, kind):
+    """ABI 3: the log_prob workspace needs no zero-fill. A workspace filled with 0xFF, or one
+    whose arrival word holds a count left mid-launch (as an aborted launch would leave it), gives
+    the serial [sum log p, B] and logp bit for bit, call after call, for every fused epilogue and
+    the separate Gaussian pass."""
+    from nfs_amd.models.normalizing_flow_model import new_gauss_workspace
+    if kind.startswith("iaf784"):
+        torch.manual_seed(9)
+        m = _perturb(nfs_amd.NormalizingFlowModel([nfs_amd.InverseAutoregressiveFlow(784, 64)]), 0.01, 9)
+        d = 784
+        B = 1024 if kind == "iaf784_push" else 8192
+    else:
+        m, d, _ = _model(kind)
+        B = 4099 if kind.startswith("iaf") else 70_001
+    m = m.to(cuda_device).eval()
+    x = torch.randn(B, d, generator=torch.Generator().manual_seed(3)).to(cuda_device)
+    ws0 = new_gauss_workspace(B, cuda_device)
+    ws0.zero_()
+    with torch.no_grad():
+        lp, s = m.log_prob(x, return_sums=True, workspace=ws0)
+        wsf = new_gauss_workspace(B, cuda_device)
+        for fill in ("ff", "midcount", "ff"):
+            if fill == "ff":
+                wsf.fill_(0xFF)
+            else:  # arrival word (after the 4096 float64 partials): another launch's tag, count 3
+                wsf.zero_()
+                w = wsf.view(torch.int64)
+                w[4096] = (0x123456789 << 16) | 3
+            for _ in range(2):
+                lp2, s2 = m.log_prob(x, return_sums=True, workspace=wsf)
+                torch.cuda.synchronize()
+                assert torch.equal(s2, s), (fill, s2.tolist(), s.tolist())
+                assert torch.equal(lp2, lp)

@@ -2,8 +2,9 @@
 # rocprofv3 around bench.py ITSELF (no launcher hop), one config per run, so the kernel trace and
 # the bench line's ms_per_step come from one process and one clock (run on the GPU box via gpurun):
 #   bash tools/profile_bench.sh <tag> [--pmc] <cfg>[:<batch>][+graph] ...
-# Writes gpurun_out/prof_<tag>/<cfg>[_<batch>]/{trace/,bench.json,fetch/,write/}. The PMC passes
-# (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) are separate runs with --kernel-trace only.
+# Writes gpurun_out/prof_<tag>/<cfg>[_<batch>]/{trace/,bench.json,fetch/,write/,mfma/}. The PMC passes
+# (FETCH_SIZE, WRITE_SIZE: they do not fit one pass; the MFMA-busy / instruction-mix / clock pass)
+# are separate runs with --kernel-trace only.
 # Reconcile afterwards on the CPU: python tools/reconcile_profile.py gpurun_out/prof_<tag> <round tag>
 set -o pipefail
 tag="$1"; shift
@@ -36,6 +37,11 @@ for spec0 in "$@"; do
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$d/write" -- \
       python3 "$root/bench.py" --config "$c" "${extra[@]}" --steps 3 --warmup 1 --no-cpu --no-secondary \
       > "$d/write.log" 2>&1 || exit $?
+    # MFMA pipe busy cycles, instruction mix and the clock (GRBM_GUI_ACTIVE over the 8 XCDs)
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE \
+      --output-format csv -d "$d/mfma" -- \
+      python3 "$root/bench.py" --config "$c" "${extra[@]}" --steps 3 --warmup 1 --no-cpu --no-secondary \
+      > "$d/mfma.log" 2>&1 || exit $?
   fi
   echo "profiled $name"
 done

@@ -76,6 +76,62 @@ def _counter(path, counter):
     return out
 
 
+N_SIMD = 256 * 4         # MI355X: 256 CUs x 4 SIMDs
+MFMA_F32_CYCLES = 64     # v_mfma_f32_32x32x2_f32: 4,096 flop at 64 flop/clk/SIMD
+PEAK_CLOCK_GHZ = 2.4     # the clock the 157.3 TFLOP/s peak is quoted at
+
+
+def mfma_busy(counter_csv, trace_csv, hot):
+    """The MFMA-busy pass: per dispatch of the hot kernel, SQ_VALU_MFMA_BUSY_CYCLES (cycles the
+    matrix pipe was busy, summed over every SIMD), SQ_INSTS_MFMA / SQ_INSTS_VALU (wave
+    instructions) and GRBM_GUI_ACTIVE (GPU-active cycles summed over the 8 XCDs). With the
+    dispatch's duration (its kernel trace) they give
+      clock_ghz      = GRBM_GUI_ACTIVE / 8 / duration           (MI355X_MICROARCH.md 'DVFS give-back')
+      mfma_busy_frac = BUSY / (1,024 SIMDs x GRBM_GUI_ACTIVE / 8) (share of the SIMD-cycles the pipe ran)
+    and the identity frac = mfma_busy_frac x clock / 2.4 GHz x (algorithmic / issued MFMA flop):
+    the roofline frac is below the busy fraction by the clock and by any MFMA work beyond the
+    algorithmic count, and the rest of the SIMD-cycles are VALU / waiting."""
+    per = {}
+    with open(counter_csv) as fh:
+        for r in csv.DictReader(fh):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            if k not in hot:
+                continue
+            key = (k, r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            per.setdefault(key, {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    dur = {}
+    if trace_csv:
+        with open(trace_csv) as fh:
+            for r in csv.DictReader(fh):
+                k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                if k in hot:
+                    dur[(k, r.get("Dispatch_Id") or r.get("Correlation_Id"))] = (
+                        int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    rows = [(v, dur.get(key)) for key, v in per.items()
+            if all(c in v for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"))]
+    if not rows:
+        return {}
+    n = len(rows)
+    busy = sum(v["SQ_VALU_MFMA_BUSY_CYCLES"] for v, _ in rows) / n
+    imfma = sum(v["SQ_INSTS_MFMA"] for v, _ in rows) / n
+    ivalu = sum(v["SQ_INSTS_VALU"] for v, _ in rows) / n
+    grbm = sum(v["GRBM_GUI_ACTIVE"] for v, _ in rows) / n
+    cyc = grbm / 8
+    out = {"pmc_mfma": {"dispatches": n, "SQ_VALU_MFMA_BUSY_CYCLES": busy, "SQ_INSTS_MFMA": imfma,
+                        "SQ_INSTS_VALU": ivalu, "GRBM_GUI_ACTIVE": grbm,
+                        "busy_cycles_per_mfma": busy / imfma if imfma else None,
+                        "source": os.path.relpath(counter_csv, ROOT)},
+           "mfma_busy_frac": busy / (N_SIMD * cyc) if cyc else None,
+           "mfma_issue_frac": imfma * MFMA_F32_CYCLES / (N_SIMD * cyc) if cyc else None,
+           "valu_insts_per_mfma": ivalu / imfma if imfma else None}
+    ds = [d for _, d in rows if d]
+    if ds:
+        mean_ns = sum(ds) / len(ds)
+        out["clock_ghz"] = cyc / mean_ns
+        out["pmc_mfma"]["mean_duration_us"] = mean_ns / 1e3
+    return out
+
+
 def reconcile(cdir, rtag):
     name = os.path.basename(cdir.rstrip("/"))
     cfg = "_".join(p for p in name.split("_") if not p.isdigit())  # cfg2_125000 -> cfg2
@@ -160,6 +216,10 @@ def reconcile(cdir, rtag):
             res["pmc_dispatches"] = len(fs)
             res["pmc_note"] = ("FETCH_SIZE (KB) doubled per MI355X_MICROARCH.md (gfx950 reports half of a wide "
                                "streaming read), WRITE_SIZE as reported; mean over the hot kernel's dispatches")
+    mf = _newest(os.path.join(cdir, "mfma", "*", "*counter_collection.csv"))
+    mt = _newest(os.path.join(cdir, "mfma", "*", "*kernel_trace.csv"))
+    if mf:
+        res.update(mfma_busy(mf, mt, hot))
     out = os.path.join(ROOT, "profiles", f"{rtag}_{name}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
