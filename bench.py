@@ -179,12 +179,11 @@ def build(config):
         H = 64
         # dominant kernel = BWD2 of the train-mode backward, per net: (diag(r2) W2)^T e2 and
         # dW2 = sum e2 a1^T (2 x 2H^2) + layer 1 (2H) + W3^T delta3 (2H), the layer-2
-        # pre-activations read from the copy the statistics pass kept (NFX_TRAIN_KEEP=0: the
-        # round-4 kernel also recomputes layer 2 and the output layer, 3 x 2H^2 + 2H + 2 x 2H)
-        if os.environ.get("NFX_TRAIN_KEEP", "1") != "0":
-            f = 2 * (2 * 2 * H * H + 2 * H + 2 * H)
-        else:
-            f = 2 * (3 * 2 * H * H + 2 * H + 2 * 2 * H)
+        # pre-activations read from the copy the statistics pass kept (run_config re-prices it
+        # from coupling.KEEP_STATS when a layer recomputed instead: NFX_TRAIN_KEEP=0 or over the
+        # keep budget, where the kernel also recomputes layer 2 and the output layer,
+        # 3 x 2H^2 + 2H + 2 x 2H)
+        f = 2 * (2 * 2 * H * H + 2 * H + 2 * H)
         import oracle
         what = ("cfg2t RealNVP(2,8,64) training step (train-mode BatchNorm: batch statistics + "
                 "running-stat update, -log_prob mean, fused backward, Adam)") if config == "cfg2t" else \
@@ -405,6 +404,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
     model, d, f_layer, spec, desc = build(config)
     training = config in TRAIN_CONFIGS
     coupling_train = config in ("cfg2t", "train5k", "trainfig")
+    from nfs_amd.flows import coupling as _cpk
+    _cpk.KEEP_STATS.update(kept=0, recompute=0)
     clip = 5.0 if (config == "trainfig" or config in FIG_TRAIN) else None
     lr = 1e-3 if config == "trainfig" else (FIG_TRAIN[config][1] if config in FIG_TRAIN else 1e-5)
     sampling = config == "cfg5f" or config.startswith("sample4k")
@@ -582,6 +583,16 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         dist.all_reduce(t_all, op=dist.ReduceOp.MAX)
     t_max = float(t_all.item())
 
+    keep_note = None
+    if config in ("cfg2t", "train5k"):
+        # price BWD2 by what the forwards actually did: kept pre-activations, or the
+        # recompute kernel (NFX_TRAIN_KEEP=0 / a copy over the keep budget)
+        H = 64
+        kept, rec = _cpk.KEEP_STATS["kept"], _cpk.KEEP_STATS["recompute"]
+        f_keep, f_rec = 2 * (2 * 2 * H * H + 2 * H + 2 * H), 2 * (3 * 2 * H * H + 2 * H + 2 * 2 * H)
+        if kept + rec:
+            f_layer = (kept * f_keep + rec * f_rec) / (kept + rec)
+        keep_note = {"layers_kept": kept, "layers_recomputed": rec}
     # dominant kernel: the per-layer fused kernel (every launch of the timed steps), named by the
     # library as dispatched (nfx_last_kernel)
     durs = [e0.elapsed_time(e1) for _, e0, e1 in events]
@@ -683,7 +694,9 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         "nll_f64": nll,
         "reference_check": ref_check,
         "timed_window_monotonic_ns": [w0, w1],
-        "roofline": {"bound": "mfma", "pipe": "valu" if config == "cfg5i" else "mfma",
+        # cfg5i's sequential kernel issues no MFMA (its dot products are VALU FMAs): bound = the
+        # fp32 VALU rate, whose peak (packed FMA) equals the fp32 MFMA peak, 157.3 TFLOP/s
+        "roofline": {"bound": "valu" if config == "cfg5i" else "mfma", "pipe": "valu" if config == "cfg5i" else "mfma",
                      "kernel": kname, "achieved": achieved,
                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
                      "traffic": traffic, "flop_per_sample_per_launch": f_launch,
@@ -729,6 +742,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
             result["data"] = ("the reference's own initial weights and 2,000 standardized two-moons points "
                               "(tests/golden/g15_fig_train.npz, written by importing the reference)")
         result["nll_f64"] = None
+        if keep_note is not None:
+            result["roofline"]["pre_activations"] = keep_note
         result["roofline"]["note"] = ("dominant kernel = BWD2 of the train-mode coupling backward "
                                       "(W2^T e2 and the sample-contraction dW2 on MFMA, one net per "
                                       "workgroup); a layer runs STATS1, STATS2 (keeps the layer-2 "

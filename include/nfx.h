@@ -411,12 +411,16 @@ int nfx_affine_eval_stats(float* const* running_mean, float* const* running_var,
  *   logp[i] = -0.5 * (fp32(d*log(2*pi)) + sum_j z[i,j]^2) + log_det[i]
  * (torch.distributions.MultivariateNormal(0, I).log_prob(z) + log_det).
  * sums[0] = sum_i logp[i] in float64, sums[1] = B (as double). `workspace` must hold
- * nfx_gauss_workspace_bytes(B) bytes, ZERO-FILLED before its first use: every call that writes
- * sums (this one and the fused *_logprob epilogues) reduces the per-workgroup partials in its last
- * workgroup and leaves the workspace's arrival counter at zero again, so one workspace serves any
- * number of stream-ordered calls (not two concurrent ones). logp may be NULL (NLL-only).
+ * nfx_gauss_workspace_bytes(B) bytes, of ANY content (ABI 3): every call that writes sums (this
+ * one and the fused *_logprob epilogues) reduces the per-workgroup partials in its last workgroup;
+ * the workspace's tagged arrival word is validated by the kernel itself (a foreign value is
+ * replaced, not added to) and left clean, so one workspace serves any number of stream-ordered
+ * calls (not two concurrent ones). nfx_gauss_workspace_init (optional, stream-ordered, graph-
+ * capturable) writes the clean word up front; without it the first call on an uninitialised
+ * workspace spends one compare-and-swap round per early workgroup. logp may be NULL (NLL-only).
  * ------------------------------------------------------------------------------------- */
 size_t nfx_gauss_workspace_bytes(int64_t B);
+int nfx_gauss_workspace_init(void* workspace, void* stream);
 int nfx_gauss_logprob(const float* z, const float* log_det, float* logp, double* sums,
                       void* workspace, int64_t B, int d, void* stream);
 /* Its adjoint (training: loss = -mean log p): grad_z[i, j] = -z[i, j] * grad_logp[i],

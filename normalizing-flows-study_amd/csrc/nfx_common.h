@@ -158,17 +158,18 @@ constexpr int kMaxPartials = 4096;  // < 2^16: the arrival word's count field
 // shuffle-down tree per 64, the four wave sums in order), so fused and unfused results agree bit
 // for bit whatever the workgroup size NT (a multiple of 64).
 //
-// The arrival word is 64-bit: [63:16] a launch tag, [15:0] the count. The tag is this dispatch's
-// AQL packet address (a ring slot: distinct for every launch in flight on a queue, and never the
-// pattern of a fill), so a workgroup finding another tag in the word — a workspace that was never
-// zeroed, or one left mid-count by an aborted launch — starts the count afresh (CAS) instead of
-// adding to it. The caller's workspace therefore needs no zero-fill and no reset launch (round 6;
-// ABI version 3). The last workgroup still stores 0, so a stale tag can only ever be the one of a
-// launch that did not finish.
-__device__ __forceinline__ uint64_t logp_launch_tag() {
-    const uint64_t p = reinterpret_cast<uint64_t>(__builtin_amdgcn_dispatch_ptr());
-    return ((p >> 6) & 0xFFFFFFFFFFFFull) << 16;
-}
+// The arrival word is 64-bit: [63:16] a tag, [15:0] the count (round 6; ABI version 3). A clean
+// word holds the fixed tag kLogpClean with count 0, and every launch's last workgroup stores that
+// back. A workgroup adds 1 to the word (one atomic, as the ABI-2 counter did) and, when the value
+// it got back carries the clean tag, its count IS the arrival index. Anything else in the word — a
+// workspace that was never initialised (torch.empty, 0xFF fills, a reused allocation holding
+// other data, or all zeros) — is overwritten by ONE compare-and-swap to "clean tag, count 1" by
+// the first workgroup to find it; workgroups that met the foreign value meanwhile retry on the
+// clean word, so the count stays exact. Only that first launch on a fresh workspace pays the
+// swaps (nfx_gauss_workspace_init writes the clean word instead). A foreign word matches the tag
+// with probability 2^-48. (A count left mid-launch cannot be met: a launch that does not finish
+// faults the device and ends the process.)
+constexpr uint64_t kLogpClean = 0x4E46584C5047ull << 16;  // "NFXLPG", count 0
 
 template <int NT>
 __device__ __forceinline__ void logp_commit(double v, double* partials, double* sums, int64_t B) {
@@ -180,13 +181,18 @@ __device__ __forceinline__ void logp_commit(double v, double* partials, double* 
     if (threadIdx.x == 0) {
         partials[blockIdx.x] = t;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const uint64_t tag = logp_launch_tag();
-        uint64_t old = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nw;
-        do {
-            nw = ((old & ~0xFFFFull) == tag) ? old + 1 : (tag | 1u);
-        } while (!__hip_atomic_compare_exchange_weak(cnt, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT));
-        last = (unsigned)(nw & 0xFFFFu) == gridDim.x;
+        uint64_t prev = __hip_atomic_fetch_add(cnt, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((prev & ~0xFFFFull) != kLogpClean) {
+            // foreign word (rare): my add did not count. Claim the word, or add to the clean one
+            uint64_t cur = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((cur & ~0xFFFFull) == kLogpClean) {
+                prev = __hip_atomic_fetch_add(cnt, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (__hip_atomic_compare_exchange_strong(cnt, &cur, kLogpClean | 1u, __ATOMIC_RELAXED,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                prev = kLogpClean;
+            }
+        }
+        last = (unsigned)(prev & 0xFFFFu) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
@@ -205,7 +211,7 @@ __device__ __forceinline__ void logp_commit(double v, double* partials, double* 
         for (int w = 0; w < 4; ++w) s += red4[w];
         sums[0] = s;
         sums[1] = (double)B;
-        __hip_atomic_store(cnt, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt, kLogpClean, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -130,6 +130,18 @@ extern "C" int nfx_gauss_logprob_backward(const float* z, const float* grad_logp
     return check_launch("gauss_logprob_bwd_kernel");
 }
 
+namespace nfx {
+__global__ void gauss_workspace_init_kernel(double* partials) {
+    *reinterpret_cast<uint64_t*>(partials + kMaxPartials) = kLogpClean;
+}
+}  // namespace nfx
+
+extern "C" int nfx_gauss_workspace_init(void* workspace, void* stream) {
+    if (!workspace) return set_error(NFX_EINVAL, "gauss_workspace_init: null workspace");
+    gauss_workspace_init_kernel<<<1, 1, 0, (hipStream_t)stream>>>(reinterpret_cast<double*>(workspace));
+    return check_launch("gauss_workspace_init_kernel");
+}
+
 extern "C" size_t nfx_gauss_workspace_bytes(int64_t B) {
     (void)B;
     return (size_t)(kMaxPartials + 1) * sizeof(double);  // partials + logp_commit's arrival counter

@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "nfx_affine_train_stats_keep", "nfx_affine_train_backward_keep", "nfx_affine_train_output", "nfx_affine_train_update_running_counted",
     "nfx_spline_backward_packed_floats", "nfx_spline_backward_param_floats",
     "nfx_spline_backward_workspace_bytes", "nfx_spline_pack_backward", "nfx_spline_coupling_backward",
-    "nfx_gauss_workspace_bytes", "nfx_gauss_logprob", "nfx_gauss_logprob_backward",
+    "nfx_gauss_workspace_bytes", "nfx_gauss_workspace_init", "nfx_gauss_logprob", "nfx_gauss_logprob_backward",
     "nfx_flowbn_workspace_bytes", "nfx_flowbn_apply", "nfx_flowbn_moments", "nfx_flowbn_update_running",
     "nfx_flowbn_backward",
     "nfx_linear_forward", "nfx_linear_backward_data", "nfx_linear_workspace_bytes", "nfx_linear_backward_weight",
@@ -199,6 +199,7 @@ _SIGNATURES = {
     "nfx_spline_coupling_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int, _int, _int,
                                             _f, _f, _f, _f, _int, _vp]),
     "nfx_gauss_workspace_bytes": (_sz, [_i64]),
+    "nfx_gauss_workspace_init": (_int, [_vp, _vp]),
     "nfx_gauss_logprob": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _int, _vp]),
     "nfx_gauss_logprob_backward": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _vp]),
     "nfx_flowbn_workspace_bytes": (_sz, [_i64, _int]),

@@ -21,6 +21,8 @@ all data-parallel ranks (SyncBN).
 import ctypes
 import os
 
+import weakref
+
 import torch
 import torch.nn as nn
 
@@ -99,15 +101,34 @@ def _pad_d(d):
 
 
 _KEEP_BUDGET = {}
+_KEPT_LIVE = {}  # device index -> bytes of kept pre-activations alive (every layer, every model)
+# How the train-mode forwards ran since the last reset: layers that kept their pre-activations
+# and layers whose backward recomputes them (bench.py prices the backward's flops from this).
+KEEP_STATS = {"kept": 0, "recompute": 0}
 
 
 def _keep_budget(dev):
-    """Bytes one train-mode layer may keep for its backward: 1/32 of the device's memory (the
-    activations of every layer of a model stay alive until its backward)."""
+    """Bytes ONE train-mode layer may keep for its backward: 1/32 of the device's memory."""
     i = dev.index if dev.index is not None else torch.cuda.current_device()
     if i not in _KEEP_BUDGET:
         _KEEP_BUDGET[i] = torch.cuda.get_device_properties(i).total_memory // 32
     return _KEEP_BUDGET[i]
+
+
+def _keep_reserve(dev, nbytes):
+    """Admit one more kept copy: within the per-layer cap and with the copies still alive on the
+    device (all layers and models together, until their backward frees them) within 1/8 of its
+    memory. Returns the device index to release against, or None (the backward recomputes)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    live = _KEPT_LIVE.get(i, 0)
+    if nbytes > _keep_budget(dev) or live + nbytes > 4 * _keep_budget(dev):
+        return None
+    _KEPT_LIVE[i] = live + nbytes
+    return i
+
+
+def _keep_release(i, nbytes):
+    _KEPT_LIVE[i] = _KEPT_LIVE.get(i, 0) - nbytes
 
 
 class _CouplingTrainFunction(torch.autograd.Function):
@@ -121,13 +142,17 @@ class _CouplingTrainFunction(torch.autograd.Function):
         ctx.direction = direction
         ctx.tpack = tpack
         ctx.stats = stats
-        ctx.save_for_backward(x)
+        # the kept layer-2 pre-activations go through save_for_backward (not an attribute of the
+        # pack): autograd frees them when this node's backward has run
+        h2 = getattr(tpack, "_nfx_h2", None)
+        tpack._nfx_h2 = None
+        ctx.save_for_backward(x, h2)
         return y, ld
 
     @staticmethod
     def backward(ctx, gy, gld):
-        (x,) = ctx.saved_tensors
-        gx, grads = ctx.layer._train_backward(x, gy, gld, ctx.direction, ctx.tpack, ctx.stats)
+        x, h2 = ctx.saved_tensors
+        gx, grads = ctx.layer._train_backward(x, gy, gld, ctx.direction, ctx.tpack, ctx.stats, h2=h2)
         STATS["hip"] += 1
         params = list(ctx.layer.parameters())
         gparams = [g if p.requires_grad else None for p, g in zip(params, grads)]
@@ -387,9 +412,14 @@ class CouplingLayer(HipFlow):
         ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
         keep = keep and os.environ.get("NFX_TRAIN_KEEP", "1") != "0"  # 0: the backward recomputes
         nkeep = L.nfx_affine_train_keep_floats(B, d, H) if keep else 0
-        if nkeep and 4 * nkeep > _keep_budget(dev):
-            nkeep = 0  # a layer's kept copy is capped at 1/32 of HBM (9 GB, 17.6M samples at H = 64)
-        h2 = torch.empty(nkeep, device=dev, dtype=torch.float32) if nkeep else None
+        # a layer's kept copy is capped at 1/32 of HBM (9 GB, 17.6M samples at H = 64), the live
+        # copies of all layers at 1/8; beyond that the backward recomputes layers 1-2
+        rel = _keep_reserve(dev, 4 * nkeep) if nkeep else None
+        h2 = None
+        if rel is not None:
+            h2 = torch.empty(nkeep, device=dev, dtype=torch.float32)
+            weakref.finalize(h2, _keep_release, rel, 4 * nkeep)
+        KEEP_STATS["kept" if h2 is not None else "recompute"] += 1
         ev = TRAIN_EVENTS
         p = _lib.ptr
         _lib.check(L.nfx_affine_train_pack(s_raw, b_raw, p(mask), None, None, d, H, p(tpack), None, st),
@@ -485,7 +515,7 @@ class CouplingLayer(HipFlow):
         tpack, stats = self._packed(x.device, self._build_eval_backward_pack, slot="_nfx_evalbwd_pack_cache")
         return self._train_backward(x, gy, gld, direction, tpack, stats, sync=False)
 
-    def _train_backward(self, x, gy, gld, direction, tpack, stats, sync=True):
+    def _train_backward(self, x, gy, gld, direction, tpack, stats, sync=True, h2=None):
         """dL/dx and the parameter gradients (parameters() order) of one train-mode call
         (sync=False: eval mode, the BatchNorm sums are plain parameter-gradient partials)."""
         L = _lib.lib()
@@ -503,7 +533,8 @@ class CouplingLayer(HipFlow):
         ws = torch.empty(L.nfx_affine_train_workspace_bytes(B, d, H), device=dev, dtype=torch.uint8)
         Hp, D = 32 * ((H + 31) // 32), _pad_d(d)
         s_blocks = {1: G[0:4 * Hp], 2: G[4 * Hp + 2 * (D * Hp + D):][:4 * Hp]}
-        h2 = getattr(tpack, "_nfx_h2", None)  # kept by a train-mode forward (else: recompute)
+        if h2 is None:  # kept by a train-mode forward (else: recompute)
+            h2 = getattr(tpack, "_nfx_h2", None)
         p = _lib.ptr
         ev = TRAIN_EVENTS
         for stage in (1, 2, 3):

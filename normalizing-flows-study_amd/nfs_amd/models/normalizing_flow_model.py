@@ -249,7 +249,7 @@ def gauss_workspace(B, device, stream=None):
     n = _lib.lib().nfx_gauss_workspace_bytes(B)
     ws = _GAUSS_WS.get(key)
     if ws is None or ws.numel() < n:
-        ws = torch.empty(n, device=dev, dtype=torch.uint8)
+        ws = new_gauss_workspace(B, dev)
         _GAUSS_WS[key] = ws
     _GAUSS_WS.move_to_end(key)
     while len(_GAUSS_WS) > _GAUSS_WS_MAX:
@@ -258,8 +258,13 @@ def gauss_workspace(B, device, stream=None):
 
 
 def new_gauss_workspace(B, device):
-    """A fresh log_prob workspace for B samples (for callers that own one; no fill needed)."""
-    return torch.empty(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
+    """A fresh log_prob workspace for B samples (for callers that own one). Any content is valid
+    (ABI 3); nfx_gauss_workspace_init writes the clean arrival word up front (on the current
+    stream), so even the first call skips the kernels' one-time claim of a foreign word."""
+    ws = torch.empty(_lib.lib().nfx_gauss_workspace_bytes(B), device=device, dtype=torch.uint8)
+    if ws.device.type == "cuda":
+        _lib.check(_lib.lib().nfx_gauss_workspace_init(_lib.ptr(ws), _lib.stream_of(ws)), "nfx_gauss_workspace_init")
+    return ws
 
 
 def check_gauss_workspace(ws, B, device):

@@ -323,10 +323,9 @@ def test_last_kernel_names_dispatch(cuda_device):
 
 @pytest.mark.parametrize("kind", KINDS + ["iaf784_push", "iaf784_seqs"])
 def test_garbage_workspace_gives_serial_sums(cuda_device, kind):
-    """ABI 3: the log_prob workspace needs no zero-fill. A workspace filled with 0xFF, or one
-    whose arrival word holds a count left mid-launch (as an aborted launch would leave it), gives
-    the serial [sum log p, B] and logp bit for bit, call after call, for every fused epilogue and
-    the separate Gaussian pass."""
+    """ABI 3: the log_prob workspace needs no zero-fill. A workspace filled with 0xFF, zeros, or
+    an arrival word holding another tag with a count, gives the serial [sum log p, B] and logp bit
+    for bit, call after call, for every fused epilogue and the separate Gaussian pass."""
     from nfs_amd.models.normalizing_flow_model import new_gauss_workspace
     if kind.startswith("iaf784"):
         torch.manual_seed(9)
@@ -343,9 +342,11 @@ def test_garbage_workspace_gives_serial_sums(cuda_device, kind):
     with torch.no_grad():
         lp, s = m.log_prob(x, return_sums=True, workspace=ws0)
         wsf = new_gauss_workspace(B, cuda_device)
-        for fill in ("ff", "midcount", "ff"):
+        for fill in ("ff", "midcount", "zero", "ff"):
             if fill == "ff":
                 wsf.fill_(0xFF)
+            elif fill == "zero":  # the ABI-2 convention: a foreign word for ABI 3, claimed once
+                wsf.zero_()
             else:  # arrival word (after the 4096 float64 partials): another launch's tag, count 3
                 wsf.zero_()
                 w = wsf.view(torch.int64)
