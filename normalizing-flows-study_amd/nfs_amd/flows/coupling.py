@@ -144,8 +144,9 @@ class _CouplingTrainFunction(torch.autograd.Function):
         ctx.stats = stats
         # the kept layer-2 pre-activations go through save_for_backward (not an attribute of the
         # pack): autograd frees them when this node's backward has run
-        h2 = getattr(tpack, "_nfx_h2", None)
-        tpack._nfx_h2 = None
+        h2 = getattr(tpack, "_nfx_h2", None)  # (the any-shape path's tpack is a plain list)
+        if h2 is not None:
+            tpack._nfx_h2 = None
         ctx.save_for_backward(x, h2)
         return y, ld
 
