@@ -155,11 +155,20 @@ template <int K, int S, int VAR>
 __device__ __forceinline__ bool seqp_chunk(SeqpState<S>& st, const SeqpCtx& c, SeqpDesc& e) {
     constexpr int KE = K + 1 < S ? K + 1 : S - 1;  // the completion sum's last slot
     constexpr int KL = K + 2 < S ? K + 2 : S - 1;  // the prefetched W1 row's last slot
+#ifdef NFX_SEQP_NEAR
+    // timing ablation only (wrong results): the chain wave's share of a two-wave split — pushes
+    // into slots K .. K + 2, the layer-1 sum over slots K - 1 .. K + 1
+    constexpr int SP = K + 3 < S ? K + 3 : S;
+    constexpr int S0 = K > 0 ? K - 1 : 0;
+#else
+    constexpr int SP = S;
+    constexpr int S0 = 0;
+#endif
     // 1. the last completion's h3 into every later step (needs nothing from the entry)
 #pragma unroll
-    for (int j = (K > 0 ? K - 1 : 0) / 2; j < (S + 1) / 2; ++j) seqp_use(st.W4q[j]);
+    for (int j = (K > 0 ? K - 1 : 0) / 2; j < (SP + 1) / 2; ++j) seqp_use(st.W4q[j]);
 #pragma unroll
-    for (int s = K; s < S; ++s) {
+    for (int s = K; s < SP; ++s) {
         const f32x4 w = st.W4q[s / 2];
         st.A[s] = pk_fma((s & 1) ? f32x2{w[2], w[3]} : f32x2{w[0], w[1]}, st.h3g, st.A[s]);
         seqp_pin(st.A[s]);
@@ -172,7 +181,7 @@ __device__ __forceinline__ bool seqp_chunk(SeqpState<S>& st, const SeqpCtx& c, S
     const uint64_t M2 = ((1ull << ((fl >> 16) & 63)) - 1ull);
     // 2. unit g's column in flight until the next chunk pushes it
 #pragma unroll
-    for (int j = K / 2; j < (S + 1) / 2; ++j) st.W4q[j] = seqp_ld4(c, 16 * c.lane + 1024 * j, (int)e[5]);
+    for (int j = K / 2; j < (SP + 1) / 2; ++j) st.W4q[j] = seqp_ld4(c, 16 * c.lane + 1024 * j, (int)e[5]);
     // 3. the chunk's steps
     const float v = seqp_affine<VAR>(st.A[K], st.X[K], M, st.Z[K], st.Al[K]);
     float v2 = 0.f;
@@ -184,9 +193,9 @@ __device__ __forceinline__ bool seqp_chunk(SeqpState<S>& st, const SeqpCtx& c, S
     {
         float t = seqp_sel(1ull, __uint_as_float(e[8]), 0.f);
 #pragma unroll
-        for (int j = 0; j <= KL / 4; ++j) seqp_use(st.W1q[j]);
+        for (int j = S0 / 4; j <= KL / 4; ++j) seqp_use(st.W1q[j]);
 #pragma unroll
-        for (int s = 0; s <= KE; ++s) t = fmaf(st.W1q[s / 4][s % 4], st.Z[s], t);
+        for (int s = S0; s <= KE; ++s) t = fmaf(st.W1q[s / 4][s % 4], st.Z[s], t);
         const float wd2 = __uint_as_float(e[9]), wd3 = __uint_as_float(e[14]);
         const float P2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(st.acc23[0]), g));
         const float P3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(st.acc23[1]), g));
@@ -203,7 +212,7 @@ __device__ __forceinline__ bool seqp_chunk(SeqpState<S>& st, const SeqpCtx& c, S
     }
     // 5. the rows of unit u, in flight until the next chunk completes it
 #pragma unroll
-    for (int j = 0; j <= KL / 4; ++j) st.W1q[j] = seqp_ld4(c, 16 * c.lane + 1024 * j, (int)e[6]);
+    for (int j = S0 / 4; j <= KL / 4; ++j) st.W1q[j] = seqp_ld4(c, 16 * c.lane + 1024 * j, (int)e[6]);
     st.w23 = seqp_ld2(c, 8 * c.lane, (int)e[7]);
     // 6. a non-finite step kills the chunk's later steps; NaN through the next push poisons every
     // later one (cold)

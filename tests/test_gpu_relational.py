@@ -9,15 +9,20 @@ Mirrors:
 * test_autoregressive_mask_correctness.py — the Jacobian is triangular; here checked on the
   kernels themselves, bit for bit: perturbing input j leaves every output i < j unchanged.
 * test_distribution_preservation.py — 200 Adam steps on N(0, I) data on the HIP path (train-mode
-  coupling kernels + fused backward, fused MAF backward), test NLL < 3.0, sample mean/covariance
-  within the reference's bounds (median over three seeds: the outcome is chaotic).
+  coupling kernels + fused backward, fused MAF backward), test NLL < 3.0 on the reference's seed
+  and within the oracle's own per-seed bound on the others, sample mean/covariance within the
+  reference's bounds (median over three seeds: the outcome is chaotic).
 """
 import copy
+import json
+import os
 
 import pytest
 import torch
 
 import nfs_amd
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 pytestmark = pytest.mark.gpu
 
@@ -136,20 +141,38 @@ def _train(flow, data, steps=200, lr=1e-3):
     return flow
 
 
+def _oracle_nll_bounds():
+    """Per (model, seed) NLL bounds from the ORACLE's own runs of this protocol
+    (tests/golden/relational_oracle.jsonl, tools/relational_seeds_oracle.py: the reference
+    arithmetic on CPU, fp32 and float64, same seeds, same initial weights and data): the larger of
+    the oracle's two values for that seed plus that model's largest fp32-vs-float64 gap over its
+    seeds (at least 0.01) — how far the reference's own arithmetic moves the 200-step result."""
+    rows = [json.loads(ln) for ln in open(os.path.join(GOLDEN, "relational_oracle.jsonl"))]
+    by = {}
+    for r in rows:
+        by.setdefault((r["kind"], r["seed"]), {})[r["dtype"]] = r["nll"]
+    gap = {}
+    for (k, _), v in by.items():
+        gap[k] = max(gap.get(k, 0.01), abs(v["float32"] - v["float64"]))
+    bounds = {key: max(v.values()) + gap[key[0]] for key, v in by.items()}
+    f32 = {key: v["float32"] for key, v in by.items()}
+    return bounds, f32
+
+
 @pytest.mark.parametrize("kind", ["realnvp", "maf2", "mixed"])
 def test_distribution_preservation_training(cuda_device, kind):
     """tests/correctness/test_distribution_preservation.py: train on N(0, I) samples, then the
     model's samples must have mean ~0 and covariance ~I. 200 Adam steps from a fresh init are
-    chaotic after ~50 steps (the fp32 trajectories of the reference's own CPU composite differ
-    between machines), and the covariance of the result swings widely with the seed: for
-    RealNVP(2,4,32) the reference composite on CPU gives ||cov - I|| = 0.33, 0.50, 0.41, 0.05,
-    1.16, 0.09, 0.58, 0.48 for seeds 0..7 (tools/dbg_train_seeds.py; the kernels: 0.16, 0.27, 0.18,
-    0.22, 0.15, 0.31, 0.06, 0.10). The reference's mean / covariance thresholds are therefore
-    applied to the median over three seeds; its NLL < 3 to its own seed (42, the only one its test
-    runs), and the two added seeds must reach a finite NLL < 3.5: the test NLL after 200 steps is
-    as chaotic (tools/relational_seeds.py, seeds 42, 0..7 on the GPU: 2.91, 3.01, 3.08, 2.93, 3.21,
-    3.04, 2.90, 2.89, 2.90 on the default train path; 2.96, 2.90, 2.98, 2.90, 3.01, 2.87, 3.26,
-    2.91, 2.90 with NFX_TRAIN_KEEP=0)."""
+    chaotic for the train-mode BatchNorm models: the reference arithmetic itself (the oracle on
+    CPU, tests/golden/relational_oracle.jsonl) ends seed 0 at NLL 3.35 in fp32 and 2.85 in float64,
+    seed 7 at 3.63 / 2.92, and reaches ||cov - I|| = 1.04 (seed 2, fp32). The reference's mean /
+    covariance thresholds are therefore applied to the median over three seeds; its NLL < 3 to
+    its own seed (42, the only one its test runs); every seed's NLL must stay within the oracle's
+    own per-seed bound (_oracle_nll_bounds), and their mean within 0.1 of the oracle's fp32 mean over
+the same seeds. The GPU values per seed on both train paths are in
+    profiles/r06_relational_seeds/ (tools/relational_seeds.py)."""
+    bounds, oracle32 = _oracle_nll_bounds()
+    nlls = []
     dim, H = 2, 32
     covs, means = [], []
     for seed in (42, 0, 1):
@@ -171,9 +194,15 @@ def test_distribution_preservation_training(cuda_device, kind):
         with torch.no_grad():
             nll = -f.log_prob(test)
             assert torch.isfinite(nll).all()
-            assert nll.mean().item() < (3.0 if seed == 42 else 3.5), (seed, nll.mean().item())
+            assert nll.mean().item() < bounds[(kind, seed)], (seed, nll.mean().item(), bounds[(kind, seed)])
+            if seed == 42:
+                assert nll.mean().item() < 3.0, nll.mean().item()  # the reference's own bar
+            nlls.append(nll.mean().item())
             xs, _ = f.forward(torch.randn(1000, dim, device=cuda_device))
         means.append(torch.norm(xs.mean(0)).item())
         covs.append(torch.norm(torch.cov(xs.T) - torch.eye(dim, device=cuda_device)).item())
     assert sorted(means)[1] < 0.3, means
     assert sorted(covs)[1] < 0.5, covs
+    # and over the three seeds the kernels do no worse than the reference arithmetic in fp32
+    ref = sum(oracle32[(kind, sd)] for sd in (42, 0, 1)) / 3
+    assert sum(nlls) / 3 <= ref + 0.1, (nlls, ref)

@@ -378,3 +378,19 @@ def test_options_g17(case):
     for k in g:  # running statistics after the step(s): updated once per MADE call
         if k.startswith(after):
             close(sd[k[len(after):]], g[k], rtol=1e-5, atol=1e-6)
+
+
+def test_relational_oracle_fixture_reproduces():
+    """tests/golden/relational_oracle.jsonl (the per-seed bounds of
+    test_gpu_relational.py::test_distribution_preservation_training) is the oracle's own output:
+    re-run the cheapest entry (maf2, seed 42, fp32: 200 Adam steps through oracle/flows_ref.py)."""
+    import json
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import relational_seeds_oracle as rso
+    rows = [json.loads(ln) for ln in open(os.path.join(root, "tests", "golden", "relational_oracle.jsonl"))]
+    want = next(r for r in rows if r["kind"] == "maf2" and r["seed"] == 42 and r["dtype"] == "float32")
+    got = rso.run(42, torch.float32, "maf2")
+    assert got["steps"] == want["steps"] and abs(got["nll"] - want["nll"]) <= 2e-4, (got, want)
