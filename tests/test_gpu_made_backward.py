@@ -216,3 +216,72 @@ def test_wide_hidden_training_step(cuda_device, cls):
     assert abs(loss.item() - l64.item()) <= 1e-5 * (1 + abs(l64.item()))
     for (k, p), (_, p64) in zip(mg.named_parameters(), m64.named_parameters()):
         _check(p.grad, p64.grad, 5e-5)
+
+
+def test_made_weight_grad_nonfinite_pattern(cuda_device):
+    """The weight-gradient contraction skips output tiles whose 32x32 mask block is all zero
+    (round 6). Where the reference's (δ·aᵀ) ⊙ mask is NaN there (0 x inf: a non-finite upstream
+    gradient reaches a δ row), the kernel must give NaN too: every parameter gradient has the
+    composite's NaN / inf pattern, and equal values elsewhere within the parity bar."""
+    d, H, B = 63, 64, 512
+    f = _maf(d, H, 11)
+    x = torch.randn(B, d)
+    gz, gld = torch.randn(B, d), torch.randn(B)
+    gz[7, 20] = float("inf")
+    gxc, gpc = _grads(copy.deepcopy(f), x, gz, gld)
+    gx, gp = _grads(f.to(cuda_device).train(), x.to(cuda_device), gz.to(cuda_device), gld.to(cuda_device))
+    for g, r in zip(gp, gpc):
+        g = g.cpu()
+        assert torch.equal(g.isnan(), r.isnan()), (int(g.isnan().sum()), int(r.isnan().sum()))
+        assert torch.equal(g.isinf(), r.isinf())
+        fin = r.isfinite()
+        if fin.any():
+            _check(g[fin], r[fin], 2e-5)
+
+
+@pytest.mark.parametrize("B", [1000, 4099])
+def test_made_backward_weights_abi_nonfinite_factors(cuda_device, B):
+    """nfx_made_backward_weights on synthetic factors against float64 (δ·aᵀ) ⊙ mask and Σ δ:
+    a non-finite INPUT row entry (column flags of the skipped masked tiles) and a NaN δ entry
+    (row flags) give the reference's NaN / inf pattern; every finite entry within 2e-5 of the
+    float64 value's scale."""
+    from nfs_amd import _lib
+    import ctypes
+    L = _lib.lib()
+    d, H = 63, 64
+    f = _maf(d, H, 5)
+    masks = [lin.mask.detach().float() for lin in f.conditioner.linears()]
+    g = torch.Generator().manual_seed(B)
+    rows = 2 * d + 3 * H + 3 * (H + 1) + (d + 1)
+    fac = torch.randn(rows, B, generator=g)
+    o = {"D4": 0, "D3": 2 * d, "D2": 2 * d + H, "D1": 2 * d + 2 * H, "H3": 2 * d + 3 * H,
+         "H2": 2 * d + 4 * H + 1, "H1": 2 * d + 5 * H + 2, "X1": 2 * d + 6 * H + 3}
+    fac[o["X1"] + 40, 5] = float("inf")   # input 40 of layer 1: a column of W1's tiles
+    fac[o["D2"] + 3, 7] = float("nan")    # δ row 3 of layer 2
+    pairs = [("D1", H, "X1", d), ("D2", H, "H1", H), ("D3", H, "H2", H), ("D4", 2 * d, "H3", H)]
+    want = []
+    for (dn, m, an, n), mk in zip(pairs, masks):
+        D = fac[o[dn]:o[dn] + m].double()
+        A = fac[o[an]:o[an] + n].double()
+        want += [(D @ A.T) * mk.double(), D.sum(1)]
+    assert L.nfx_made_backward_factor_floats(B, d, H) >= fac.numel()
+    dev = cuda_device
+    facd = torch.zeros(L.nfx_made_backward_factor_floats(B, d, H), device=dev)
+    facd[:fac.numel()] = fac.reshape(-1).to(dev)
+    grads = torch.empty(L.nfx_made_param_floats(d, H), device=dev)
+    ws = torch.empty(max(1, L.nfx_made_wgrad_workspace_bytes(B, d, H)), device=dev, dtype=torch.uint8)
+    md = [m.to(dev).contiguous() for m in masks]
+    mp = (ctypes.c_void_p * 4)(*[m.data_ptr() for m in md])
+    _lib.check(L.nfx_made_backward_weights(_lib.ptr(facd), B, d, H, mp, _lib.ptr(grads), _lib.ptr(ws),
+                                           _lib.stream_of(facd)), "nfx_made_backward_weights")
+    got, off = [], 0
+    gc = grads.cpu()
+    for w in want:
+        got.append(gc[off:off + w.numel()].view_as(w))
+        off += w.numel()
+    for gv, wv in zip(got, want):
+        assert torch.equal(gv.isnan(), wv.isnan()), (int(gv.isnan().sum()), int(wv.isnan().sum()))
+        assert torch.equal(gv.isinf(), wv.isinf())
+        fin = wv.isfinite()
+        err = (gv.double()[fin] - wv[fin]).abs().max().item()
+        assert err <= 2e-5 * (1 + wv[fin].abs().max().item()), err
