@@ -135,6 +135,16 @@ int nfx_affine_chain(const float* const* packs, int n_layers, const float* in, f
 int nfx_affine_chain_logprob(const float* const* packs, int n_layers, const float* in, float* out,
                              float* log_det, float* logp, double* sums, void* workspace, int64_t B,
                              int d, int H, int accumulate, void* stream);
+/* The sampling pass with its base draw fused in (Flow.sample, src/flows/flow/flow.py:40-54; the
+ * reference's throughput loop plots/_common.py:264-274): z ~ N(0, I) drawn on the device
+ * (Philox4x32-10 keyed by `seed`, counter = (sample, offset); Box-Muller), then the forward chain,
+ * in ONE launch of the small-batch chain (B up to 64k rows at d = 2; NFX_EUNSUPPORTED above).
+ * rng_state: device uint64[2] = {counter offset, arrival count}, zero-filled once; every launch
+ * reads the offset and its last workgroup advances it, so repeated launches (and replays of a
+ * captured graph) draw fresh values. z (may be NULL) receives the draws, x = forward(z) bit for bit
+ * as nfx_affine_chain would give for that z, log_det written. */
+int nfx_affine_chain_sample(const float* const* packs, int n_layers, uint64_t seed, uint64_t* rng_state,
+                            float* z, float* x, float* log_det, int64_t B, int d, int H, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Rational-quadratic spline coupling — SplineCouplingLayer

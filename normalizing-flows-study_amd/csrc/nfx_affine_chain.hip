@@ -18,12 +18,17 @@
 
 namespace nfx {
 
-template <int HT, int D, int DIR, bool LOGP>
+// SAMPLE (forward chains): the rows are not read from `in` but drawn on the device — z ~ N(0, I)
+// from Philox4x32-10 keyed by `seed` at the counter offset rng[0] (base_draw, nfx_chain.h),
+// written to `zout` when non-null — and the LAST workgroup to finish advances rng[0] past this
+// launch's draws (arrival count in rng[1]), so a replayed graph draws fresh values every time.
+template <int HT, int D, int DIR, bool LOGP, bool SAMPLE = false>
 __global__ __launch_bounds__(128 * HT) void affine_chain_kernel(NfxChainPacks packs, int nl, const float* __restrict__ in,
                                                                 float* __restrict__ out, float* __restrict__ logdet,
                                                                 int64_t B, int accumulate, int64_t ntiles, int tpw,
                                                                 float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums,
-                                                                float cgauss) {
+                                                                float cgauss, uint64_t seed = 0, uint64_t* rng = nullptr,
+                                                                float* __restrict__ zout = nullptr) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
     constexpr int NB1 = HT * 32;
@@ -42,7 +47,22 @@ __global__ __launch_bounds__(128 * HT) void affine_chain_kernel(NfxChainPacks pa
     const int64_t t0 = (int64_t)blockIdx.x * tpw;
     const int nt = (int)(ntiles - t0 < tpw ? ntiles - t0 : tpw);
     const int64_t r0 = t0 * 32;
-    for (int e = threadIdx.x; e < nt * 32 * D; e += NTHR) sx[e] = r0 + e / D < B ? in[r0 * D + e] : 0.f;
+    if constexpr (SAMPLE) {
+        const uint64_t off = __hip_atomic_load(rng, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int e = threadIdx.x; e < nt * 32; e += NTHR) {
+            const int64_t row = r0 + e;
+            float z[D];
+            base_draw<D>(row, seed, off, z);
+#pragma unroll
+            for (int j = 0; j < D; ++j) sx[e * D + j] = row < B ? z[j] : 0.f;
+            if (zout && row < B) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) zout[row * D + j] = z[j];
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < nt * 32 * D; e += NTHR) sx[e] = r0 + e / D < B ? in[r0 * D + e] : 0.f;
+    }
     for (int e = threadIdx.x; e < nt * 32; e += NTHR) sld[e] = (accumulate && r0 + e < B) ? logdet[r0 + e] : 0.f;
 
     for (int li = 0; li < nl; ++li) {
@@ -175,10 +195,25 @@ __global__ __launch_bounds__(128 * HT) void affine_chain_kernel(NfxChainPacks pa
     if constexpr (LOGP) {
         logp_commit<NTHR>(lpacc, partials, sums, B);
     }
+    if constexpr (SAMPLE) {
+        // every workgroup read rng[0] in its prologue; the last one to get here moves it on
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            uint64_t* cnt = rng + 1;
+            const uint64_t prev = __hip_atomic_fetch_add(cnt, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == (uint64_t)gridDim.x - 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                __hip_atomic_store(rng, __hip_atomic_load(rng, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(cnt, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 }
 
 typedef void (*affine_chain_t)(NfxChainPacks, int, const float*, float*, float*, int64_t, int, int64_t, int, float*,
-                               double*, double*, float);
+                               double*, double*, float, uint64_t, uint64_t*, float*);
 
 template <int HT, int D>
 static affine_chain_t chain_pick_d(int dir, bool logp) {
@@ -191,6 +226,13 @@ static affine_chain_t chain_pick_ht(int d, int dir, bool logp) {
     if (d <= 2) return chain_pick_d<HT, 2>(dir, logp);
     if (d <= 4) return chain_pick_d<HT, 4>(dir, logp);
     return chain_pick_d<HT, 8>(dir, logp);
+}
+
+template <int HT>
+static affine_chain_t sample_pick_ht(int d) {
+    if (d <= 2) return affine_chain_kernel<HT, 2, 1, false, true>;
+    if (d <= 4) return affine_chain_kernel<HT, 4, 1, false, true>;
+    return affine_chain_kernel<HT, 8, 1, false, true>;
 }
 
 static int chain_pad_d(int d) { return d <= 2 ? 2 : (d <= 4 ? 4 : 8); }
@@ -216,8 +258,9 @@ bool chain_supported(int64_t B, int d, int H) {
 
 static int chain_launch(const float* const* packs, int nl, const float* in, float* out, float* log_det, int64_t B,
                         int d, int H, int direction, int accumulate, float* logp, double* sums, void* workspace,
-                        hipStream_t s) {
+                        hipStream_t s, uint64_t* rng = nullptr, uint64_t seed = 0, float* zout = nullptr) {
     const bool fused = sums != nullptr;
+    const bool sample = rng != nullptr;
     if (nl <= 0 || nl > kChainMax) return set_error(NFX_EINVAL, "affine_chain: 1 <= n_layers <= %d (got %d)", kChainMax, nl);
     if (d <= 0 || d > 8 || H <= 0 || H > 128)
         return set_error(NFX_EUNSUPPORTED, "affine_chain: d=%d H=%d outside d<=8, H<=128", d, H);
@@ -226,9 +269,12 @@ static int chain_launch(const float* const* packs, int nl, const float* in, floa
     if (fused && direction != NFX_INVERSE) return set_error(NFX_EINVAL, "affine_chain_logprob: inverse chains only");
     if (B < 0) return set_error(NFX_EINVAL, "affine_chain: B < 0");
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, s) : NFX_OK;
-    if (!packs || !in || !out || !log_det || (fused && (!logp || !workspace)))
+    if (!packs || (!in && !sample) || !out || !log_det || (fused && (!logp || !workspace)))
         return set_error(NFX_EINVAL, "affine_chain: null pointer");
-    if (in == out) return set_error(NFX_EINVAL, "affine_chain: in and out must not alias");
+    if (in == out && !sample) return set_error(NFX_EINVAL, "affine_chain: in and out must not alias");
+    if (sample && (direction != NFX_FORWARD || fused || accumulate))
+        return set_error(NFX_EINVAL, "affine_chain_sample: forward chains, no accumulate");
+    if (sample && zout == out) return set_error(NFX_EINVAL, "affine_chain_sample: z and x must not alias");
     NfxChainPacks P{};
     for (int l = 0; l < nl; ++l) {
         if (!packs[l]) return set_error(NFX_EINVAL, "affine_chain: layer %d pack is null", l);
@@ -241,9 +287,13 @@ static int chain_launch(const float* const* packs, int nl, const float* in, floa
     // policy forces either (tests compare each with its per-layer kernel bit for bit).
     const int pol = affine_policy_get();
     const bool want_stream = pol == NFX_AFFINE_STREAMING || (pol == NFX_AFFINE_AUTO && B > kSmallChainMaxB);
-    if (want_stream && schain_supported(B, d, H))
+    if (want_stream && schain_supported(B, d, H) && !sample)
         return schain_launch(P, nl, in, out, log_det, B, d, H, direction, accumulate, logp, sums, workspace, s);
-    affine_chain_t k = HT == 1 ? chain_pick_ht<1>(d, direction, fused)
+    if (sample && B > small_chain_max_b(D))
+        return set_error(NFX_EUNSUPPORTED, "affine_chain_sample: B=%lld above the small-batch chain", (long long)B);
+    affine_chain_t k = sample ? (HT == 1 ? sample_pick_ht<1>(d) : HT == 2 ? sample_pick_ht<2>(d)
+                                 : HT == 3 ? sample_pick_ht<3>(d) : sample_pick_ht<4>(d))
+                       : HT == 1 ? chain_pick_ht<1>(d, direction, fused)
                        : HT == 2 ? chain_pick_ht<2>(d, direction, fused)
                        : HT == 3 ? chain_pick_ht<3>(d, direction, fused) : chain_pick_ht<4>(d, direction, fused);
     const int64_t ntiles = (B + 31) / 32;
@@ -259,7 +309,7 @@ static int chain_launch(const float* const* packs, int nl, const float* in, floa
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
     k<<<(unsigned)grid, 128 * HT, lds, s>>>(P, nl, in, out, log_det, B, accumulate, ntiles, (int)tpw, logp,
-                                            reinterpret_cast<double*>(workspace), sums, gauss_const(d));
+                                            reinterpret_cast<double*>(workspace), sums, gauss_const(d), seed, rng, zout);
     return check_launch("affine_chain_kernel");
 }
 
@@ -282,4 +332,11 @@ extern "C" int nfx_affine_chain_logprob(const float* const* packs, int n_layers,
     if (!sums) return set_error(NFX_EINVAL, "affine_chain_logprob: null sums");
     return chain_launch(packs, n_layers, in, out, log_det, B, d, H, NFX_INVERSE, accumulate, logp, sums, workspace,
                         (hipStream_t)stream);
+}
+
+extern "C" int nfx_affine_chain_sample(const float* const* packs, int n_layers, uint64_t seed, uint64_t* rng_state,
+                                       float* z, float* x, float* log_det, int64_t B, int d, int H, void* stream) {
+    if (!rng_state) return set_error(NFX_EINVAL, "affine_chain_sample: null rng_state");
+    return chain_launch(packs, n_layers, nullptr, x, log_det, B, d, H, NFX_FORWARD, 0, nullptr, nullptr, nullptr,
+                        (hipStream_t)stream, rng_state, seed, z);
 }

@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "nfx_abi_version", "nfx_last_error", "nfx_last_kernel", "nfx_debug_fill_lds",
     "nfx_affine_packed_floats", "nfx_affine_pack", "nfx_affine_coupling", "nfx_affine_coupling_logprob",
     "nfx_affine_kernel_policy", "nfx_affine_chain", "nfx_affine_chain_logprob", "nfx_affine_chain_supported",
+    "nfx_affine_chain_sample",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
     "nfx_spline_chain_supported", "nfx_spline_chain", "nfx_spline_chain_logprob",
     "nfx_rqs_unit", "nfx_rqs_unit_backward",
@@ -137,6 +138,8 @@ _SIGNATURES = {
     "nfx_affine_chain": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _i64, _int, _int, _int, _int, _vp]),
     "nfx_affine_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,
                                         _int, _vp]),
+    "nfx_affine_chain_sample": (_int, [ctypes.POINTER(_vp), _int, ctypes.c_uint64, _vp, _vp, _vp, _vp, _i64, _int, _int,
+                                       _vp]),
     "nfx_arqs_packed_floats": (_sz, [_int, _int, _int]),
     "nfx_arqs_pack": (_int, [ctypes.POINTER(NfxMlpRaw), _int, _int, _int, _vp, _vp]),
     "nfx_arqs": (_int, [_vp, _vp, _vp, _vp, _i64, _int, _int, _int, _f, _f, _f, _int, ctypes.c_double,

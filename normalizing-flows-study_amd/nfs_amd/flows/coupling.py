@@ -96,6 +96,38 @@ def chain_launch(flows, x, out, ld, direction, accumulate, logprob=None):
     STATS["hip"] += 1
 
 
+def sample_chain_ok(flows, n, device):
+    """chain_ok for the fused sampling pass (nfx_affine_chain_sample): eval-mode CouplingLayers of
+    one (d, H), d in {2, 4, 8}, H <= 128, n rows within the small-batch chain, a ROCm device."""
+    if FORCE_GENERIC or not flows or len(flows) > 64 or n <= 0 or torch.device(device).type != "cuda":
+        return False
+    f0 = flows[0]
+    if type(f0) is not CouplingLayer:
+        return False
+    d, H = f0.data_dim, f0._hidden()
+    if d not in (2, 4, 8) or H > MAX_H or n > SAMPLE_CHAIN_MAX_B:
+        return False
+    return all(type(f) is CouplingLayer and f.data_dim == d and f._hidden() == H and not f._torch_only()
+               and not f.training for f in flows)
+
+
+# the fused sampling pass runs the small-batch chain layout (one workgroup per 32-row tile up to
+# 4 per CU, then several tiles per workgroup): up to 64k rows, the sizes sampling is called at
+SAMPLE_CHAIN_MAX_B = 1 << 16
+
+
+def chain_sample(flows, rng_state, seed, z, x, ld):
+    """z ~ N(0, I) drawn on the device and x, ld = forward(z) through every flow, one launch
+    (nfx_affine_chain_sample); rng_state = the device uint64[2] generator state it advances."""
+    packs = (ctypes_vp * len(flows))(*[_lib.ptr(f._packed(x.device, f._build_pack)) for f in flows])
+    d, H = flows[0].data_dim, flows[0]._hidden()
+    p = _lib.ptr
+    _lib.check(_lib.lib().nfx_affine_chain_sample(packs, len(flows), int(seed) & ((1 << 64) - 1), p(rng_state), p(z),
+                                                  p(x), p(ld), x.shape[0], d, H, _lib.stream_of(x)),
+               "nfx_affine_chain_sample")
+    STATS["hip"] += 1
+
+
 def _pad_d(d):
     return 2 if d <= 2 else (4 if d <= 4 else 8)
 

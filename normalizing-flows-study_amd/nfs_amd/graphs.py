@@ -9,10 +9,13 @@ bound by. Inputs go through a static buffer; outputs are the graph's static tens
 until the next replay).
 
 mode="sample" is the fused sampling path (`Flow.sample`, flow.py:40-54,
-and the reference's sampling throughput loop, plots/_common.py:217-222,264-274): the graph
-draws z ~ N(0, I) on device with torch's graph-safe Philox generator (a fresh draw per replay)
-and runs forward(z) — one graph launch per batch of samples, no host round trip. The example
-tensor only gives the shape [n, d]; `static_in` holds the last z.
+and the reference's sampling throughput loop, plots/_common.py:217-222,264-274): z ~ N(0, I) is
+drawn on the device and forward(z) runs in one graph launch per batch of samples, no host round
+trip. For chains of eval CouplingLayers (RealNVP) the draw is fused INTO the chain kernel
+(nfx_affine_chain_sample: Philox4x32-10 in the kernel's prologue, the generator state advanced on
+the device, so every replay draws afresh — the graph holds one kernel); other models draw with
+torch's graph-safe Philox generator (normal_) ahead of their forward. The example tensor only
+gives the shape [n, d]; `static_in` holds the last z.
 
 The packed weight images are built before capture and baked into the graph. With
 `strict=True` (default) every call checks that no parameter or buffer changed since capture
@@ -74,6 +77,15 @@ class GraphedFlow:
 
     def _call(self):
         if self.mode == "sample":
+            n = self.static_in.shape[0]
+            if hasattr(self.model, "sample_fused_ok") and self.model.sample_fused_ok(n, self.static_in.device):
+                if not hasattr(self, "_sx"):
+                    self._sx = torch.empty_like(self.static_in)
+                    self._sld = torch.empty(n, device=self.static_in.device)
+                self.fused_draw = True
+                x, ld, _ = self.model.sample_fused(n, self.static_in.device, out=(self.static_in, self._sx, self._sld))
+                return x, ld
+            self.fused_draw = False
             self.static_in.normal_()
             return self.model.forward(self.static_in)
         if self.mode == "log_prob":

@@ -219,6 +219,40 @@ class NormalizingFlowModel(nn.Module):
                                 torch.tensor(float(z.shape[0]), dtype=torch.float64, device=z.device)])
         return (logp, sums) if return_sums else logp
 
+    # -- sampling with the base draw on the device ---------------------------------------------
+    def sample_fused_ok(self, num_samples, device):
+        """True when sample_fused runs as one kernel (eval-mode CouplingLayers, no between-layer
+        BatchNorm, d in {2, 4, 8}, H <= 128, up to 64k samples)."""
+        return not self.batch_norm_between_layers and _coupling.sample_chain_ok(list(self.flows), num_samples, device)
+
+    def sample_fused(self, num_samples, device="cuda", out=None):
+        """Flow.sample (src/flows/flow/flow.py:40-54) with the N(0, I) base draw fused into the
+        sampling forward: z ~ N(0, I) on the device (Philox4x32-10, this model's own generator
+        state, seeded from torch's CPU generator on first use) and x = forward(z), ONE launch
+        (nfx_affine_chain_sample). Returns (x, log_det, z); x equals forward(z) bit for bit.
+        out=(z, x, ld) writes into caller buffers (GraphedFlow(mode="sample"))."""
+        dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if not self.sample_fused_ok(num_samples, dev):
+            raise NotImplementedError("sample_fused: the fused sampling chain does not take this model / size")
+        st = getattr(self, "_nfx_rng", None)
+        if st is None:
+            st = self._nfx_rng = {}
+        if dev not in st:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            st[dev] = (seed, torch.zeros(2, dtype=torch.int64, device=dev))
+        seed, state = st[dev]
+        d = self.flows[0].data_dim
+        if out is None:
+            z = torch.empty(num_samples, d, device=dev)
+            x = torch.empty_like(z)
+            ld = torch.empty(num_samples, device=dev)
+        else:
+            z, x, ld = out
+        _coupling.chain_sample(list(self.flows), state, seed, z, x, ld)
+        return x, ld, z
+
     def nll(self, x):
         """Mean negative log-likelihood, accumulated in float64 (python float)."""
         _, sums = self.log_prob(x, return_sums=True)
