@@ -117,6 +117,9 @@ __device__ __forceinline__ void seqp_use(const T& v) { asm volatile("" ::"v"(v))
 // (row_bcast:31; lanes of disabled rows keep their value); the total is lane 63's, returned
 // uniform. (The s_nop covers the DPP read-after-VALU-write hazard the asm hides from the compiler.)
 __device__ __forceinline__ float seqp_wave_sum(float v) {
+#ifdef NFX_SEQP_ABL_SUM  // timing ablation only (wrong results): no cross-lane reduction
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+#endif
     v = row16_allsum(v);
     asm volatile(
         "s_nop 1\n\t"
@@ -133,6 +136,13 @@ template <int VAR>
 __device__ __forceinline__ float seqp_affine(const f32x2 p, float x, uint64_t M, float& z, float& al) {
 #pragma clang fp contract(off)
     float v, a;
+#ifdef NFX_SEQP_ABL_AFF  // timing ablation only (wrong results): the affine map without clamp / exp
+    a = p[1];
+    v = x - p[0];
+    z = seqp_sel(M, v, z);
+    al = seqp_sel(M, a, al);
+    return v;
+#endif
     if constexpr (VAR == NFX_MAF_FORWARD) {
         a = tclamp(p[1], -3.f, 3.f);
         v = x * exp_fast(a) + p[0];
@@ -201,9 +211,13 @@ __device__ __forceinline__ bool seqp_chunk(SeqpState<S>& st, const SeqpCtx& c, S
         const float P3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(st.acc23[1]), g));
         const float tsum = seqp_wave_sum(t);
         NFX_PMARK(st, 2);  // W1 wait + layer-1 sum
+#ifdef NFX_SEQP_ABL_CHAIN  // timing ablation only (wrong results): layers 1-3 of the completing unit skipped
+        const float h1 = tsum, h2 = tsum + wd2 * 0.f * P2, h3 = tsum + wd3 * 0.f * P3;
+#else
         const float h1 = trelu(tsum);
         const float h2 = trelu(fmaf(wd2, h1, P2));
         const float h3 = trelu(fmaf(wd3, h2, P3));
+#endif
         const uint64_t c1 = seqp_mask(e[2], e[3]), c2 = seqp_mask(e[10], e[11]), c3 = seqp_mask(e[12], e[13]);
         st.acc23 = __builtin_elementwise_fma(st.w23, f32x2{seqp_sel(c1, h1, 0.f), seqp_sel(c2, h2, 0.f)}, st.acc23);
         seqp_pin(st.acc23);
