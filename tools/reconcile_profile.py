@@ -123,13 +123,36 @@ def mfma_busy(counter_csv, trace_csv, hot):
                         "source": os.path.relpath(counter_csv, ROOT)},
            "mfma_busy_frac": busy / (N_SIMD * cyc) if cyc else None,
            "mfma_issue_frac": imfma * MFMA_F32_CYCLES / (N_SIMD * cyc) if cyc else None,
-           "valu_insts_per_mfma": ivalu / imfma if imfma else None}
+           "valu_insts_per_mfma": ivalu / imfma if imfma else None,
+           # VALU issue slots used, at 4 cycles per wave instruction (8 for transcendentals: a
+           # lower bound) — the pipe of the kernels that issue no MFMA (cfg5i)
+           "valu_issue_frac": ivalu * 4 / (N_SIMD * cyc) if cyc else None}
     ds = [d for _, d in rows if d]
     if ds:
         mean_ns = sum(ds) / len(ds)
         out["clock_ghz"] = cyc / mean_ns
         out["pmc_mfma"]["mean_duration_us"] = mean_ns / 1e3
     return out
+
+
+def busy_identity(res, f_launch, spl):
+    """The frac of the MFMA-busy pass's own dispatches (algorithmic flop / its duration / peak)
+    and the same number rebuilt from the counters: busy x clock / 2.4 GHz / (issued / algorithmic
+    MFMA flop) — equal by construction when BUSY counts 64 cycles per fp32 32x32x2 MFMA; the
+    trace pass's frac differs from it only by the PMC pass running its kernels a little slower."""
+    pm = res.get("pmc_mfma")
+    if not pm or not pm.get("mean_duration_us") or not pm.get("SQ_INSTS_MFMA"):
+        return
+    alg = f_launch * spl
+    issued = pm["SQ_INSTS_MFMA"] * 4096.0
+    frac_pmc = alg / (pm["mean_duration_us"] * 1e-6) / 1e12 / PEAK
+    res["mfma_identity"] = {
+        "frac_pmc_pass": frac_pmc,
+        "issued_over_algorithmic": issued / alg,
+        "busy_x_clock_over_peak_clock": res["mfma_busy_frac"] * res["clock_ghz"] / PEAK_CLOCK_GHZ,
+        "rebuilt_frac": res["mfma_busy_frac"] * res["clock_ghz"] / PEAK_CLOCK_GHZ * alg / issued,
+        "note": "frac = busy x clock/2.4 GHz x algorithmic/issued; the rest of the SIMD-cycles are "
+                "VALU (fp32 VALU and fp32 MFMA share the pipe) and waits"}
 
 
 def reconcile(cdir, rtag):
@@ -220,6 +243,7 @@ def reconcile(cdir, rtag):
     mt = _newest(os.path.join(cdir, "mfma", "*", "*kernel_trace.csv"))
     if mf:
         res.update(mfma_busy(mf, mt, hot))
+        busy_identity(res, f_launch, spl)
     out = os.path.join(ROOT, "profiles", f"{rtag}_{name}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
