@@ -185,6 +185,11 @@ int nfx_spline_chain_logprob(const float* const* packs, int n_layers, const floa
                              float* log_det, float* logp, double* sums, void* workspace, int64_t B, int d,
                              int H, int K, float bound, float min_bin_width, float min_bin_height,
                              float min_derivative, int accumulate, void* stream);
+/* The sampling pass of a d = 2 spline chain (RealNVPSpline.forward on z ~ N(0, I)) with the base
+ * draw fused in, as nfx_affine_chain_sample (same generator, same rng_state semantics). */
+int nfx_spline_chain_sample(const float* const* packs, int n_layers, uint64_t seed, uint64_t* rng_state,
+                            float* z, float* x, float* log_det, int64_t B, int d, int H, int K, float bound,
+                            float min_bin_width, float min_bin_height, float min_derivative, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Unit-interval RQ spline — rational_quadratic_spline

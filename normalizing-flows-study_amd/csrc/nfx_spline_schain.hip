@@ -23,8 +23,11 @@ static bool spline_chain_supported(int64_t B, int d, int H, int K) {
 static int spline_chain_launch(const float* const* packs, int nl, const float* in, float* out, float* log_det,
                                int64_t B, int d, int H, int K, float bound, float min_w, float min_h, float min_d,
                                int direction, int accumulate, float* logp, double* sums, void* workspace,
-                               hipStream_t s) {
+                               hipStream_t s, uint64_t* rng = nullptr, uint64_t seed = 0, float* zout = nullptr) {
     const bool fused = sums != nullptr;
+    const bool sample = rng != nullptr;
+    if (sample && (direction != NFX_FORWARD || fused || accumulate))
+        return set_error(NFX_EINVAL, "spline_chain_sample: forward chains, no accumulate");
     if (nl <= 0 || nl > kChainMax) return set_error(NFX_EINVAL, "spline_chain: 1 <= n_layers <= %d (got %d)", kChainMax, nl);
     if (direction != NFX_FORWARD && direction != NFX_INVERSE)
         return set_error(NFX_EINVAL, "spline_chain: direction must be +1 or -1");
@@ -33,9 +36,10 @@ static int spline_chain_launch(const float* const* packs, int nl, const float* i
     if (!spline_chain_supported(B, d, H, K))
         return set_error(NFX_EUNSUPPORTED, "spline_chain: d=%d H=%d K=%d outside d = 2, H <= 64, 2 <= K <= 11", d, H, K);
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, s) : NFX_OK;
-    if (!packs || !in || !out || !log_det || (fused && (!logp || !workspace)))
+    if (!packs || (!in && !sample) || !out || !log_det || (fused && (!logp || !workspace)))
         return set_error(NFX_EINVAL, "spline_chain: null pointer");
-    if (in == out) return set_error(NFX_EINVAL, "spline_chain: in and out must not alias");
+    if (in == out && !sample) return set_error(NFX_EINVAL, "spline_chain: in and out must not alias");
+    if (sample && zout == out) return set_error(NFX_EINVAL, "spline_chain_sample: z and x must not alias");
     NfxChainPacks P{};
     for (int l = 0; l < nl; ++l) {
         if (!packs[l]) return set_error(NFX_EINVAL, "spline_chain: layer %d pack is null", l);
@@ -66,7 +70,7 @@ static int spline_chain_launch(const float* const* packs, int nl, const float* i
     if (rc) return rc;
     k<<<(unsigned)grid, 64 * nw, lds, s>>>(P, nl, in, out, log_det, B, C, accumulate, nchunks,
                                                             (int)slice, logp, reinterpret_cast<double*>(workspace),
-                                                            sums, gauss_const(d));
+                                                            sums, gauss_const(d), seed, rng, zout);
     return check_launch("spline_schain_kernel");
 }
 
@@ -92,4 +96,13 @@ extern "C" int nfx_spline_chain_logprob(const float* const* packs, int n_layers,
     if (!sums) return set_error(NFX_EINVAL, "spline_chain_logprob: null sums");
     return spline_chain_launch(packs, n_layers, in, out, log_det, B, d, H, K, bound, min_bin_width, min_bin_height,
                                min_derivative, NFX_INVERSE, accumulate, logp, sums, workspace, (hipStream_t)stream);
+}
+
+extern "C" int nfx_spline_chain_sample(const float* const* packs, int n_layers, uint64_t seed, uint64_t* rng_state,
+                                       float* z, float* x, float* log_det, int64_t B, int d, int H, int K, float bound,
+                                       float min_bin_width, float min_bin_height, float min_derivative, void* stream) {
+    if (!rng_state) return set_error(NFX_EINVAL, "spline_chain_sample: null rng_state");
+    return spline_chain_launch(packs, n_layers, nullptr, x, log_det, B, d, H, K, bound, min_bin_width, min_bin_height,
+                               min_derivative, NFX_FORWARD, 0, nullptr, nullptr, nullptr, (hipStream_t)stream,
+                               rng_state, seed, z);
 }

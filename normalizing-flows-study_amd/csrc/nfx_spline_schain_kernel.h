@@ -22,7 +22,8 @@ template <int HT, int K, int DIR, bool LOGP, int NW>
 __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
     NfxChainPacks packs, int nl, const float* __restrict__ in, float* __restrict__ out,
     float* __restrict__ logdet, int64_t B, SplineConsts C, int accumulate, int64_t nchunks, int slice_chunks,
-    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
+    float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss,
+    uint64_t seed, uint64_t* rng, float* __restrict__ zout) {
 #pragma clang fp contract(off)
     constexpr int D = 2;
     constexpr SplineLayout L = spline_layout(HT, D);
@@ -63,7 +64,21 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
         const int64_t s1 = s0 + slice_chunks < c1 ? s0 + slice_chunks : c1;
         const int64_t r0 = s0 * 64;
         const int rows = (int)((B < s1 * 64 ? B : s1 * 64) - r0);
-        for (int e = threadIdx.x; e < rows * D; e += NTH) sx[e] = in[r0 * D + e];
+        if (rng) {  // the fused sampling pass: z ~ N(0, I) drawn here (base_draw, nfx_chain.h)
+            const uint64_t off = __hip_atomic_load(rng, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int e = threadIdx.x; e < rows; e += NTH) {
+                float z[D];
+                base_draw<D>(r0 + e, seed, off, z);
+                sx[e * D] = z[0];
+                sx[e * D + 1] = z[1];
+                if (zout) {
+                    zout[(r0 + e) * D] = z[0];
+                    zout[(r0 + e) * D + 1] = z[1];
+                }
+            }
+        } else {
+            for (int e = threadIdx.x; e < rows * D; e += NTH) sx[e] = in[r0 * D + e];
+        }
         for (int e = threadIdx.x; e < rows; e += NTH) sld[e] = accumulate ? logdet[r0 + e] : 0.f;
         const int nch = (int)(s1 - s0);
         const int F = nch / NW, R = nch - F * NW;
@@ -171,10 +186,24 @@ __global__ __launch_bounds__(64 * NW) void spline_schain_kernel(
     if constexpr (LOGP) {
         logp_commit<NTH>(lpacc, partials, sums, B);
     }
+    if (rng) {  // every workgroup read rng[0] in its slices; the last one to get here moves it on
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            uint64_t* cnt = rng + 1;
+            const uint64_t prev = __hip_atomic_fetch_add(cnt, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == (uint64_t)gridDim.x - 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                __hip_atomic_store(rng, __hip_atomic_load(rng, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(cnt, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 }
 
 typedef void (*spline_schain_t)(NfxChainPacks, int, const float*, float*, float*, int64_t, SplineConsts, int, int64_t,
-                                int, float*, double*, double*, float);
+                                int, float*, double*, double*, float, uint64_t, uint64_t*, float*);
 
 constexpr int kSplineSchainWaves = 12;
 // Strong-scaled shards (at most one 64-row unit per wave and layer): 8 waves, two per SIMD, which

@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "nfx_affine_kernel_policy", "nfx_affine_chain", "nfx_affine_chain_logprob", "nfx_affine_chain_supported",
     "nfx_affine_chain_sample",
     "nfx_spline_packed_floats", "nfx_spline_pack", "nfx_spline_coupling", "nfx_spline_coupling_logprob",
-    "nfx_spline_chain_supported", "nfx_spline_chain", "nfx_spline_chain_logprob",
+    "nfx_spline_chain_supported", "nfx_spline_chain", "nfx_spline_chain_logprob", "nfx_spline_chain_sample",
     "nfx_rqs_unit", "nfx_rqs_unit_backward",
     "nfx_arqs_packed_floats", "nfx_arqs_pack", "nfx_arqs",
     "nfx_made_packed_floats", "nfx_made_pack", "nfx_made_pack_parallel", "nfx_made_pack_sequential", "nfx_made_affine", "nfx_made_affine_logprob", "nfx_made_seq_policy",
@@ -155,6 +155,8 @@ _SIGNATURES = {
                                 _int, _int, _vp]),
     "nfx_spline_chain_logprob": (_int, [ctypes.POINTER(_vp), _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _int,
                                         _int, _f, _f, _f, _f, _int, _vp]),
+    "nfx_spline_chain_sample": (_int, [ctypes.POINTER(_vp), _int, ctypes.c_uint64, _vp, _vp, _vp, _vp, _i64, _int, _int,
+                                       _int, _f, _f, _f, _f, _vp]),
     "nfx_rqs_unit": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int, _vp]),
     "nfx_rqs_unit_backward": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _int, _f, _f, _f, _int,
                                      _vp]),

@@ -425,22 +425,7 @@ def chain_ok(flows, x):
     fp32 ROCm rows that nfx_spline_chain takes."""
     if not CHAIN_ENABLED or FORCE_GENERIC or not flows or len(flows) > 64 or x.shape[0] < max(1, CHAIN_MIN_B):
         return False
-    f0 = flows[0]
-    if type(f0) is not SplineCouplingLayer:
-        return False
-    key = (f0.data_dim, f0._hidden(), f0.num_bins, float(f0.bound), float(f0.min_bin_width),
-           float(f0.min_bin_height), float(f0.min_derivative))
-    if x.dim() != 2 or x.shape[1] != f0.data_dim:
-        return False
-    for f in flows:
-        if type(f) is not SplineCouplingLayer or f._torch_only() or not f._fused_family():
-            return False
-        if f._rescale_scalars() != (0, 0.0, 0.0):
-            return False
-        if (f.data_dim, f._hidden(), f.num_bins, float(f.bound), float(f.min_bin_width), float(f.min_bin_height),
-                float(f.min_derivative)) != key:
-            return False
-    return bool(_lib.lib().nfx_spline_chain_supported(x.shape[0], key[0], key[1], key[2]))
+    return _chain_key_ok(flows, x)
 
 
 def chain_launch(flows, x, out, ld, direction, accumulate, logprob=None):
@@ -460,6 +445,49 @@ def chain_launch(flows, x, out, ld, direction, accumulate, logprob=None):
         _lib.check(L.nfx_spline_chain(packs, len(flows), p(x), p(out), p(ld), x.shape[0], f0.data_dim, f0._hidden(),
                                       f0.num_bins, *consts, int(direction), int(bool(accumulate)), _lib.stream_of(x)),
                    "nfx_spline_chain")
+    STATS["hip"] += 1
+
+
+def sample_chain_ok(flows, n, device):
+    """chain_ok for the fused sampling pass (nfx_spline_chain_sample): eval-mode d = 2
+    SplineCouplingLayers of one (H, K, bound, minimums), no rescale, n rows, a ROCm device."""
+    if not CHAIN_ENABLED or FORCE_GENERIC or not flows or len(flows) > 64 or n <= 0:
+        return False
+    if torch.device(device).type != "cuda" or any(getattr(f, "training", False) for f in flows):
+        return False
+    probe = torch.empty(n, flows[0].data_dim if hasattr(flows[0], "data_dim") else 0, device="meta")
+    return _chain_key_ok(flows, probe)
+
+
+def _chain_key_ok(flows, x):
+    f0 = flows[0]
+    if type(f0) is not SplineCouplingLayer:
+        return False
+    key = (f0.data_dim, f0._hidden(), f0.num_bins, float(f0.bound), float(f0.min_bin_width),
+           float(f0.min_bin_height), float(f0.min_derivative))
+    if x.dim() != 2 or x.shape[1] != f0.data_dim:
+        return False
+    for f in flows:
+        if type(f) is not SplineCouplingLayer or f._torch_only() or not f._fused_family():
+            return False
+        if f._rescale_scalars() != (0, 0.0, 0.0):
+            return False
+        if (f.data_dim, f._hidden(), f.num_bins, float(f.bound), float(f.min_bin_width), float(f.min_bin_height),
+                float(f.min_derivative)) != key:
+            return False
+    return bool(_lib.lib().nfx_spline_chain_supported(x.shape[0], key[0], key[1], key[2]))
+
+
+def chain_sample(flows, rng_state, seed, z, x, ld):
+    """z ~ N(0, I) drawn on the device and x, ld = forward(z) through every flow, one launch
+    (nfx_spline_chain_sample); rng_state = the device uint64[2] generator state it advances."""
+    packs = (ctypes.c_void_p * len(flows))(*[_lib.ptr(f._packed(x.device, f._build_pack)) for f in flows])
+    f0 = flows[0]
+    p = _lib.ptr
+    _lib.check(_lib.lib().nfx_spline_chain_sample(
+        packs, len(flows), int(seed) & ((1 << 64) - 1), p(rng_state), p(z), p(x), p(ld), x.shape[0], f0.data_dim,
+        f0._hidden(), f0.num_bins, float(f0.bound), float(f0.min_bin_width), float(f0.min_bin_height),
+        float(f0.min_derivative), _lib.stream_of(x)), "nfx_spline_chain_sample")
     STATS["hip"] += 1
 
 

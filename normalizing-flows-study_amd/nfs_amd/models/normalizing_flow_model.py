@@ -221,15 +221,24 @@ class NormalizingFlowModel(nn.Module):
 
     # -- sampling with the base draw on the device ---------------------------------------------
     def sample_fused_ok(self, num_samples, device):
-        """True when sample_fused runs as one kernel (eval-mode CouplingLayers, no between-layer
-        BatchNorm, d in {2, 4, 8}, H <= 128, up to 64k samples)."""
-        return not self.batch_norm_between_layers and _coupling.sample_chain_ok(list(self.flows), num_samples, device)
+        """True when sample_fused runs as one kernel: eval-mode CouplingLayers (d in {2, 4, 8},
+        H <= 128, up to 64k samples) or d = 2 SplineCouplingLayers (any batch), no between-layer
+        BatchNorm."""
+        return not self.batch_norm_between_layers and self._sample_chain(num_samples, device) is not None
+
+    def _sample_chain(self, num_samples, device):
+        fl = list(self.flows)
+        for m in (_coupling, _spline):
+            if m.sample_chain_ok(fl, num_samples, device):
+                return m
+        return None
 
     def sample_fused(self, num_samples, device="cuda", out=None):
         """Flow.sample (src/flows/flow/flow.py:40-54) with the N(0, I) base draw fused into the
         sampling forward: z ~ N(0, I) on the device (Philox4x32-10, this model's own generator
         state, seeded from torch's CPU generator on first use) and x = forward(z), ONE launch
-        (nfx_affine_chain_sample). Returns (x, log_det, z); x equals forward(z) bit for bit.
+        (nfx_affine_chain_sample / nfx_spline_chain_sample). Returns (x, log_det, z); x equals
+        forward(z) bit for bit.
         out=(z, x, ld) writes into caller buffers (GraphedFlow(mode="sample"))."""
         dev = torch.device(device)
         if dev.type == "cuda" and dev.index is None:
@@ -250,7 +259,7 @@ class NormalizingFlowModel(nn.Module):
             ld = torch.empty(num_samples, device=dev)
         else:
             z, x, ld = out
-        _coupling.chain_sample(list(self.flows), state, seed, z, x, ld)
+        self._sample_chain(num_samples, dev).chain_sample(list(self.flows), state, seed, z, x, ld)
         return x, ld, z
 
     def nll(self, x):

@@ -30,3 +30,9 @@ class RealNVPSpline(nn.Module):
 
     def nll(self, x):
         return self.flow.nll(x)
+
+    def sample_fused_ok(self, num_samples, device):
+        return self.flow.sample_fused_ok(num_samples, device)
+
+    def sample_fused(self, num_samples, device="cuda", out=None):
+        return self.flow.sample_fused(num_samples, device, out)

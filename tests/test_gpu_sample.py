@@ -1,8 +1,8 @@
 """GPU: the sampling pass with its base draw fused in (Flow.sample,
 src/flows/flow/flow.py:40-54; the reference's throughput loop, plots/_common.py:264-274).
 
-nfx_affine_chain_sample draws z ~ N(0, I) on the device (Philox4x32-10 + Box-Muller in the chain
-kernel's prologue) and runs the forward chain in the same launch. Checked: x and log_det equal the
+nfx_affine_chain_sample / nfx_spline_chain_sample draw z ~ N(0, I) on the device (Philox4x32-10 +
+Box-Muller in the chain kernel's prologue) and run the forward chain in the same launch. Checked: x and log_det equal the
 plain chain's forward(z) on the returned z bit for bit; every call (and every replay of a
 captured graph) draws afresh; the same generator state reproduces the same draw; the draws are
 standard normal (moments, Kolmogorov-Smirnov distance, no correlation between dimensions or
@@ -105,3 +105,47 @@ def test_fused_sample_limits(cuda_device):
     assert not m.sample_fused_ok(100, cuda_device)       # train-mode BatchNorm: not a fixed map
     with pytest.raises(NotImplementedError):
         m.sample_fused(100, cuda_device)
+
+
+def _spline(n_layers, H, seed):
+    torch.manual_seed(seed)
+    m = nfs_amd.RealNVPSpline(2, n_layers, H)
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.1 * torch.randn(p.shape, generator=g))
+    return m
+
+
+@pytest.mark.parametrize("L,H", [(8, 64), (4, 32)])
+@pytest.mark.parametrize("n", [1, 4000, 300_001])
+def test_fused_spline_sample_equals_forward_of_its_draw(cuda_device, L, H, n):
+    """RealNVPSpline (K = 10): the spline chain draws z itself; x, log_det = forward(z) bit for
+    bit, fresh draws per call, any batch (the streaming spline chain)."""
+    m = _spline(L, H, L + H).to(cuda_device).eval()
+    assert m.sample_fused_ok(n, cuda_device)
+    nfs_amd.reset_stats()
+    with torch.no_grad():
+        x, ld, z = m.sample_fused(n, cuda_device)
+        assert nfs_amd.STATS["hip"] == 1 and nfs_amd.STATS["torch"] == 0
+        z = z.clone()
+        xr, ldr = m.forward(z)
+        _, _, z2 = m.sample_fused(n, cuda_device)
+    assert torch.isfinite(z).all()
+    assert torch.equal(x, xr) and torch.equal(ld, ldr)
+    if n > 1:
+        assert not torch.equal(z, z2)
+        assert abs(z.mean().item()) < 6 / math.sqrt(z.numel()) + 1e-3 and abs(z.std().item() - 1) < 0.05
+
+
+def test_graphed_fused_spline_sampling(cuda_device):
+    m = _spline(8, 64, 9).to(cuda_device).eval()
+    g = nfs_amd.GraphedFlow(m, torch.empty(4000, 2, device=cuda_device), mode="sample")
+    assert g.fused_draw and g.launches == 1
+    x1 = g()[0].clone()
+    z1 = g.static_in.clone()
+    g()
+    z2 = g.static_in.clone()
+    assert not torch.equal(z1, z2)
+    with torch.no_grad():
+        assert torch.equal(m.forward(z1)[0], x1)
