@@ -107,6 +107,10 @@ def build(config):
         f = 2 * (d * H + 2 * H * H + 2 * d * H)
         import oracle
         return m, d, f, oracle.maf_spec(5), "cfg4 5x MaskedAutoregressiveFlow(63, 64) log_prob, eval"
+    if config in ("sample4k_fused", "sample4k_spline_fused"):
+        m, d, f, spec, desc = build(config[:-len("_fused")])
+        return m, d, f, spec, desc.replace("sampling: model.forward(z)", "sampling with the N(0, I) draw fused on the "
+                                                                         "device: model.sample_fused(n)")
     if config == "sample4k":
         torch.manual_seed(3)
         m = nfs_amd.RealNVP(2, 10, 128)
@@ -225,7 +229,8 @@ TRAIN_CONFIGS = ("cfg4t", "cfg2t", "train5k", "cfg3t", "trainfig", "trainfig_spl
 DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "trainfig": 2_000, "trainfig_spline": 2_000,
                  "trainfig_maf": 2_000, "trainfig_iaf": 2_000, "cfg3": 1_000_000, "cfg3t": 1_000_000,
                  "cfg4": 4_000_000, "cfg4t": 500_000, "cfg5f": 524_288, "cfg5i": 8_192,
-                 "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000, "sample4k_iaf": 4_000}
+                 "sample4k": 4_000, "sample4k_spline": 4_000, "sample4k_maf": 4_000, "sample4k_iaf": 4_000,
+                 "sample4k_fused": 4_000, "sample4k_spline_fused": 4_000}
 # The reference's only published throughput (assets/benchmark.png via
 # plots/_common.py:264-274): RealNVP(2,10,128) sampling, model.forward(z) on n = 4,000, CPU.
 # The same figure's other sampling numbers: Spline = RealNVPSpline(2,8,64) K=10,
@@ -233,7 +238,11 @@ DEFAULT_BATCH = {"cfg2": 1_000_000, "cfg2t": 1_000_000, "train5k": 5_000, "train
 PUBLISHED_SAMPLING = {"sample4k": ("RealNVP(2,10,128)", 186_000.0),
                       "sample4k_spline": ("RealNVPSpline(2,8,64), K=10", 334_000.0),
                       "sample4k_maf": ("6x MAF(2,64)", 602_000.0),
-                      "sample4k_iaf": ("6x IAF(2,64)", 1_121_000.0)}
+                      "sample4k_iaf": ("6x IAF(2,64)", 1_121_000.0),
+                      # the same models with the base draw inside the timed step (the reference's
+                      # figure times forward(z) on a fixed z: this line does strictly more work)
+                      "sample4k_fused": ("RealNVP(2,10,128), draw included", 186_000.0),
+                      "sample4k_spline_fused": ("RealNVPSpline(2,8,64), K=10, draw included", 334_000.0)}
 # Reference-pinned workloads: weights from the golden fixture (written by importing the
 # reference, tests/golden/make_golden.py), input = the G8 seeded batch, result vs the reference's
 # own full-scale NLL / checksums (tests/golden/g8_full_nll.json).
@@ -448,9 +457,11 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         x = torch.randn(B, d, device=dev, generator=g)
     flow = model.flow if hasattr(model, "flow") else model
 
+    fused_draw = config.endswith("_fused")
     graphed = None
     if graph and not training:
-        graphed = nfs_amd.GraphedFlow(flow, x, mode="forward" if sampling else "log_prob", strict=False)
+        graphed = nfs_amd.GraphedFlow(flow, x, mode=("sample" if fused_draw else "forward") if sampling else "log_prob",
+                                      strict=False)
     # Adam (the reference's optimizer, plots/_common.py:194-211) in torch's fused form: one
     # multi-tensor kernel per step instead of a few dozen per-parameter elementwise launches
     opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=graph, fused=True) if training else None
@@ -493,6 +504,8 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
             if sampling:
                 return out
             sums = out[1]
+        elif sampling and fused_draw:  # z ~ N(0, I) drawn inside the chain kernel, x = forward(z)
+            return flow.sample_fused(B, dev)
         elif sampling:  # sampling pass: x = forward(z), no exchange
             return flow.forward(x)
         else:
@@ -569,7 +582,14 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                 preroll()
                 for r in (None, rec):
                     flow.layer_events = r
-                    if sampling:
+                    if sampling and fused_draw:
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        flow.sample_fused(B, dev)
+                        e1.record()
+                        if r is not None:
+                            r.append((nfs_amd._lib.last_kernel(), e0, e1))
+                    elif sampling:
                         flow.forward(x)
                     else:
                         flow.log_prob(x, return_sums=True)
@@ -916,7 +936,8 @@ def main(argv=None):
     ap.add_argument("--config", default="cfg2",
                     choices=["cfg2", "cfg2t", "train5k", "trainfig", "trainfig_spline", "trainfig_maf", "trainfig_iaf", "cfg3", "cfg3t", "cfg4", "cfg4t", "cfg5f", "cfg5i",
                              "sample4k",
-                             "sample4k_spline", "sample4k_maf", "sample4k_iaf"])
+                             "sample4k_spline", "sample4k_maf", "sample4k_iaf", "sample4k_fused",
+                             "sample4k_spline_fused"])
     ap.add_argument("--batch", type=int, default=None,
                     help="global batch (default: the BASELINE batch, 1M; 4M cfg4; 512Ki cfg5f; 8Ki cfg5i)")
     ap.add_argument("--no-cpu", action="store_true")
