@@ -248,8 +248,9 @@ def reconcile(cdir, rtag):
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     shutil.copy(ks_path, os.path.join(ROOT, "profiles", f"{rtag}_{name}_kernel_stats.csv"))
-    # the file bench.py quotes for this config (full-batch runs only)
-    if name in HOT or name == cfg and name in HOT:
+    # the file bench.py quotes for this config (profiles/rocprof_<cfg>[_<batch>].json: a shard run
+    # with --batch B quotes rocprof_<cfg>_<B>.json)
+    if cfg in HOT:
         with open(os.path.join(ROOT, "profiles", f"rocprof_{name}.json"), "w") as fh:
             json.dump(res, fh, indent=1)
     return res
