@@ -692,7 +692,13 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                             "clock_ghz": rj.get("clock_ghz"), "valu_insts_per_mfma": rj.get("valu_insts_per_mfma"),
                             "busy_cycles_per_mfma": rj["pmc_mfma"].get("busy_cycles_per_mfma"),
                             "valu_issue_frac": rj.get("valu_issue_frac"),
-                            "identity": rj.get("mfma_identity")})
+                            "pmc_pass_mean_launch_us": rj["pmc_mfma"].get("mean_duration_us"),
+                            "identity": rj.get("mfma_identity"),
+                            "busy_note": ("busy and clock come from the counter pass, whose dispatches run a little "
+                                          "slower than the trace pass and this run (pmc_pass_mean_launch_us vs "
+                                          "mean_launch_us); within that pass frac = busy x clock / 2.4 GHz x "
+                                          "algorithmic/issued exactly (identity.rebuilt_frac = "
+                                          "identity.frac_pmc_pass), so busy >= frac at any clock <= 2.4 GHz")})
     result = {
         "metric": METRIC,
         "value": B_global * a.steps / t_max,

@@ -35,8 +35,8 @@ extern "C" {
 
 /* ABI 3: the log_prob workspace (nfx_gauss_workspace_bytes) may hold anything on entry — the
  * fused epilogues' last workgroup finishes the float64 sums in the same launch, and its arrival
- * word is tagged per launch, so garbage or a count left by an aborted launch is discarded (ABI 2
- * required a zero-filled workspace); nfx_made_affine_backward / nfx_made_seq_backward / nfx_made_backward_weights
+ * word carries a fixed tag: a word without it (garbage, a fill, zeros, another allocation's data)
+ * is claimed once instead of added to (ABI 2 required a zero-filled workspace); nfx_made_affine_backward / nfx_made_seq_backward / nfx_made_backward_weights
  * return NFX_EUNSUPPORTED above nfx_made_backward_max_batch(d, H) (callers split the batch). */
 #define NFX_ABI_VERSION 3
 
