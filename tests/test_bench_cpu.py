@@ -40,18 +40,19 @@ def _bench(env_extra, *args, timeout=180):
                           text=True, timeout=timeout)
 
 
-def test_gpus_flag_launches_ranks():
-    """`bench.py --gpus 2` with no launcher around it starts 2 ranks itself and they join one
+@pytest.mark.parametrize("n", [2, 4])
+def test_gpus_flag_launches_ranks(n):
+    """`bench.py --gpus N` with no launcher around it starts N ranks itself and they join one
     process group (NFX_BENCH_LAUNCH_CHECK: gloo, no GPU call); rank 0's line is relayed."""
     import json
-    r = _bench({"NFX_BENCH_LAUNCH_CHECK": "1"}, "--gpus", "2")
+    r = _bench({"NFX_BENCH_LAUNCH_CHECK": "1"}, "--gpus", str(n))
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["launch_check"] and line["world_size"] == 2
-    assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
-    assert [x["local_rank"] for x in sorted(line["ranks"], key=lambda x: x["rank"])] == [0, 1]
-    assert len({x["pid"] for x in line["ranks"]}) == 2
-    assert "2 child ranks" in line["launcher"]
+    assert line["launch_check"] and line["world_size"] == n
+    assert sorted(x["rank"] for x in line["ranks"]) == list(range(n))
+    assert [x["local_rank"] for x in sorted(line["ranks"], key=lambda x: x["rank"])] == list(range(n))
+    assert len({x["pid"] for x in line["ranks"]}) == n
+    assert f"{n} child ranks" in line["launcher"]
 
 
 def test_gpus_flag_rank_failure_fails_the_run():
