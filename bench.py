@@ -690,6 +690,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
             # frac = busy x clock / 2.4 GHz x (algorithmic / issued MFMA flop)
             rocprof.update({"mfma_busy_frac": rj["mfma_busy_frac"], "mfma_issue_frac": rj.get("mfma_issue_frac"),
                             "clock_ghz": rj.get("clock_ghz"), "valu_insts_per_mfma": rj.get("valu_insts_per_mfma"),
+                            "non_mfma_valu_per_mfma": rj.get("non_mfma_valu_per_mfma"),
                             "busy_cycles_per_mfma": rj["pmc_mfma"].get("busy_cycles_per_mfma"),
                             "valu_issue_frac": rj.get("valu_issue_frac"),
                             "pmc_pass_mean_launch_us": rj["pmc_mfma"].get("mean_duration_us"),

@@ -124,9 +124,11 @@ def mfma_busy(counter_csv, trace_csv, hot):
            "mfma_busy_frac": busy / (N_SIMD * cyc) if cyc else None,
            "mfma_issue_frac": imfma * MFMA_F32_CYCLES / (N_SIMD * cyc) if cyc else None,
            "valu_insts_per_mfma": ivalu / imfma if imfma else None,
+           # SQ_INSTS_VALU counts the MFMAs themselves too: the other vector instructions per MFMA
+           "non_mfma_valu_per_mfma": (ivalu - imfma) / imfma if imfma else None,
            # VALU issue slots used, at 4 cycles per wave instruction (8 for transcendentals: a
            # lower bound) — the pipe of the kernels that issue no MFMA (cfg5i)
-           "valu_issue_frac": ivalu * 4 / (N_SIMD * cyc) if cyc else None}
+           "valu_issue_frac": (ivalu - imfma) * 4 / (N_SIMD * cyc) if cyc else None}
     ds = [d for _, d in rows if d]
     if ds:
         mean_ns = sum(ds) / len(ds)
