@@ -355,19 +355,26 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
         return check_launch("made_wide_kernel");  // (LOGP: the last workgroup wrote sums)
     }
     if ((variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) && d <= kTileMaxD) {
+        const int64_t ntiles = (B + 31) / 32;
+        // 8 waves per workgroup (two per SIMD) while the batch fills the chip. Below that (no
+        // fused log_prob) as few waves per workgroup as spread the tiles one wave per SIMD, the
+        // weights read through L2 rather than staged per workgroup: 6x IAF(2, 64) sampling at
+        // n = 4,000 112 -> 73 us; staging the weights per workgroup measured no better at d = 63
+        // (profiles/r06_tile/)
+        int nw = 8;
+        if (!fused && ntiles < 4 * (int64_t)num_cus()) nw = (int)((ntiles + num_cus() - 1) / num_cus());
         const size_t wbytes = (size_t)L.par_total * sizeof(float);
-        const size_t tiles8 = 8 * 32 * (size_t)kTileStride * sizeof(float);
-        const bool wlds = wbytes + tiles8 <= kLdsBytes;
+        const size_t tiles = nw * 32 * (size_t)kTileStride * sizeof(float);
+        const bool wlds = nw == 8 && wbytes + tiles <= kLdsBytes;
         made_par_kernel_t k = pick_tile(HT, wlds, variant, fused);
         if (!k) return set_error(NFX_EUNSUPPORTED, "made_affine: no kernel for H=%d", H);
-        const size_t lds = (wlds ? wbytes : 0) + tiles8;
+        const size_t lds = (wlds ? wbytes : 0) + tiles;
         int rc = prepare_lds((const void*)k, lds);
         if (rc) return rc;
-        const int64_t ntiles = (B + 31) / 32;
-        int grid = resident_grid((const void*)k, 512, lds, (ntiles + 7) / 8);
+        int grid = resident_grid((const void*)k, 64 * nw, lds, (ntiles + nw - 1) / nw);
         if (grid > kMaxPartials) grid = kMaxPartials;
-        k<<<grid, 512, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials, sums,
-                                 gauss_const(d));
+        k<<<grid, 64 * nw, lds, s>>>(packed, in, out, log_det, B, d, accumulate, ntiles, logp, partials, sums,
+                                     gauss_const(d));
         return check_launch("made_tile_kernel");
     }
     if (variant == NFX_MAF_INVERSE || variant == NFX_IAF_FORWARD) {
@@ -393,8 +400,10 @@ static int made_launch(const float* packed, const float* in, float* out, float* 
     const int seq_pol = made_seq_policy().load(std::memory_order_relaxed);
     // AUTO: the push kernel while it leads (IAF(784, 64) + log_prob: 31.9 vs 53.5 / 92.7 us at 1,024,
     // 82.7 vs 137.5 / 94.9 us at 4,096 for the wave / segment kernels; the segment kernel from
-    // 8,192, gpurun_out/r05a/sweep.jsonl)
-    const bool push_auto = seq_pol == NFX_MADE_SEQ_AUTO && B <= 4096 * (int64_t)num_cus() / 256;
+    // 8,192, gpurun_out/r05a/sweep.jsonl) — for d > 32 only: at d <= 32 it trails the wave and
+    // segment kernels at every batch up to 4,000 (MAF(32, 64) at 1,024: 48.4 vs 35.6 / 52.6 us;
+    // MAF(2, 64) at 4,000: 39.6 vs 36.1 / 30.2 us, profiles/r06_tile/seq.jsonl)
+    const bool push_auto = seq_pol == NFX_MADE_SEQ_AUTO && d > 32 && B <= 4096 * (int64_t)num_cus() / 256;
     if (seqs && (seq_pol == NFX_MADE_SEQ_PUSH || push_auto) && L.ps > 0)
         return made_seqp_launch(packed, in, out, log_det, B, d, H, variant, accumulate, logp, partials, sums, fused, s);
     if (seqs && (seq_pol == NFX_MADE_SEQ_PUSH || seq_pol == NFX_MADE_SEQ_WAVE || (seq_pol == NFX_MADE_SEQ_AUTO && B <= 2048 * (int64_t)num_cus() / 256))) {

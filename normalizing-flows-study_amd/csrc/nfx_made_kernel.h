@@ -616,14 +616,16 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
     extern __shared__ f32x4 lds4[];
     float* lds = reinterpret_cast<float*>(lds4);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // waves per workgroup: 8, or fewer (no fused log_prob) to spread a small batch over more CUs
+    const int nwg = LOGP ? 8 : (int)(blockDim.x >> 6);
     if constexpr (WLDS) {
         const f32x4* src = reinterpret_cast<const f32x4*>(packed);
-        for (int i = threadIdx.x; i < L.par_total / 4; i += 512) lds4[i] = src[i];
+        for (int i = threadIdx.x; i < L.par_total / 4; i += 64 * nwg) lds4[i] = src[i];
     }
     float* xt = lds + (WLDS ? L.par_total : 0) + wave * 32 * S;
     if constexpr (WLDS) __syncthreads();
     const int lane = lane_id(), h = lane >> 5, col = lane & 31;
-    const int64_t nwaves = (int64_t)gridDim.x * 8;
+    const int64_t nwaves = (int64_t)gridDim.x * nwg;
     // Rows move through raw buffer loads/stores: the per-tile descriptor's range check returns 0
     // for (and drops stores to) lanes >= d and rows >= B, so no per-row branches or 64-bit
     // address arithmetic; the row offset r*d*4 rides in the scalar soffset.
@@ -643,7 +645,7 @@ __global__ __launch_bounds__(512) void made_tile_kernel(
     }
     const float tsafe = packed[L.tsafe];
 
-    int64_t t = (int64_t)blockIdx.x * 8 + wave;
+    int64_t t = (int64_t)blockIdx.x * nwg + wave;
     double lpacc = 0.0;
     float pf[32];
     float ldpf = 0.f;  // incoming log-det of the lane's sample (accumulate), prefetched too

@@ -281,3 +281,26 @@ def test_made_block_skip_bit_identical(cuda_device, d, H):
         keep = torch.ones(96, dtype=torch.bool, device=cuda_device)
         keep[37] = False
         assert torch.equal(y[keep], yd[keep]) and torch.equal(ld[keep], ldd[keep])
+
+
+@pytest.mark.parametrize("d,H", [(2, 64), (63, 64), (17, 128)])
+def test_made_tile_spread_launch_bit_identical(cuda_device, d, H):
+    """Below 4 tiles per CU the parallel direction launches the tile kernel with 1-3 waves per
+    workgroup and the weights read through L2 instead of 8-wave workgroups staging them in LDS
+    (csrc/nfx_made.hip, round 6): the per-tile arithmetic is the same, so rows computed in a
+    small batch equal the same rows inside a full-size batch bit for bit (ragged tails too)."""
+    torch.manual_seed(d * 7 + H)
+    big = 4 * 256 * 32 + 77  # at least 4 tiles per CU on a 256-CU part: the 8-wave launch
+    for cls in (nfs_amd.MaskedAutoregressiveFlow, nfs_amd.InverseAutoregressiveFlow):
+        f = cls(d, H)
+        with torch.no_grad():
+            for p in f.parameters():
+                p.add_(0.1 * torch.randn_like(p))
+        f = f.to(cuda_device).eval()
+        fwd = f.forward if cls is nfs_amd.InverseAutoregressiveFlow else f.inverse
+        x = torch.randn(big, d, device=cuda_device)
+        with torch.no_grad():
+            yb, ldb = fwd(x)
+            for B in (1, 31, 33, 4000, 20000):
+                y, ld = fwd(x[:B].contiguous())
+                assert torch.equal(y, yb[:B]) and torch.equal(ld, ldb[:B]), (cls.__name__, B)
