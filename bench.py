@@ -52,6 +52,12 @@ sys.path.insert(0, ROOT)
 import nfs_amd  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2516.6  # MI355X dense BF16 MFMA: 256 CUs x 4 SIMDs x 1024 flop/clk x 2.4 GHz
+# The streaming affine kernels (cfg2) run layer 2 of each conditioner net as six bf16 piece
+# products per fp32 multiply-add (csrc/nfx_affine_kernel.h, affine_net_split): the ceiling of
+# that scheme, in the fp32 flops the layer computes, is the bf16 peak / 6.
+PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
+SPLIT_CONFIGS = ("cfg2",)
 METRIC = "log_prob samples/sec/GPU + test-NLL match; RealNVP d=2 and MAF d=63"
 
 
@@ -700,6 +706,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
                                           "mean_launch_us); within that pass frac = busy x clock / 2.4 GHz x "
                                           "algorithmic/issued exactly (identity.rebuilt_frac = "
                                           "identity.frac_pmc_pass), so busy >= frac at any clock <= 2.4 GHz")})
+    peak = PEAK_SPLIT_TFLOPS if config in SPLIT_CONFIGS else PEAK_FP32_TFLOPS
     result = {
         "metric": METRIC,
         "value": B_global * a.steps / t_max,
@@ -727,7 +734,7 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         # fp32 VALU rate, whose peak (packed FMA) equals the fp32 MFMA peak, 157.3 TFLOP/s
         "roofline": {"bound": "valu" if config == "cfg5i" else "mfma", "pipe": "valu" if config == "cfg5i" else "mfma",
                      "kernel": kname, "achieved": achieved,
-                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS,
+                     "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                      "traffic": traffic, "flop_per_sample_per_launch": f_launch,
                      "layers_per_launch": layers_per_launch,
                      "samples_per_launch": B, "mean_launch_ms": mean_ms, "launches": len(durs),
@@ -743,6 +750,13 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         # (kernels run a little slower under rocprofv3 than unprofiled: the ratio says how much)
         rocprof["kernel_ms_over_this_step"] = rocprof["kernel_ms_per_step"] / result["ms_per_step"]
         rocprof["frac_rel_diff_vs_events"] = abs(rocprof["frac"] - result["roofline"]["frac"]) / result["roofline"]["frac"]
+    if config in SPLIT_CONFIGS:
+        result["roofline"].update({
+            "peak_basis": ("bf16 MFMA peak / 6: layer 2 of every conditioner net runs as six bf16 piece products "
+                           "per fp32 multiply-add (v_mfma_f32_32x32x16_bf16, fp32 accumulate; fp32-accurate, not the "
+                           "fp32 chain's bits); achieved counts the fp32 flops of the reference's arithmetic"),
+            "frac_of_fp32_peak": achieved / PEAK_FP32_TFLOPS, "peak_fp32": PEAK_FP32_TFLOPS,
+            "peak_bf16": PEAK_BF16_TFLOPS})
     if config == "cfg4":
         fe = made_executed_flop_per_sample(63, 64)
         ach_e = fe * B / (mean_ms * 1e-3) / 1e12

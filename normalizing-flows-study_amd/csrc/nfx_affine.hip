@@ -33,7 +33,7 @@ __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float
                                    int H, float* packed) {
     const int HT = (H + 31) / 32;
     const AffineLayout L = affine_layout(d, HT);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.total; i += gridDim.x * blockDim.x) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < L.s; i += gridDim.x * blockDim.x) {
         float v = 0.f;
         if (i >= L.mask) {
             int j = i - L.mask;
@@ -79,6 +79,104 @@ __global__ void affine_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const float
         }
         packed[i] = v;
     }
+}
+
+// The split tail of an affine image (affine_split, nfx_affine_kernel.h), derived from the fp32
+// image written before it on the same stream: copies of w1 b1 b2 w3 b3 and the mask, W2's three
+// round-to-nearest bf16 pieces in v_mfma_f32_32x32x16_bf16 A-operand order, and the safety words (W2 finite
+// and |w| <= 1e6; xsafe = (1e30 - max|b1|) / max_row sum|w1|). One workgroup: the two maxima
+// are reductions and the tail is ~14k floats.
+__global__ __launch_bounds__(1024) void affine_split_pack_kernel(float* packed, int d, int H) {
+    const int HT = (H + 31) / 32, KS1 = (d + 1) / 2;
+    const AffineLayout L = affine_layout(d, HT);
+    const AffineSplit S = affine_split(d, HT);
+    float* out = packed + L.s;
+    __shared__ int w2_bad;
+    __shared__ float rowsum[2 * 64], bmax[2 * 64];
+    if (threadIdx.x == 0) w2_bad = 0;
+    __syncthreads();
+    bool bad = false;
+    for (int i = threadIdx.x; i < S.total; i += blockDim.x) {
+        const int net = i < S.mask ? i / S.net : 0;
+        const int o = i - net * S.net;
+        const float* P = packed + net * L.net;
+        uint32_t v = 0;
+        if (i >= S.ok) {
+            continue;  // the safety words: below, after the reductions
+        } else if (i >= S.mask) {
+            v = __float_as_uint(packed[L.mask + (i - S.mask)]);
+        } else if (o < S.b1) {
+            v = __float_as_uint(P[L.w1 + (o - S.w1)]);
+        } else if (o < S.b2) {
+            v = __float_as_uint(P[L.b1 + (o - S.b1)]);
+        } else if (o < S.w3) {
+            v = __float_as_uint(P[L.b2 + (o - S.b2)]);
+        } else if (o < S.b3) {
+            v = __float_as_uint(P[L.w3 + (o - S.w3)]);
+        } else if (o < S.w2s) {
+            v = __float_as_uint(P[L.b3 + (o - S.b3)]);
+        } else {
+            // dword t: [out tile hto][k block kb][piece p][lane][q], elements 2q, 2q + 1
+            const int t = o - S.w2s, q = t & 3, lane = (t >> 2) & 63, g = t >> 8;
+            const int p = g % 3, kb = (g / 3) % (2 * HT), hto = (g / 3) / (2 * HT);
+            const int kt = kb >> 1;
+            uint32_t half[2];
+            for (int e = 0; e < 2; ++e) {
+                const int r = 8 * (kb & 1) + 2 * q + e;  // accumulator register of the B operand
+                const float w = P[L.w2 + ((hto * HT + kt) * 4 + (r >> 2)) * 256 + lane * 4 + (r & 3)];
+                if (!(fabsf(w) <= 1e6f)) bad = true;
+                // round-to-nearest pieces (random signs: unbiased dropped products, split_block)
+                const uint32_t u0 = __builtin_bit_cast(uint16_t, (__bf16)w);
+                const float r1 = w - __uint_as_float(u0 << 16);
+                const uint32_t u1 = __builtin_bit_cast(uint16_t, (__bf16)r1);
+                const uint32_t u2 = __builtin_bit_cast(uint16_t, (__bf16)(r1 - __uint_as_float(u1 << 16)));
+                half[e] = p == 0 ? u0 : p == 1 ? u1 : u2;
+            }
+            v = half[0] | (half[1] << 16);
+        }
+        out[i] = __uint_as_float(v);
+    }
+    if (bad) atomicOr(&w2_bad, 1);
+    // layer-1 bound: row sums of |w1| (rows 32 ht + c of net n) and |b1|
+    for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) {
+        rowsum[i] = 0.f;
+        bmax[i] = 0.f;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * 32 * HT) {
+        const int net = threadIdx.x / (32 * HT), row = threadIdx.x % (32 * HT), ht = row >> 5, c = row & 31;
+        const float* P = packed + net * L.net;
+        float sum = 0.f;
+        for (int ks = 0; ks < KS1; ++ks)
+            for (int hh = 0; hh < 2; ++hh) sum += fabsf(P[L.w1 + (ht * KS1 + ks) * 64 + c + 32 * hh]);
+        rowsum[net * 64 + row] = sum;
+        float b = 0.f;
+        for (int r = 0; r < 16; ++r)
+            for (int hh = 0; hh < 2; ++hh)
+                if (crow(r, hh) == c) b = fabsf(P[L.b1 + ht * 32 + 16 * hh + r]);
+        bmax[net * 64 + row] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float n1 = 0.f, c1 = 0.f;
+        bool nan = false;
+        for (int i = 0; i < 2 * 64; ++i) {
+            nan = nan || !(rowsum[i] <= 3e38f) || !(bmax[i] <= 3e38f);
+            n1 = fmaxf(n1, rowsum[i]);
+            c1 = fmaxf(c1, bmax[i]);
+        }
+        const float xs = nan ? 0.f : (1e30f - c1) / n1;  // n1 == 0: +inf (no x reaches layer 1)
+        out[S.ok] = w2_bad ? 0.f : 1.f;
+        out[S.ok + 1] = xs > 0.f ? xs : 0.f;
+        out[S.ok + 2] = 0.f;
+        out[S.ok + 3] = 0.f;
+    }
+}
+
+int affine_split_pack(float* packed, int d, int H, hipStream_t s) {
+    if (!affine_has_split(d, (H + 31) / 32)) return NFX_OK;
+    affine_split_pack_kernel<<<1, 1024, 0, s>>>(packed, d, H);
+    return check_launch("affine_split_pack_kernel");
 }
 
 static affine_kernel_t pick_affine(int HT, int d, int dir, bool logp) {
@@ -164,7 +262,8 @@ static int affine_launch(const float* packed, const float* in, float* out, float
     if (B == 0) return fused ? gauss_finish(reinterpret_cast<double*>(workspace), 0, sums, 0, stream) : NFX_OK;
     if (!packed || !in || !out || !log_det) return set_error(NFX_EINVAL, "affine_coupling: null pointer");
     if (in == out) return set_error(NFX_EINVAL, "affine_coupling: in and out must not alias");
-    const size_t lds = (size_t)affine_layout(d, HT).total * sizeof(float);
+    const AffineLayout L = affine_layout(d, HT);
+    const size_t lds = (size_t)(affine_has_split(d, HT) ? affine_split(d, HT).total : L.total) * sizeof(float);
     int rc = prepare_lds((const void*)k, lds);
     if (rc) return rc;
     double* partials = reinterpret_cast<double*>(workspace);
@@ -241,7 +340,8 @@ extern "C" int nfx_affine_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_net, c
     int blocks = (total + 255) / 256;
     if (blocks > 1024) blocks = 1024;
     affine_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*s_net, *b_net, mask, d, H, packed);
-    return check_launch("affine_pack_kernel");
+    const int rc = check_launch("affine_pack_kernel");
+    return rc ? rc : affine_split_pack(packed, d, H, (hipStream_t)stream);
 }
 
 extern "C" int nfx_affine_coupling(const float* packed, const float* in, float* out, float* log_det,

@@ -21,7 +21,38 @@ __host__ __device__ constexpr int up4(int v) { return (v + 3) & ~3; }
 struct AffineLayout {
     int d, HT, KS1;
     int w1, b1, w2, b2, w3, b3, net, mask, total;
+    int s;  // base of the split tail (affine_split), == the fp32 image's end
 };
+
+// Split tail (d <= 8, H <= 64), appended to the image and derived from it on device
+// (nfx_affine_split_pack): what affine_net_split reads, contiguous so that a kernel stages only
+// this region into LDS. Per net: w1 b1 b2 w3 b3 (copies, the fp32 formats above) and W2 as three
+// bf16 pieces W2 ~ W2_0 + W2_1 + W2_2 (round-to-nearest split, split_block) in v_mfma_f32_32x32x16_bf16
+// A-operand order [out tile][k block][piece][lane][4 dwords]; then the mask and two safety words:
+// ok[0] = 1 when every W2 entry is finite with |w| <= 1e6, ok[1] = xsafe, the largest |x * m|
+// for which every layer-1 activation stays <= 1e30 (so no bf16 piece product or layer-2 partial
+// sum can overflow).
+struct AffineSplit {
+    int w1, b1, b2, w3, b3, w2s, net, mask, ok, total;
+};
+
+__host__ __device__ constexpr AffineSplit affine_split(int d, int HT) {
+    AffineSplit S{};
+    int o = 0;
+    S.w1 = o; o += HT * ((d + 1) / 2) * 64;
+    S.b1 = o; o += HT * 32;
+    S.b2 = o; o += HT * 32;
+    S.w3 = o; o += d * HT * 32;
+    S.b3 = o; o += up4(d);
+    S.w2s = o; o += HT * 2 * HT * 768;
+    S.net = o;
+    S.mask = 2 * o;
+    S.ok = S.mask + up4(d);
+    S.total = S.ok + 4;
+    return S;
+}
+
+__host__ __device__ constexpr bool affine_has_split(int d, int HT) { return d <= 8 && HT <= 2; }
 
 __host__ __device__ constexpr AffineLayout affine_layout(int d, int HT) {
     AffineLayout L{};
@@ -44,6 +75,8 @@ __host__ __device__ constexpr AffineLayout affine_layout(int d, int HT) {
     L.net = o;
     L.mask = 2 * o;
     L.total = 2 * o + up4(d);
+    L.s = L.total;
+    if (affine_has_split(d, HT)) L.total += affine_split(d, HT).total;
     return L;
 }
 
@@ -142,6 +175,177 @@ __device__ __forceinline__ void affine_net(const float* __restrict__ P, const Af
         res[j] = tclamp(halves_sum(part[j][0], part[j][1]) + P[L.b3 + j], -10.f, 10.f);
 }
 
+// ---- layer 2 as bf16x3-split MFMAs (H <= 64, d <= 8; round 6) ----------------------------------
+// fp32 has no fast matrix path on gfx950 (v_mfma_f32_32x32x2_f32 runs at 1/16 of the bf16 rate).
+// Layer 2 (H x H, 97 % of the conditioner's flops) instead splits both operands into three bf16
+// pieces and sums the six products a_i * w_j with i + j <= 2 on v_mfma_f32_32x32x16_bf16 (fp32
+// accumulate; every piece product is exact in fp32). Activations split exactly by truncation
+// (a0 = top 8 significant bits, a1 the next 8, a2 the rest: |a1| <= 2^-8 |a|, |a2| <= 2^-16 |a|),
+// weights by round-to-nearest at pack time (|w1| <= 2^-9 |w|, |w2| <= 2^-18 |w|, random signs),
+// so the dropped a1w2, a2w1, a2w2 are unbiased and below 2^-25 of the term: the layer keeps fp32
+// accuracy (not the fp32 chain's bits; all-truncation pieces measured a systematic NLL shift of
+// 4e-8, this split 1e-9, profiles/r06_split/). Six 32-cycle
+// MFMAs replace the eight 64-cycle fp32 MFMAs of a 16-deep k block, and the splitting VALU issues
+// in their shadow. A 32-row sample tile whose masked input fails |x * m| <= xsafe (non-finite or
+// huge), or a layer whose W2 is not finite / exceeds 1e6, runs the fp32 chain instead, so
+// non-finite rows keep the reference's inf / NaN propagation; the decision is per 32-row tile
+// (32-aligned in every kernel), so a row's bits depend only on its own tile.
+#ifndef NFX_SPLIT_TERMS
+#define NFX_SPLIT_TERMS 6  // piece products per k block (8: + w1 x2, w2 x1)
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                    0, 0, 0);
+}
+
+// The three pieces (fp32 bit patterns, zero low halves) of a finite activation x, by truncation:
+// x0 keeps x's top 8 significant bits, x1 the next 8 of the exact remainder, x2 the rest (exact).
+__device__ __forceinline__ void split3(float x, uint32_t& u0, uint32_t& u1, uint32_t& u2) {
+    u0 = __float_as_uint(x) & 0xffff0000u;
+    const float r1 = x - __uint_as_float(u0);
+    u1 = __float_as_uint(r1) & 0xffff0000u;
+    u2 = __float_as_uint(r1 - __uint_as_float(u1));
+}
+
+// bf16x2 word: element lo in bits 0..15, hi in 16..31 (the high halves of the two patterns).
+__device__ __forceinline__ uint32_t pack_bf16(uint32_t lo, uint32_t hi) {
+    return __builtin_amdgcn_perm(hi, lo, 0x07060302u);
+}
+
+// B-operand pieces of k block kb of an activation tile: the lane's registers 8 (kb & 1) + j,
+// j = 0..7 (hidden units 32 (kb >> 1) + crow(8 (kb & 1) + j, h); the pack orders W2's k to match).
+__device__ __forceinline__ void split_block(const f32x16& a, int half, u32x4 (&xp)[3]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t l0, l1, l2, h0, h1, h2;
+        split3(a[8 * half + 2 * q], l0, l1, l2);
+        split3(a[8 * half + 2 * q + 1], h0, h1, h2);
+        xp[0][q] = pack_bf16(l0, h0);
+        xp[1][q] = pack_bf16(l1, h1);
+        xp[2][q] = pack_bf16(l2, h2);
+    }
+}
+
+// Conditioner MLP of one net on the split tail S (LDS) for a 64-sample chunk (TILES = 2) or a
+// 32-sample half chunk. Returns clamp(net(x*m), -10, 10)[j] for the lane's sample, as affine_net.
+template <int HT, int D, int TILES = 2>
+__device__ __forceinline__ void affine_net_split(const float* __restrict__ S, const AffineSplit& SL,
+                                                 const float (&xb)[2][(D + 1) / 2], float (&res)[D]) {
+    constexpr int KS1 = (D + 1) / 2;
+    const int lane = lane_id(), h = lane >> 5;
+
+    f32x16 h1[HT][2];
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) {
+        f32x16 a0, a1;
+        load_bias16_x2(S + SL.b1 + ht * 32, h, a0, a1);
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) {
+            const float w = S[SL.w1 + (ht * KS1 + ks) * 64 + lane];
+            a0 = mfma32(w, xb[0][ks], a0);
+            if constexpr (TILES == 2) a1 = mfma32(w, xb[1][ks], a1);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            a0[r] = trelu(a0[r]);
+            if constexpr (TILES == 2) a1[r] = trelu(a1[r]);
+        }
+        h1[ht][0] = a0;
+        h1[ht][1] = a1;
+    }
+
+    float part[D][2];
+#pragma unroll
+    for (int j = 0; j < D; ++j) part[j][0] = part[j][1] = 0.f;
+    auto fold = [&](int hto, const f32x16& a, int st) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const f32x16 w3 = load_bias16(S + SL.w3 + (j * HT + hto) * 32, h);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) part[j][st] = fmaf(w3[r], trelu(a[r]), part[j][st]);
+        }
+    };
+    const u32x4* w2s = reinterpret_cast<const u32x4*>(S + SL.w2s) + lane;
+    // sample tile outer: the tile's activations are split once (h1 of the tile dies), then per
+    // output tile the k blocks accumulate the big product w0 x0 into hi (bias-initialised) and
+    // the small ones into lo, added once at the end: the running sum takes only 2 HT MFMA
+    // roundings instead of 6 per k block
+#pragma unroll
+    for (int st = 0; st < TILES; ++st) {
+        u32x4 xp[2 * HT][3];
+#pragma unroll
+        for (int kb = 0; kb < 2 * HT; ++kb) split_block(h1[kb >> 1][st], kb & 1, xp[kb]);
+        const u32x4* w2 = w2s + opaque_zero();  // re-read per tile: no 96-VGPR cache of W2
+#pragma unroll
+        for (int hto = 0; hto < HT; ++hto) {
+            f32x16 hi = load_bias16(S + SL.b2 + hto * 32 + opaque_zero(), h), lo = {};
+#pragma unroll
+            for (int kb = 0; kb < 2 * HT; ++kb) {
+                const int g = (hto * 2 * HT + kb) * 3;
+                const u32x4 w[3] = {w2[g * 64], w2[(g + 1) * 64], w2[(g + 2) * 64]};
+#if NFX_SPLIT_TERMS == 8
+                lo = mfma_bf16(w[2], xp[kb][1], lo);
+                lo = mfma_bf16(w[1], xp[kb][2], lo);
+#endif
+                lo = mfma_bf16(w[2], xp[kb][0], lo);
+                lo = mfma_bf16(w[1], xp[kb][1], lo);
+                lo = mfma_bf16(w[0], xp[kb][2], lo);
+                lo = mfma_bf16(w[1], xp[kb][0], lo);
+                lo = mfma_bf16(w[0], xp[kb][1], lo);
+                hi = mfma_bf16(w[0], xp[kb][0], hi);
+            }
+            fold(hto, hi + lo, st);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        res[j] = tclamp(halves_sum(part[j][0], part[j][1]) + S[SL.b3 + j], -10.f, 10.f);
+}
+
+// Both conditioner nets of a unit: the split nets from the staged tail S, and — only when a
+// 32-row sample tile has a masked input beyond xsafe (non-finite or huge; NaN fails the test) or
+// the layer's W2 is unsafe — the fp32 nets (affine_net) from the layer's fp32 image Pg in global
+// memory, whose results replace the split ones on that tile's lanes (lane l holds sample
+// ub + l: tile l >> 5). The choice is per 32-aligned tile, so a row's bits never depend on
+// rows outside its tile.
+template <int HT, int D, int TILES>
+__device__ __forceinline__ void affine_nets_split(const float* __restrict__ S, const AffineSplit& SL,
+                                                  const float* __restrict__ Pg, const AffineLayout& L,
+                                                  const float (&xb)[2][(D + 1) / 2], float (&sv)[D], float (&bv)[D]) {
+    constexpr int KS1 = (D + 1) / 2;
+    const bool wok = S[SL.ok] != 0.f;
+    const float xs = S[SL.ok + 1];
+    bool fast[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+        bool bad = false;
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) bad = bad || !(fabsf(xb[st][ks]) <= xs);
+        fast[st] = wok && __builtin_amdgcn_ballot_w64(bad) == 0;
+    }
+    affine_net_split<HT, D, TILES>(S, SL, xb, sv);
+    __builtin_amdgcn_sched_barrier(0);  // one net's activations live at a time
+    affine_net_split<HT, D, TILES>(S + SL.net, SL, xb, bv);
+    if (!(fast[0] && (TILES == 1 || fast[1]))) {
+        __builtin_amdgcn_sched_barrier(0);
+        const float* P = Pg + opaque_zero();  // (no hoisted global addresses for this rare path)
+        float s2[D], b2[D];
+        affine_net<HT, D, TILES>(P, L, xb, s2);
+        __builtin_amdgcn_sched_barrier(0);
+        affine_net<HT, D, TILES>(P + L.net, L, xb, b2);
+        if (!fast[lane_id() >> 5]) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                sv[j] = s2[j];
+                bv[j] = b2[j];
+            }
+        }
+    }
+}
+
 // LOGP: fused log_prob epilogue for the last layer of an inverse chain — logp = -0.5*(c +
 // sum_j z_j^2) + total log-det per sample, and one float64 partial sum per workgroup.
 template <int HT, int D, int DIR, bool LOGP>
@@ -151,10 +355,14 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
     float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
     constexpr int KS1 = L.KS1;
+    // H <= 64: only the split tail is staged (layer 2 on the split bf16 MFMAs, affine_net_split)
+    constexpr bool SPLIT = affine_has_split(D, HT);
+    constexpr AffineSplit SL = affine_split(D, HT);
+    constexpr int MASK = SPLIT ? SL.mask : L.mask;
     extern __shared__ f32x4 lds4[];
     {
-        const f32x4* src = reinterpret_cast<const f32x4*>(packed);
-        for (int i = threadIdx.x; i < L.total / 4; i += 256) lds4[i] = src[i];
+        const f32x4* src = reinterpret_cast<const f32x4*>(packed + (SPLIT ? L.s : 0));
+        for (int i = threadIdx.x; i < (SPLIT ? SL.total : L.total) / 4; i += 256) lds4[i] = src[i];
     }
     __syncthreads();
     const float* sm = reinterpret_cast<const float*>(lds4);
@@ -163,9 +371,9 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
     const int64_t nwaves = (int64_t)gridDim.x * 4;
     float mk[D], mkb[KS1];
 #pragma unroll
-    for (int j = 0; j < D; ++j) mk[j] = sm[L.mask + j];
+    for (int j = 0; j < D; ++j) mk[j] = sm[MASK + j];
 #pragma unroll
-    for (int ks = 0; ks < KS1; ++ks) mkb[ks] = (2 * ks + h < D) ? sm[L.mask + 2 * ks + h] : 0.f;
+    for (int ks = 0; ks < KS1; ++ks) mkb[ks] = (2 * ks + h < D) ? sm[MASK + 2 * ks + h] : 0.f;
 
     // Work split: every wave takes F = nchunks / nwaves whole 64-sample chunks (grid-stride); the
     // R leftover chunks go out as 2R 32-sample half chunks, one to each of the first 2R waves
@@ -223,8 +431,12 @@ __global__ __launch_bounds__(256) void affine_coupling_kernel(
         }
 
         float sv[D], bv[D];
-        affine_net<HT, D, TILES>(smi, L, xb, sv);
-        affine_net<HT, D, TILES>(smi + L.net, L, xb, bv);
+        if constexpr (SPLIT) {
+            affine_nets_split<HT, D, TILES>(smi, SL, packed, L, xb, sv, bv);
+        } else {
+            affine_net<HT, D, TILES>(smi, L, xb, sv);
+            affine_net<HT, D, TILES>(smi + L.net, L, xb, bv);
+        }
 
         const int64_t so = base + lane;
         if (lane < 32 * TILES && so < B) {
@@ -422,5 +634,8 @@ typedef void (*affine_kernel_t)(const float*, const float*, float*, float*, int6
 
 template <int HT>
 affine_kernel_t affine_pick_ht(int d, int dir, bool logp);
+
+// Writes the split tail of an eval image after its fp32 part (no-op without one); same stream.
+int affine_split_pack(float* packed, int d, int H, hipStream_t s);
 
 }  // namespace nfx

@@ -23,9 +23,11 @@
 
 namespace nfx {
 
+// Staged image per layer: the split tail (affine_split; H <= 64 always has one here), padded to
+// a multiple of one 1-KiB DMA piece.
 template <int HT, int D>
 __host__ __device__ constexpr int schain_wpad() {
-    return (affine_layout(D, HT).total + 255) & ~255;  // floats; a multiple of one 1-KiB DMA piece
+    return (affine_split(D, HT).total + 255) & ~255;  // floats
 }
 
 template <int HT, int D, int DIR, bool LOGP, int NW>
@@ -34,6 +36,8 @@ __global__ __launch_bounds__(64 * NW) void affine_schain_kernel(
     float* __restrict__ logdet, int64_t B, int accumulate, int64_t nchunks, int slice_chunks,
     float* __restrict__ logp, double* __restrict__ partials, double* __restrict__ sums, float cgauss) {
     constexpr AffineLayout L = affine_layout(D, HT);
+    constexpr AffineSplit SL = affine_split(D, HT);
+    static_assert(affine_has_split(D, HT), "the streaming chain runs the split nets");
     constexpr int KS1 = L.KS1;
     constexpr int WPAD = schain_wpad<HT, D>();
     constexpr int NT = 64 * NW;
@@ -49,10 +53,10 @@ __global__ __launch_bounds__(64 * NW) void affine_schain_kernel(
 
     // DMA layer li's packed image (module order reversed for an inverse chain) into buffer buf.
     auto stage = [&](int li, int buf) {
-        const float* src = packs.p[DIR > 0 ? li : nl - 1 - li];
+        const float* src = packs.p[DIR > 0 ? li : nl - 1 - li] + L.s;
         for (int c = wave; c < WPAD / 256; c += NW) {
             int idx = c * 256 + lane * 4;
-            if (idx > L.total - 4) idx = L.total - 4;  // tail lanes re-read the last float4 into padding
+            if (idx > SL.total - 4) idx = SL.total - 4;  // tail lanes re-read the last float4 into padding
             lds_dma_x4(src + idx, wbuf_lds + (uint32_t)(buf * WPAD + c * 256) * 4u);
         }
     };
@@ -81,12 +85,13 @@ __global__ __launch_bounds__(64 * NW) void affine_schain_kernel(
             else if (s0 + slice_chunks < c1)
                 stage(0, (g + 1) & 1);
             const float* W = wbuf + (g & 1) * WPAD;
+            const float* Pg = packs.p[DIR > 0 ? li : nl - 1 - li];  // fp32 image: fallback tiles
             const bool first = li == 0 && !accumulate;
             float mk[D], mkb[KS1];
 #pragma unroll
-            for (int j = 0; j < D; ++j) mk[j] = W[L.mask + j];
+            for (int j = 0; j < D; ++j) mk[j] = W[SL.mask + j];
 #pragma unroll
-            for (int ks = 0; ks < KS1; ++ks) mkb[ks] = (2 * ks + h < D) ? W[L.mask + 2 * ks + h] : 0.f;
+            for (int ks = 0; ks < KS1; ++ks) mkb[ks] = (2 * ks + h < D) ? W[SL.mask + 2 * ks + h] : 0.f;
 
             auto unit = [&](auto tiles_c, int ub) {
                 constexpr int TILES = decltype(tiles_c)::value;
@@ -119,8 +124,7 @@ __global__ __launch_bounds__(64 * NW) void affine_schain_kernel(
                 }
                 const float* Wi = W + opaque_zero();
                 float sv[D], bv[D];
-                affine_net<HT, D, TILES>(Wi, L, xb, sv);
-                affine_net<HT, D, TILES>(Wi + L.net, L, xb, bv);
+                affine_nets_split<HT, D, TILES>(Wi, SL, Pg, L, xb, sv, bv);
                 if (act) {
 #pragma clang fp contract(off)  // separate mul/add roundings, as affine_coupling_kernel / the reference
                     float y[D];
@@ -191,7 +195,7 @@ static schain_t schain_pick(int HT, int D, int dir, bool logp) {
 }
 
 static int schain_wpad_rt(int HT, int D) {
-    return (affine_layout(D, HT).total + 255) & ~255;
+    return (affine_split(D, HT).total + 255) & ~255;
 }
 
 constexpr size_t kSchainLds = 160 * 1024;   // gfx950 LDS per CU

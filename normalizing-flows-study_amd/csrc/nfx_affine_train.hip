@@ -131,7 +131,7 @@ __global__ void affine_train_pack_kernel(NfxMlpRaw s_net, NfxMlpRaw b_net, const
     if (!epack) return;
     // eval-layout pack of the streaming kernel, BatchNorm folded with the batch statistics
     const AffineLayout E = affine_layout(d, HT);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < E.total; i += gstride) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < E.s; i += gstride) {  // (split tail: affine_split_pack)
         float v = 0.f;
         if (i >= E.mask) {
             const int j = i - E.mask;
@@ -512,7 +512,8 @@ extern "C" int nfx_affine_train_pack(const NfxMlpRaw* s_net, const NfxMlpRaw* b_
     if (blocks > 1024) blocks = 1024;
     affine_train_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(*s_net, *b_net, mask, stats1, stats2, d, D, H,
                                                                       tpack, epack);
-    return check_launch("affine_train_pack_kernel");
+    rc = check_launch("affine_train_pack_kernel");
+    return rc || !epack ? rc : affine_split_pack(epack, d, H, (hipStream_t)stream);
 }
 
 // Floats of the kept layer-2 pre-activations (nfx_affine_train_stats_keep /

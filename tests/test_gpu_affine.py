@@ -271,3 +271,61 @@ def test_streaming_half_chunk_tail_vs_oracle(cuda_device, B):
     assert_y(xf[tail].cpu(), xr)
     assert_ld(ldf[tail].cpu(), lfr)
     assert_lp(lp[tail].cpu(), lpr)
+
+
+def _policy_run(pol, fn):
+    L = nfs_amd._lib
+    f = L.lib().nfx_affine_kernel_policy
+    prev = f(pol)
+    try:
+        with torch.no_grad():
+            return fn()
+    finally:
+        f(prev)
+
+
+def test_split_mfma_layer2_accuracy_and_bias(cuda_device):
+    """The streaming kernels run layer 2 of each net as six bf16 piece products per fp32
+    multiply-add (csrc/nfx_affine_kernel.h affine_net_split, round 6). Against the fp32 chain of
+    the small-batch kernel on the G2 RealNVP at 1M rows: per element within 2e-6 (1 + |ref|)
+    (the bound two fp32 orderings meet too), and no systematic shift — the mean log p agrees to
+    2e-8 (all-truncation pieces measured 4e-8, the shipped split 5e-9; profiles/r06_split/)."""
+    m, _ = realnvp_from_golden(cuda_device)
+    x = (torch.randn(1 << 20, 2, generator=torch.Generator().manual_seed(1234)) * 1.5).to(cuda_device)
+    L = nfs_amd._lib
+    zs, lds = _policy_run(L.NFX_AFFINE_STREAMING, lambda: m.inverse(x))
+    lps = _policy_run(L.NFX_AFFINE_STREAMING, lambda: m.log_prob(x)).double()
+    zf, ldf = _policy_run(L.NFX_AFFINE_SMALL, lambda: m.inverse(x))
+    lpf = _policy_run(L.NFX_AFFINE_SMALL, lambda: m.log_prob(x)).double()
+    assert ((zs - zf).abs() <= 2e-6 * (1 + zf.abs())).all()
+    assert (lds - ldf).abs().max().item() <= 1e-5
+    assert abs((lps - lpf).mean().item()) <= 2e-8
+
+
+def test_split_mfma_fallback_is_per_tile(cuda_device):
+    """A 32-row tile holding a non-finite or huge masked input runs the fp32 nets (the reference's
+    inf / NaN propagation); the choice is per 32-aligned tile, so every other tile's rows — the
+    other tile of the same 64-row unit included — are bit-identical to a clean batch, and the
+    tile's finite rows stay within the oracle's tolerance."""
+    m, _ = realnvp_from_golden(cuda_device)
+    layer = m.flows[0]
+    B = 1 << 17
+    x = torch.randn(B, 2, generator=torch.Generator().manual_seed(7)).to(cuda_device)
+    xb = x.clone()
+    xb[40, 0] = float("inf")   # tile 1 (rows 32..63) of unit 0
+    xb[100, 1] = 3e38          # tile 3 (rows 96..127), huge but finite
+    L = nfs_amd._lib
+    for fn in (layer.forward, layer.inverse):
+        y0, l0 = _policy_run(L.NFX_AFFINE_STREAMING, lambda: fn(x))
+        y1, l1 = _policy_run(L.NFX_AFFINE_STREAMING, lambda: fn(xb))
+        keep = torch.ones(B, dtype=torch.bool, device=cuda_device)
+        keep[32:64] = False
+        keep[96:128] = False
+        assert torch.equal(y0[keep], y1[keep]) and torch.equal(l0[keep], l1[keep])
+        # the fallback tiles' clean rows: the fp32 nets, within the parity tolerance of the clean run
+        for lo, bad in ((32, 40), (96, 100)):
+            rows = [r for r in range(lo, lo + 32) if r != bad]
+            assert ((y1[rows] - y0[rows]).abs() <= 1e-5 * (1 + y0[rows].abs())).all()
+        ys, ls = _policy_run(L.NFX_AFFINE_SMALL, lambda: fn(xb))
+        assert torch.equal(torch.isnan(y1), torch.isnan(ys)) and torch.equal(torch.isinf(y1), torch.isinf(ys))
+        assert torch.equal(torch.isnan(l1), torch.isnan(ls))

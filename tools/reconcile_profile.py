@@ -203,6 +203,9 @@ def reconcile(cdir, rtag):
     f_launch = rf["flop_per_sample_per_launch"]
     spl = rf["samples_per_launch"]
     ach = f_launch * spl / (mean_us * 1e-6) / 1e12
+    # the bench line's own peak: the fp32 MFMA peak, or for the split-MFMA configs (cfg2: layer 2
+    # as six bf16 piece products per fp32 multiply-add) the bf16 peak / 6
+    peak = rf.get("peak") or PEAK
     res = {
         "config": name, "round": rtag, "lib_sha256": bench.get("lib_sha256"),
         "bench": {k: bench.get(k) for k in ("value", "ms_per_step", "steps", "warmup", "n_gpus")},
@@ -215,16 +218,16 @@ def reconcile(cdir, rtag):
         "rocprof_hot_ms_per_step": hot_ms,
         "rocprof_ms_per_step": hot_ms + extra_ms,
         "fits_bench_step": hot_ms + extra_ms <= bench["ms_per_step"],
-        "rocprof_achieved_tflops": ach, "rocprof_frac": ach / PEAK,
+        "rocprof_achieved_tflops": ach, "rocprof_frac": ach / peak, "peak_tflops": peak,
         # dense-count fracs on both sides (cfg4's headline frac is the executed one)
         "event_frac": rf.get("frac_dense", rf["frac"]),
-        "frac_rel_diff": abs(ach / PEAK - rf.get("frac_dense", rf["frac"])) / rf.get("frac_dense", rf["frac"]),
+        "frac_rel_diff": abs(ach / peak - rf.get("frac_dense", rf["frac"])) / rf.get("frac_dense", rf["frac"]),
         "source": {"kernel_stats": os.path.relpath(ks_path, ROOT),
                    "bench": os.path.relpath(os.path.join(cdir, "bench.json"), ROOT)},
     }
     if rf.get("frac_executed"):
         fe = rf["flop_per_sample_executed"]
-        res["rocprof_frac_executed"] = fe * spl / (mean_us * 1e-6) / 1e12 / PEAK
+        res["rocprof_frac_executed"] = fe * spl / (mean_us * 1e-6) / 1e12 / peak
         res["event_frac_executed"] = rf["frac_executed"]
     fetch = _newest(os.path.join(cdir, "fetch", "*", "*counter_collection.csv"))
     write = _newest(os.path.join(cdir, "write", "*", "*counter_collection.csv"))
@@ -245,7 +248,14 @@ def reconcile(cdir, rtag):
     mt = _newest(os.path.join(cdir, "mfma", "*", "*kernel_trace.csv"))
     if mf:
         res.update(mfma_busy(mf, mt, hot))
-        busy_identity(res, f_launch, spl)
+        if rf.get("peak_basis"):
+            # mixed bf16 (32-cycle) and fp32 (64-cycle) MFMAs: the busy fraction stands, the
+            # fp32-only issue count and identity do not apply
+            res["mfma_issue_frac"] = None
+            res["mfma_identity"] = {"note": "split-MFMA kernel (bf16 32x32x16 + fp32 32x32x2): the busy fraction "
+                                            "counts both; frac is against the bf16 peak / 6 (bench peak_basis)"}
+        else:
+            busy_identity(res, f_launch, spl)
     out = os.path.join(ROOT, "profiles", f"{rtag}_{name}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
