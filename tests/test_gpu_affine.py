@@ -308,7 +308,7 @@ def test_split_mfma_fallback_is_per_tile(cuda_device):
     other tile of the same 64-row unit included — are bit-identical to a clean batch, and the
     tile's finite rows stay within the oracle's tolerance."""
     m, _ = realnvp_from_golden(cuda_device)
-    layer = m.flows[0]
+    layer = m.flow.flows[0]
     B = 1 << 17
     x = torch.randn(B, 2, generator=torch.Generator().manual_seed(7)).to(cuda_device)
     xb = x.clone()

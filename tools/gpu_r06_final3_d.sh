@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6 rebuild: the default bench line (as the driver runs it) and the --gpus 2 launcher rehearsal
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r06final2_bench; mkdir -p $O; cd $R
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r06final3_bench; mkdir -p $O; cd $R
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/default.json 2> $O/default.err || exit $?
 NFX_BENCH_REHEARSE=1 timeout -k 10 300 python3 bench.py --gpus 2 --config cfg2 --steps 10 --warmup 3 --no-cpu > $O/gpus2_rehearse.json 2> $O/gpus2_rehearse.err || exit $?
 timeout -k 10 300 python3 bench.py --config cfg5i --batch 1024 --steps 20 --warmup 5 --no-cpu > $O/cfg5i_1024.json 2> $O/cfg5i_1024.err || exit $?
