@@ -751,6 +751,10 @@ def run_config(config, a, world, rank, dev, strong, graph, with_cpu):
         rocprof["kernel_ms_over_this_step"] = rocprof["kernel_ms_per_step"] / result["ms_per_step"]
         rocprof["frac_rel_diff_vs_events"] = abs(rocprof["frac"] - result["roofline"]["frac"]) / result["roofline"]["frac"]
     if config in SPLIT_CONFIGS:
+        result["dtype_note"] = ("fp32 in, out and accumulate; layer 2 of each conditioner net multiplies as bf16 "
+                                "piece products (each exact in fp32, six per fp32 multiply-add, dropped terms below "
+                                "2^-25): vs the fp32 chain max |dz|/(1+|z|) 1.0e-6, mean dlogp 4.7e-9 at 1M rows "
+                                "(tools/split_precision.py, profiles/r06_split/); nll_f64 vs the reference above")
         result["roofline"].update({
             "peak_basis": ("bf16 MFMA peak / 6: layer 2 of every conditioner net runs as six bf16 piece products "
                            "per fp32 multiply-add (v_mfma_f32_32x32x16_bf16, fp32 accumulate; fp32-accurate, not the "
